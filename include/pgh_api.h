@@ -1,0 +1,133 @@
+/* libpygrid_hip -- C ABI of the MI355X (gfx950) aggregation engine behind PyGrid Node's
+ * model-centric cycle close.
+ *
+ * What it replaces (reference = /root/reference, read-only):
+ *   CycleManager._average_plan_diffs, apps/node/src/app/main/model_centric/cycles/
+ *   cycle_manager.py:219-323, the slice :240-303 -- checkpoint unserialize (:240), per-diff
+ *   unserialize (:247-250), hosted iterative avg plan (:266-269), hard-coded mean
+ *   (:276-288), apply (:293-296) -- plus the PySyft 0.2.9 Z_2^64 share sum + fixed-point
+ *   decode exercised by tests/data_centric/test_basic_syft_operations.py:388-454.
+ *   The reference has no FFI of its own; this ABI is what a ctypes binding in the node
+ *   process binds (INTEGRATION.md shows the stub).
+ *
+ * Conventions: every int-returning entry point returns PGH_OK (0) or a negative pgh_status;
+ * pgh_last_error() then holds the message.  Plain pointers and sizes only.  Host buffers
+ * passed in are borrowed for the duration of the call.  A context is single-owner and not
+ * re-entrant (the reference serialises cycle close with run_task_once,
+ * apps/node/src/app/main/model_centric/tasks/cycle.py:9-25).  One context drives one GPU;
+ * multi-GPU runs one process (and one context) per GPU, each owning a parameter shard.
+ */
+#ifndef PGH_API_H
+#define PGH_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGH_ABI_VERSION 1
+
+typedef struct pgh_ctx pgh_ctx;
+
+typedef enum {
+    PGH_OK = 0,
+    PGH_E_ARG = -1,        /* bad argument (null, size mismatch, out of range) */
+    PGH_E_HIP = -2,        /* HIP runtime / kernel launch error */
+    PGH_E_STATE = -3,      /* call order / missing clients / layout not set */
+    PGH_E_OOM = -4,        /* device or pinned allocation failed */
+    PGH_E_PARSE = -5,      /* malformed State protobuf bytes */
+    PGH_E_UNSUPPORTED = -6
+} pgh_status;
+
+/* Averaging mode.  PGH_MEAN: hard-coded path, cycle_manager.py:276-288.
+ * PGH_ITERATIVE_MEAN: hosted iterative avg_plan, cycle_manager.py:266-269 with the plan of
+ * examples/model-centric/01-Create-plan.ipynb:450-454.  PGH_WEIGHTED_MEAN: north_star's
+ * weighted FedAvg (no reference counterpart; equals PGH_MEAN bit for bit at w == 1). */
+typedef enum { PGH_MEAN = 0, PGH_ITERATIVE_MEAN = 1, PGH_WEIGHTED_MEAN = 2 } pgh_mode;
+
+typedef enum { PGH_F32 = 0, PGH_I64 = 1 } pgh_dtype;
+
+typedef struct {
+    double kernel_ms_last;     /* duration of the last reduction kernel (HIP events) */
+    double kernel_ms_total;    /* sum over timed launches since the last reset */
+    uint64_t kernel_launches;  /* timed launches since the last reset */
+    uint64_t kernel_bytes_last;/* algorithmic bytes of the last reduction launch */
+    double h2d_ms_total;       /* ingest wall time (host buffer -> HBM), ms */
+    uint64_t h2d_bytes_total;  /* bytes moved host -> HBM by ingest */
+    double close_ms_last;      /* wall time of the last pgh_fedavg / pgh_secagg (host in/out) */
+    int64_t p_shard;           /* params in this context's shard */
+    int64_t ld;                /* slab row stride (elements) */
+    int32_t n_clients;         /* clients ingested (contiguous from 0) */
+    int32_t max_clients;       /* slab capacity */
+} pgh_stats_t;
+
+/* ---- context lifecycle ------------------------------------------------------------------ */
+int pgh_abi_version(void);
+int pgh_device_count(int* n);
+/* Bind a context to GPU `device`, with a pinned host staging ring of `pinned_bytes` total
+ * (0 = default 256 MiB, split into 2 slots). */
+int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out);
+void pgh_destroy(pgh_ctx* ctx);
+const char* pgh_last_error(const pgh_ctx* ctx);   /* ctx may be NULL (creation errors) */
+
+/* ---- layout ------------------------------------------------------------------------------
+ * Flat parameter vector = tensors concatenated in State order
+ * (model_manager.py:94-103 state.tensors()); P = sum(numel). */
+int pgh_set_layout(pgh_ctx* ctx, int n_tensors, const int64_t* numel);
+/* Restrict this context to the flat range [lo, hi) (param-axis shard).  Default: [0, P). */
+int pgh_set_shard(pgh_ctx* ctx, int64_t lo, int64_t hi);
+/* Allocate the HBM slab: max_clients rows of the shard, dtype PGH_F32 (fp32 diffs) or
+ * PGH_I64 (n_parties int64 shares per client).  Forgets previously ingested clients. */
+int pgh_reserve(pgh_ctx* ctx, int max_clients, int dtype, int n_parties);
+/* Forget ingested clients and weights (start of a new cycle); keeps allocations. */
+int pgh_reset(pgh_ctx* ctx);
+
+/* ---- ingest (the diffs of cycle_manager.py:243-250) -------------------------------------- */
+/* Client `client`'s already-decoded flat diff.  PGH_F32: `flat` holds P float32 (the whole
+ * model; the shard slice is taken).  PGH_I64: n_parties x P int64 shares, party-major.
+ * Copied via the pinned ring into slab row `client` with hipMemcpyAsync. */
+int pgh_ingest_raw(pgh_ctx* ctx, int client, const void* flat, size_t nbytes, int dtype);
+/* Client diff as syft State protobuf bytes (model_manager.py:94-103 wire format, build-owned
+ * schema restatement: DESIGN.md "State codec"); fp32 tensors only. */
+int pgh_ingest_state(pgh_ctx* ctx, int client, const uint8_t* pb, size_t n);
+/* Fill slab rows [0, n_clients) with the deterministic synthetic diffs (or shares) of
+ * SURVEY.md 8(d) for this shard, generated on the GPU (oracle/oracle.py restates them). */
+int pgh_synth_fill(pgh_ctx* ctx, uint64_t seed, int n_clients);
+/* Per-client weights for PGH_WEIGHTED_MEAN (n == clients ingested at reduction time). */
+int pgh_set_weights(pgh_ctx* ctx, const float* w, int n);
+
+/* ---- reduction ----------------------------------------------------------------------------
+ * out = ckpt - avg(diffs), over this context's shard.  Host pointers, P_shard floats each. */
+int pgh_fedavg(pgh_ctx* ctx, int mode, const float* ckpt, float* out);
+/* Same with device pointers (16-byte aligned, P_shard floats) on caller stream `stream`
+ * (a hipStream_t; NULL = the context's own stream).  Nothing is copied to the host. */
+int pgh_fedavg_device(pgh_ctx* ctx, int mode, const float* d_ckpt, float* d_out, void* stream);
+/* Z_2^64 share sum over all clients x parties, then decode float32(sum) / base**prec.
+ * sum_out (int64) and dec_out (float32) are host arrays of P_shard; either may be NULL. */
+int pgh_secagg(pgh_ctx* ctx, int base, int prec, int64_t* sum_out, float* dec_out);
+int pgh_secagg_device(pgh_ctx* ctx, int base, int prec, int64_t* d_sum, float* d_dec, void* stream);
+/* Fill a device buffer with the synthetic checkpoint of this shard (P_shard floats). */
+int pgh_synth_ckpt_device(pgh_ctx* ctx, uint64_t seed, float* d_ckpt, void* stream);
+
+/* ---- tuning and observability -------------------------------------------------------------- */
+int pgh_set_variant(pgh_ctx* ctx, int variant);   /* kernel variant, for A/B measurement */
+int pgh_stats(pgh_ctx* ctx, pgh_stats_t* out);     /* synchronises pending timing events */
+int pgh_reset_stats(pgh_ctx* ctx);
+/* Device pointer of the slab and its row stride, for callers that drive the kernels. */
+int pgh_slab(pgh_ctx* ctx, void** d_slab, int64_t* ld);
+
+/* ---- State codec (host only; replaces syft serde at model_manager.py:79-103) ------------- */
+/* Locate each tensor's packed float32 payload in a State message: byte offset and element
+ * count, State order.  Up to `cap` entries are written; *n_tensors = tensors found. */
+int pgh_state_scan(const uint8_t* pb, size_t n, int cap, int64_t* offsets, int64_t* counts, int* n_tensors);
+/* New checkpoint (serialize_model_params, model_manager.py:79-92, as used at
+ * cycle_manager.py:303): `tmpl` with every payload overwritten by `values` (P floats).  `out`
+ * has n bytes; out == tmpl patches in place. */
+int pgh_state_patch(const uint8_t* tmpl, size_t n, const float* values, int64_t n_values, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PGH_API_H */

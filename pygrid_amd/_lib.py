@@ -1,0 +1,90 @@
+"""ctypes binding of libpygrid_hip.so (the C ABI of ``include/pgh_api.h``).
+
+``ctypes.CDLL`` releases the GIL around every call, so a cycle close on the node's
+Flask-Executor thread (``apps/node/src/app/__init__.py:29,197-199``) does not block the
+request threads.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+from .exceptions import EngineUnavailableError
+
+LIB_PATH = Path(__file__).resolve().with_name("libpygrid_hip.so")
+
+PGH_OK = 0
+STATUS_NAMES = {-1: "PGH_E_ARG", -2: "PGH_E_HIP", -3: "PGH_E_STATE", -4: "PGH_E_OOM",
+                -5: "PGH_E_PARSE", -6: "PGH_E_UNSUPPORTED"}
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("kernel_ms_last", C.c_double),
+        ("kernel_ms_total", C.c_double),
+        ("kernel_launches", C.c_uint64),
+        ("kernel_bytes_last", C.c_uint64),
+        ("h2d_ms_total", C.c_double),
+        ("h2d_bytes_total", C.c_uint64),
+        ("close_ms_last", C.c_double),
+        ("p_shard", C.c_int64),
+        ("ld", C.c_int64),
+        ("n_clients", C.c_int32),
+        ("max_clients", C.c_int32),
+    ]
+
+
+_vp, _i, _i64, _u64, _sz = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_size_t
+_P64 = C.POINTER(C.c_int64)
+
+# name -> (restype, argtypes); every entry point declared in include/pgh_api.h
+SIGNATURES = {
+    "pgh_abi_version": (_i, []),
+    "pgh_device_count": (_i, [C.POINTER(C.c_int)]),
+    "pgh_create": (_i, [_i, _sz, C.POINTER(_vp)]),
+    "pgh_destroy": (None, [_vp]),
+    "pgh_last_error": (C.c_char_p, [_vp]),
+    "pgh_set_layout": (_i, [_vp, _i, _P64]),
+    "pgh_set_shard": (_i, [_vp, _i64, _i64]),
+    "pgh_reserve": (_i, [_vp, _i, _i, _i]),
+    "pgh_reset": (_i, [_vp]),
+    "pgh_ingest_raw": (_i, [_vp, _i, _vp, _sz, _i]),
+    "pgh_ingest_state": (_i, [_vp, _i, C.c_char_p, _sz]),
+    "pgh_synth_fill": (_i, [_vp, _u64, _i]),
+    "pgh_set_weights": (_i, [_vp, C.POINTER(C.c_float), _i]),
+    "pgh_fedavg": (_i, [_vp, _i, _vp, _vp]),
+    "pgh_fedavg_device": (_i, [_vp, _i, _vp, _vp, _vp]),
+    "pgh_secagg": (_i, [_vp, _i, _i, _vp, _vp]),
+    "pgh_secagg_device": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
+    "pgh_synth_ckpt_device": (_i, [_vp, _u64, _vp, _vp]),
+    "pgh_set_variant": (_i, [_vp, _i]),
+    "pgh_stats": (_i, [_vp, C.POINTER(Stats)]),
+    "pgh_reset_stats": (_i, [_vp]),
+    "pgh_slab": (_i, [_vp, C.POINTER(_vp), _P64]),
+    "pgh_state_scan": (_i, [C.c_char_p, _sz, _i, _P64, _P64, C.POINTER(C.c_int)]),
+    "pgh_state_patch": (_i, [C.c_char_p, _sz, _vp, _i64, _vp]),
+}
+
+_LIB = None
+
+
+def load() -> C.CDLL:
+    """Load the library (once).  Raises EngineUnavailableError if it has not been built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    try:  # torch bundles libamdhip64.so.7 under the same soname: load it first so that one
+        import torch  # noqa: F401  HIP runtime serves torch's allocations and ours
+    except ImportError:
+        pass
+    if not LIB_PATH.exists():
+        raise EngineUnavailableError(
+            f"{LIB_PATH.name} is not built (run `python -m pygrid_amd.build`); "
+            "the aggregation engine has no CPU fallback")
+    lib = C.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib

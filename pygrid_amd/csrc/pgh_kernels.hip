@@ -1,0 +1,299 @@
+// gfx950 (CDNA4, MI355X) kernels for the PyGrid cycle-close aggregation path.
+//
+// K1  k_fedavg<MODE_MEAN>      out = ckpt - (((d0 + d1) + d2) + ...) / N
+//       restates cycle_manager.py:276-296 (reduce(th.add) -> th.div(., N) -> subtract)
+//     k_fedavg<MODE_WEIGHTED>  out = ckpt - (sum_c w_c*d_c) / (sum_c w_c)   (build-owned)
+// K2  k_fedavg<MODE_ITERATIVE> a = d0; a = (a*k + d_k)/(k+1); out = ckpt - a
+//       restates cycle_manager.py:266-269 + 01-Create-plan.ipynb:450-454
+// K3  k_secagg                 Z_2^64 wrap-sum over [clients*parties][P] int64 + fixed-point
+//       decode float32(int64)/10^prec (PySyft 0.2.9 semantics)
+//
+// Design (DESIGN.md "Kernels"): every kernel is a single streaming pass over a row-major
+// [rows][ld] slab held in HBM.  Parallelism is over the PARAMETER axis only: one lane owns a
+// 16-byte column (4 fp32 or 2 int64) and walks the client rows in index order, so the fp32
+// fold order is exactly the reference's left fold (bit-exact, no tree/shuffle reordering).
+// A wave reads 1 KiB contiguous per row; U rows are issued before they are consumed to keep
+// U x 1 KiB per wave in flight.  No LDS: there is no reuse to stage, and no MFMA: this is a
+// 0.25 flop/byte reduction, bound by HBM bandwidth.
+//
+// Build flags matter for parity: -ffp-contract=off (no a*k+d -> FMA), no fast-math, f32
+// denormals kept, IEEE (correctly rounded) f32 division.
+#include "pgh_kernels.h"
+
+namespace pgh {
+namespace {
+
+constexpr int BLOCK = 256;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint64_t sm64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t row_key(uint64_t seed, uint64_t stream, uint64_t row) {
+    return sm64(sm64(seed ^ (stream << 48)) ^ (row * 0xD1B54A32D192ED03ull));
+}
+
+__device__ __forceinline__ float bits_to_f32(uint64_t b, float scale) {
+    const uint32_t s = (uint32_t)(b & 0xFFFF) + (uint32_t)((b >> 16) & 0xFFFF) +
+                       (uint32_t)((b >> 32) & 0xFFFF) + (uint32_t)(b >> 48);
+    return (float)((int32_t)s - 131070) * scale;  // exact convert, one rounded multiply
+}
+
+template <bool NT>
+__device__ __forceinline__ f32x4 ld4(const float* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    else return *reinterpret_cast<const f32x4*>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ u64x2 ld2u(const int64_t* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(p));
+    else return *reinterpret_cast<const u64x2*>(p);
+}
+
+// [p]-sized vectors (acc, ckpt, out) may end mid-column: the last column goes scalar.
+__device__ __forceinline__ f32x4 ld4_tail(const float* base, int64_t q, int64_t p) {
+    const int64_t i = 4 * q;
+    if (i + 4 <= p) return *reinterpret_cast<const f32x4*>(base + i);
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    for (int e = 0; e < 4; ++e)
+        if (i + e < p) v[e] = base[i + e];
+    return v;
+}
+
+__device__ __forceinline__ void st4_tail(float* base, int64_t q, int64_t p, f32x4 v) {
+    const int64_t i = 4 * q;
+    if (i + 4 <= p) { *reinterpret_cast<f32x4*>(base + i) = v; return; }
+    for (int e = 0; e < 4; ++e)
+        if (i + e < p) base[i + e] = v[e];
+}
+
+template <int MODE>
+__device__ __forceinline__ f32x4 fold(f32x4 acc, f32x4 v, int64_t k, const float* w, int r) {
+    if constexpr (MODE == MODE_MEAN) {
+        return acc + v;                                   // th.add, cycle_manager.py:286
+    } else if constexpr (MODE == MODE_WEIGHTED) {
+        return acc + v * w[r];                            // product rounded, then add
+    } else {
+        const float kf = (float)k, kf1 = (float)(k + 1);  // th.tensor([k]) promoted to f32
+        return (acc * kf + v) / kf1;                      // 01-Create-plan.ipynb:453
+    }
+}
+
+// One 16-byte column: 4 consecutive params of the shard, all rows of the chunk, in order.
+template <int MODE, int U, bool NT>
+__device__ __forceinline__ void fedavg_column(const FedavgArgs& a, int64_t q) {
+    const float* col = a.diffs + 4 * q;
+    const int n = a.n_rows;
+    f32x4 acc;
+    int r;
+    if (a.flags & FL_FIRST) {
+        acc = ld4<NT>(col);                                    // fold starts at d0, not 0
+        if constexpr (MODE == MODE_WEIGHTED) acc = acc * a.weights[0];
+        r = 1;
+    } else {
+        acc = ld4_tail(a.acc, q, a.p);
+        r = 0;
+    }
+    for (; r + U <= n; r += U) {
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ld4<NT>(col + (size_t)(r + u) * a.ld);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = fold<MODE>(acc, v[u], a.client0 + r + u, a.weights, r + u);
+    }
+    for (; r < n; ++r) acc = fold<MODE>(acc, ld4<NT>(col + (size_t)r * a.ld), a.client0 + r, a.weights, r);
+
+    if (a.flags & FL_FINAL) {
+        const f32x4 avg = (MODE == MODE_ITERATIVE) ? acc : acc / a.divisor;  // th.div, :288
+        st4_tail(a.out, q, a.p, ld4_tail(a.ckpt, q, a.p) - avg);             // :293-296
+    } else {
+        st4_tail(a.acc, q, a.p, acc);
+    }
+}
+
+template <int MODE, int U, bool NT>
+__global__ __launch_bounds__(BLOCK) void k_fedavg(FedavgArgs a, int64_t ncol) {
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < ncol; q += stride)
+        fedavg_column<MODE, U, NT>(a, q);
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(BLOCK) void k_secagg(SecaggArgs a, int64_t ncol) {
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < ncol; q += stride) {
+        const int64_t* col = a.shares + 2 * q;
+        const int64_t i = 2 * q;
+        const bool full = i + 2 <= a.p;
+        u64x2 acc = {0ull, 0ull};
+        if (!(a.flags & FL_FIRST)) {
+            acc[0] = a.acc[i];
+            if (full) acc[1] = a.acc[i + 1];
+        }
+        int r = 0;
+        for (; r + U <= a.n_rows; r += U) {
+            u64x2 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = ld2u<NT>(col + (size_t)(r + u) * a.ld);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += v[u];     // wraps mod 2^64
+        }
+        for (; r < a.n_rows; ++r) acc += ld2u<NT>(col + (size_t)r * a.ld);
+        if (a.flags & FL_FINAL) {
+            for (int e = 0; e < 2; ++e) {
+                if (e == 1 && !full) break;
+                if (a.sum_out) a.sum_out[i + e] = (int64_t)acc[e];
+                if (a.dec_out) a.dec_out[i + e] = (float)(int64_t)acc[e] / a.divisor;
+            }
+        } else {
+            a.acc[i] = acc[0];
+            if (full) a.acc[i + 1] = acc[1];
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_synth_f32(float* out, int64_t ld, int64_t p, uint64_t seed,
+                                                     uint64_t stream_id, int64_t row0, int64_t idx0,
+                                                     float scale) {
+    const int64_t r = blockIdx.y;
+    const uint64_t key = row_key(seed, stream_id, (uint64_t)(row0 + r));
+    float* row = out + (size_t)r * ld;
+    const int64_t ncol = ld / 4;
+    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < ncol; q += (int64_t)gridDim.x * BLOCK) {
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t i = 4 * q + e;
+            v[e] = (i < p) ? bits_to_f32(sm64(key + (uint64_t)(idx0 + i)), scale) : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(row + 4 * q) = v;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_synth_shares(int64_t* out, int n_parties, int64_t ld, int64_t p,
+                                                        uint64_t seed, int64_t client0, int64_t idx0,
+                                                        float enc_scale) {
+    const int64_t c = blockIdx.y;
+    const uint64_t kx = row_key(seed, STREAM_SECRET, (uint64_t)(client0 + c));
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < ld; i += (int64_t)gridDim.x * BLOCK) {
+        int64_t* dst = out + (size_t)(c * n_parties) * ld + i;
+        if (i >= p) {
+            for (int s = 0; s < n_parties; ++s) dst[(size_t)s * ld] = 0;
+            continue;
+        }
+        const uint64_t g = (uint64_t)(idx0 + i);
+        const float x = bits_to_f32(sm64(kx + g), DIFF_SCALE);
+        const float y = x * enc_scale;                  // fix_prec: x * base**prec in f32
+        const uint64_t enc = (uint64_t)(int64_t)y;      // .long(): truncation toward zero
+        uint64_t acc = 0;
+        for (int s = 0; s < n_parties - 1; ++s) {
+            const uint64_t sh = sm64(row_key(seed, STREAM_SHARE, (uint64_t)((client0 + c) * n_parties + s)) + g);
+            dst[(size_t)s * ld] = (int64_t)sh;
+            acc += sh;
+        }
+        dst[(size_t)(n_parties - 1) * ld] = (int64_t)(enc - acc);
+    }
+}
+
+int cu_count() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cached[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cached[dev] = n;
+    }
+    return cached[dev];
+}
+
+// Grid: variant 0 = one column per lane (grid covers every column once); variant 1 =
+// persistent grid of 4 blocks per CU striding over columns; variants 2/3 = the same two with
+// non-temporal (nt) loads for the once-read diff stream.
+inline unsigned grid_for(int64_t ncol, int variant) {
+    const int64_t full = (ncol + BLOCK - 1) / BLOCK;
+    if ((variant & 1) == 0) return (unsigned)(full > 0 ? full : 1);
+    const int64_t pers = (int64_t)cu_count() * 4;
+    return (unsigned)(full < pers ? (full > 0 ? full : 1) : pers);
+}
+
+template <int MODE>
+hipError_t dispatch_fedavg(const FedavgArgs& a, int64_t ncol, hipStream_t s) {
+    const unsigned g = grid_for(ncol, a.variant);
+    switch (a.variant) {
+    case 0: case 1: k_fedavg<MODE, 8, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 2: case 3: k_fedavg<MODE, 8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 4: case 5: k_fedavg<MODE, 16, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
+    if (a.p <= 0 || a.n_rows < 0 || a.ld < a.p || (a.ld & 3)) return hipErrorInvalidValue;
+    if ((a.flags & FL_FIRST) && a.n_rows < 1) return hipErrorInvalidValue;
+    if (a.n_rows > 0 && (!a.diffs || (reinterpret_cast<uintptr_t>(a.diffs) & 15))) return hipErrorInvalidValue;
+    if (!(a.flags & FL_FIRST) && (!a.acc || (reinterpret_cast<uintptr_t>(a.acc) & 15))) return hipErrorInvalidValue;
+    if (!(a.flags & FL_FINAL) && (!a.acc || (reinterpret_cast<uintptr_t>(a.acc) & 15))) return hipErrorInvalidValue;
+    if ((a.flags & FL_FINAL) && (!a.ckpt || !a.out || (reinterpret_cast<uintptr_t>(a.ckpt) & 15) ||
+                                 (reinterpret_cast<uintptr_t>(a.out) & 15)))
+        return hipErrorInvalidValue;
+    if (a.mode == MODE_WEIGHTED && a.n_rows > 0 && !a.weights) return hipErrorInvalidValue;
+    const int64_t ncol = (a.p + 3) / 4;
+    switch (a.mode) {
+    case MODE_MEAN: return dispatch_fedavg<MODE_MEAN>(a, ncol, s);
+    case MODE_ITERATIVE: return dispatch_fedavg<MODE_ITERATIVE>(a, ncol, s);
+    case MODE_WEIGHTED: return dispatch_fedavg<MODE_WEIGHTED>(a, ncol, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s) {
+    if (a.p <= 0 || a.n_rows < 0 || a.ld < a.p || (a.ld & 1)) return hipErrorInvalidValue;
+    if (a.n_rows > 0 && (!a.shares || (reinterpret_cast<uintptr_t>(a.shares) & 15))) return hipErrorInvalidValue;
+    if (!(a.flags & FL_FINAL) && !a.acc) return hipErrorInvalidValue;
+    if (!(a.flags & FL_FIRST) && !a.acc) return hipErrorInvalidValue;
+    const int64_t ncol = (a.p + 1) / 2;
+    const unsigned g = grid_for(ncol, a.variant);
+    switch (a.variant) {
+    case 0: case 1: k_secagg<8, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 2: case 3: k_secagg<8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 4: case 5: k_secagg<16, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_f32(float* out, int n_rows, int64_t ld, int64_t p, uint64_t seed, uint64_t stream_id,
+                            int64_t row0, int64_t idx0, float scale, hipStream_t s) {
+    if (!out || n_rows < 0 || n_rows > 65535 || ld < p || (ld & 3) || (reinterpret_cast<uintptr_t>(out) & 15))
+        return hipErrorInvalidValue;
+    if (n_rows == 0 || ld == 0) return hipSuccess;
+    const int64_t ncol = ld / 4;
+    int64_t gx = (ncol + BLOCK - 1) / BLOCK;
+    if (gx > 1024) gx = 1024;
+    k_synth_f32<<<dim3((unsigned)gx, (unsigned)n_rows), BLOCK, 0, s>>>(out, ld, p, seed, stream_id, row0, idx0, scale);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_shares(int64_t* out, int n_clients, int n_parties, int64_t ld, int64_t p, uint64_t seed,
+                               int64_t client0, int64_t idx0, float enc_scale, hipStream_t s) {
+    if (!out || n_clients < 0 || n_clients > 65535 || n_parties < 1 || ld < p) return hipErrorInvalidValue;
+    if (n_clients == 0 || ld == 0) return hipSuccess;
+    int64_t gx = (ld + BLOCK - 1) / BLOCK;
+    if (gx > 1024) gx = 1024;
+    k_synth_shares<<<dim3((unsigned)gx, (unsigned)n_clients), BLOCK, 0, s>>>(out, n_parties, ld, p, seed, client0,
+                                                                            idx0, enc_scale);
+    return hipGetLastError();
+}
+
+}  // namespace pgh

@@ -1,0 +1,266 @@
+// Protobuf wire walker for the syft State message (see pgh_state.h for the schema caveat).
+#include "pgh_state.h"
+
+#include <cstring>
+
+#include "../../include/pgh_api.h"
+
+namespace pgh_state {
+namespace {
+
+struct Reader {
+    const uint8_t* p;
+    const uint8_t* end;
+    bool ok = true;
+
+    bool varint(uint64_t* v) {
+        uint64_t x = 0;
+        for (int shift = 0; shift < 64; shift += 7) {
+            if (p >= end) return ok = false;
+            const uint8_t b = *p++;
+            x |= (uint64_t)(b & 0x7F) << shift;
+            if (!(b & 0x80)) { *v = x; return true; }
+        }
+        return ok = false;
+    }
+    // Skip one field of wire type wt.
+    bool skip(uint32_t wt) {
+        uint64_t v;
+        switch (wt) {
+        case 0: return varint(&v);
+        case 1: if (end - p < 8) return ok = false; p += 8; return true;
+        case 2: if (!varint(&v) || (uint64_t)(end - p) < v) return ok = false; p += v; return true;
+        case 5: if (end - p < 4) return ok = false; p += 4; return true;
+        default: return ok = false;  // groups (3/4) are not used by proto3
+        }
+    }
+    bool len_delim(const uint8_t** b, const uint8_t** e) {
+        uint64_t v;
+        if (!varint(&v) || (uint64_t)(end - p) < v) return ok = false;
+        *b = p;
+        *e = p + v;
+        p += v;
+        return true;
+    }
+};
+
+// Walk a message; call f(field, wiretype, reader) for each field; f must consume the value.
+template <class F>
+bool each_field(const uint8_t* b, const uint8_t* e, F&& f) {
+    Reader r{b, e};
+    while (r.p < r.end) {
+        uint64_t key;
+        if (!r.varint(&key)) return false;
+        const uint32_t field = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+        if (field == 0) return false;
+        if (!f(field, wt, r)) return false;
+    }
+    return r.ok;
+}
+
+bool parse_size(const uint8_t* b, const uint8_t* e, std::vector<int64_t>* dims) {
+    return each_field(b, e, [&](uint32_t f, uint32_t wt, Reader& r) {
+        if (f == SIZE_DIMS && wt == 2) {  // packed int32
+            const uint8_t *pb, *pe;
+            if (!r.len_delim(&pb, &pe)) return false;
+            Reader q{pb, pe};
+            while (q.p < q.end) {
+                uint64_t v;
+                if (!q.varint(&v)) return false;
+                dims->push_back((int64_t)(int32_t)(uint32_t)v);
+            }
+            return true;
+        }
+        if (f == SIZE_DIMS && wt == 0) {
+            uint64_t v;
+            if (!r.varint(&v)) return false;
+            dims->push_back((int64_t)(int32_t)(uint32_t)v);
+            return true;
+        }
+        return r.skip(wt);
+    });
+}
+
+bool parse_tensor_data(const uint8_t* base, const uint8_t* b, const uint8_t* e, Span* s, std::string* msg) {
+    bool have_f32 = false;
+    bool ok = each_field(b, e, [&](uint32_t f, uint32_t wt, Reader& r) {
+        const uint8_t *pb, *pe;
+        if (f == TD_SHAPE && wt == 2) {
+            if (!r.len_delim(&pb, &pe)) return false;
+            s->shape.clear();
+            return parse_size(pb, pe, &s->shape);
+        }
+        if (f == TD_DTYPE && wt == 2) {
+            if (!r.len_delim(&pb, &pe)) return false;
+            s->dtype.assign((const char*)pb, (size_t)(pe - pb));
+            return true;
+        }
+        if (f == TD_F32) {
+            if (wt != 2) { *msg = "unpacked float32 payload is not supported"; return false; }
+            if (have_f32) { *msg = "float32 payload split over several fields"; return false; }
+            if (!r.len_delim(&pb, &pe)) return false;
+            if ((pe - pb) % 4) { *msg = "float32 payload length is not a multiple of 4"; return false; }
+            s->offset = (size_t)(pb - base);
+            s->count = (pe - pb) / 4;
+            have_f32 = true;
+            return true;
+        }
+        return r.skip(wt);
+    });
+    if (ok && !have_f32) {
+        // proto3 omits an empty packed field: a zero-element tensor has no payload
+        int64_t numel = 1;
+        for (auto d : s->shape) numel *= d;
+        if (s->shape.empty() || numel != 0) { *msg = "tensor has no float32 payload (dtype '" + s->dtype + "')"; return false; }
+        s->offset = (size_t)(e - base);
+        s->count = 0;
+    }
+    return ok;
+}
+
+bool parse_torch_tensor(const uint8_t* base, const uint8_t* b, const uint8_t* e, Span* s, std::string* msg) {
+    bool found = false;
+    bool ok = each_field(b, e, [&](uint32_t f, uint32_t wt, Reader& r) {
+        if (f == TORCH_CONTENTS_DATA && wt == 2) {
+            const uint8_t *pb, *pe;
+            if (!r.len_delim(&pb, &pe)) return false;
+            found = true;
+            return parse_tensor_data(base, pb, pe, s, msg);
+        }
+        return r.skip(wt);
+    });
+    if (ok && !found) { if (msg->empty()) *msg = "TorchTensor without contents_data (binary serializer?)"; return false; }
+    return ok;
+}
+
+bool parse_state_tensor(const uint8_t* base, const uint8_t* b, const uint8_t* e, Span* s, std::string* msg) {
+    bool found = false;
+    bool ok = each_field(b, e, [&](uint32_t f, uint32_t wt, Reader& r) {
+        const uint8_t *pb, *pe;
+        if (f == STATETENSOR_TORCH && wt == 2) {
+            if (!r.len_delim(&pb, &pe)) return false;
+            found = true;
+            return parse_torch_tensor(base, pb, pe, s, msg);
+        }
+        if (f == STATETENSOR_PARAM && wt == 2) {
+            if (!r.len_delim(&pb, &pe)) return false;
+            return each_field(pb, pe, [&](uint32_t f2, uint32_t wt2, Reader& r2) {
+                if (f2 == PARAM_TENSOR && wt2 == 2) {
+                    const uint8_t *qb, *qe;
+                    if (!r2.len_delim(&qb, &qe)) return false;
+                    found = true;
+                    return parse_torch_tensor(base, qb, qe, s, msg);
+                }
+                return r2.skip(wt2);
+            });
+        }
+        return r.skip(wt);
+    });
+    if (ok && !found) { if (msg->empty()) *msg = "StateTensor holds neither torch_tensor nor torch_param"; return false; }
+    return ok;
+}
+
+}  // namespace
+
+int scan(const uint8_t* pb, size_t n, std::vector<Span>* spans, std::string* msg) {
+    spans->clear();
+    msg->clear();
+    if (!pb && n) { *msg = "null buffer"; return PGH_E_PARSE; }
+    const uint8_t* base = pb;
+    bool ok = each_field(pb, pb + n, [&](uint32_t f, uint32_t wt, Reader& r) {
+        if (f == STATE_TENSORS && wt == 2) {
+            const uint8_t *b, *e;
+            if (!r.len_delim(&b, &e)) return false;
+            Span s;
+            if (!parse_state_tensor(base, b, e, &s, msg)) return false;
+            spans->push_back(std::move(s));
+            return true;
+        }
+        return r.skip(wt);
+    });
+    if (!ok) {
+        if (msg->empty()) *msg = "truncated or malformed protobuf";
+        return PGH_E_PARSE;
+    }
+    for (size_t t = 0; t < spans->size(); ++t) {
+        const Span& s = (*spans)[t];
+        int64_t numel = 1;
+        for (auto d : s.shape) {
+            if (d < 0) { *msg = "negative dimension in tensor " + std::to_string(t); return PGH_E_PARSE; }
+            numel *= d;
+        }
+        if (!s.shape.empty() && numel != s.count) {
+            *msg = "tensor " + std::to_string(t) + ": shape holds " + std::to_string(numel) + " elements, payload " +
+                   std::to_string(s.count);
+            return PGH_E_PARSE;
+        }
+        if (!s.dtype.empty() && s.dtype != "float32" && s.dtype != "torch.float32") {
+            *msg = "tensor " + std::to_string(t) + " has dtype '" + s.dtype + "', expected float32";
+            return PGH_E_PARSE;
+        }
+    }
+    return 0;
+}
+
+int decode_f32(const uint8_t* pb, size_t n, const std::vector<int64_t>& numel, float* out, std::string* msg) {
+    std::vector<Span> spans;
+    int rc = scan(pb, n, &spans, msg);
+    if (rc) return rc;
+    if (spans.size() != numel.size()) {
+        *msg = "State holds " + std::to_string(spans.size()) + " tensors, layout has " + std::to_string(numel.size());
+        return PGH_E_PARSE;
+    }
+    size_t off = 0;
+    for (size_t t = 0; t < spans.size(); ++t) {
+        if (spans[t].count != numel[t]) {
+            *msg = "tensor " + std::to_string(t) + " holds " + std::to_string(spans[t].count) + " floats, layout " +
+                   std::to_string(numel[t]);
+            return PGH_E_PARSE;
+        }
+        std::memcpy(out + off, pb + spans[t].offset, 4 * (size_t)spans[t].count);  // little-endian fixed32
+        off += (size_t)spans[t].count;
+    }
+    return 0;
+}
+
+}  // namespace pgh_state
+
+// ---- C ABI for the codec (host only; used by the Python mirror of model_manager) ----------
+extern "C" {
+
+// Count tensors and fill up to `cap` entries of (payload byte offset, element count).
+int pgh_state_scan(const uint8_t* pb, size_t n, int cap, int64_t* offsets, int64_t* counts, int* n_tensors) {
+    if (!n_tensors) return PGH_E_ARG;
+    std::vector<pgh_state::Span> spans;
+    std::string msg;
+    int rc = pgh_state::scan(pb, n, &spans, &msg);
+    if (rc) return rc;
+    *n_tensors = (int)spans.size();
+    for (int t = 0; t < cap && t < (int)spans.size(); ++t) {
+        if (offsets) offsets[t] = (int64_t)spans[t].offset;
+        if (counts) counts[t] = spans[t].count;
+    }
+    return PGH_OK;
+}
+
+// New checkpoint bytes = `tmpl` (the current checkpoint) with every tensor payload replaced by
+// `values` (concatenated, P floats).  `out` has room for n bytes (the size never changes).
+int pgh_state_patch(const uint8_t* tmpl, size_t n, const float* values, int64_t n_values, uint8_t* out) {
+    if (!tmpl || !out || (!values && n_values)) return PGH_E_ARG;
+    std::vector<pgh_state::Span> spans;
+    std::string msg;
+    int rc = pgh_state::scan(tmpl, n, &spans, &msg);
+    if (rc) return rc;
+    int64_t total = 0;
+    for (auto& s : spans) total += s.count;
+    if (total != n_values) return PGH_E_ARG;
+    if (out != tmpl) std::memcpy(out, tmpl, n);
+    int64_t off = 0;
+    for (auto& s : spans) {
+        std::memcpy(out + s.offset, values + off, 4 * (size_t)s.count);
+        off += s.count;
+    }
+    return PGH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,193 @@
+"""Host-side mirror of PyGrid Node's cycle-close path, with the arithmetic on the GPU.
+
+Reference: ``CycleManager.complete_cycle`` / ``_average_plan_diffs``,
+``apps/node/src/app/main/model_centric/cycles/cycle_manager.py:180-323``.
+
+* ``ready_to_average`` restates the readiness predicate (``:196-210``).
+* ``select_mode`` is the dispatch rule: no hosted plan -> hard-coded mean
+  (``:273-288``); hosted plan + ``iterative_plan`` whose behaviour is the canonical
+  ``(avg * num + item) / (num + 1)`` (``01-Create-plan.ipynb:450-454``) -> iterative mean
+  (``:266-269``); anything else (a user-defined non-iterative plan, ``:270-271``) raises
+  ``PlanNotAcceleratedError`` so the node keeps running the reference code for it.
+* ``CycleAggregator.average_plan_diffs`` replaces the slice ``:240-303``: checkpoint bytes +
+  diff bytes in, new checkpoint bytes out.  DB reads/writes and cycle bookkeeping stay with
+  the caller (``make_average_plan_diffs`` shows the wiring).
+"""
+from __future__ import annotations
+
+import logging
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+from . import state as state_codec
+from .engine import ITERATIVE_MEAN, MEAN, WEIGHTED_MEAN, F32, I64, Engine
+from .exceptions import AggregationError, PlanNotAcceleratedError
+
+
+def ready_to_average(server_config: dict, received_diffs: int, cycle_end=None, now=None) -> bool:
+    """``cycle_manager.py:196-210``."""
+    min_diffs = server_config.get("min_diffs", None)
+    max_diffs = server_config.get("max_diffs", None)
+    hit_diffs_limit = received_diffs >= max_diffs if max_diffs is not None else False
+    hit_time_limit = now >= cycle_end if cycle_end is not None else False
+    no_limits = max_diffs is None and cycle_end is None
+    has_enough_diffs = received_diffs >= min_diffs if min_diffs is not None else True
+    return bool(has_enough_diffs and (no_limits or hit_diffs_limit or hit_time_limit))
+
+
+def _canonical_step(avg, item, k):
+    f = np.float32
+    return ((avg.astype(f) * f(k)).astype(f) + item.astype(f)).astype(f) / f(k + 1)
+
+
+def is_canonical_iterative_plan(avg_plan: Callable) -> bool:
+    """Run the hosted plan once on small probe tensors (the way ``cycle_manager.py:269`` calls
+    it: ``avg_plan(list(avg), diff, th.tensor([k]))``) and compare bit for bit with the
+    canonical step.  Probes cover several k, signs, magnitudes and a subnormal."""
+    import torch as th
+
+    rng = np.random.default_rng(7)
+    probe_avg = [rng.standard_normal(17).astype(np.float32) * 1e-2,
+                 np.array([1.0, -2.5, 3.0e-39, 7.0], np.float32)]
+    probe_item = [rng.standard_normal(17).astype(np.float32),
+                  np.array([55.0, 0.125, -1.0e-38, 3.3], np.float32)]
+    for k in (1, 2, 7, 1000):
+        try:
+            res = avg_plan([th.from_numpy(a.copy()) for a in probe_avg],
+                           [th.from_numpy(b.copy()) for b in probe_item], th.tensor([k]))
+        except Exception as e:  # noqa: BLE001 -- any failure means "not the canonical plan"
+            logging.info("avg plan probe failed: %s", e)
+            return False
+        res = list(res)
+        if len(res) != len(probe_avg):
+            return False
+        for got, a, b in zip(res, probe_avg, probe_item):
+            got = np.asarray(got.detach().cpu().numpy() if hasattr(got, "detach") else got, dtype=np.float32)
+            want = _canonical_step(a, b, k)
+            if got.shape != want.shape or not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+                return False
+    return True
+
+
+def select_mode(server_config: dict, avg_plan: Optional[Callable] = None, weights=None) -> int:
+    if weights is not None:
+        return WEIGHTED_MEAN
+    if avg_plan is None:
+        return MEAN  # "Fallback to simple hardcoded avg plan", cycle_manager.py:274
+    if not server_config.get("iterative_plan", False):
+        raise PlanNotAcceleratedError("non-iterative hosted avg plan is user-defined (cycle_manager.py:270-271)")
+    if not is_canonical_iterative_plan(avg_plan):
+        raise PlanNotAcceleratedError("iterative avg plan is not (avg * num + item) / (num + 1)")
+    return ITERATIVE_MEAN
+
+
+class CycleAggregator:
+    """Owns one Engine (one GPU) across cycles; the slab is re-used while it fits."""
+
+    def __init__(self, engine: Optional[Engine] = None, device: int = 0):
+        self.engine = engine if engine is not None else Engine(device)
+        self._numel: tuple = ()
+        self._cap = 0
+        self._dtype = None
+        self._parties = 0
+
+    def _prepare(self, numel: Sequence[int], n: int, dtype: int = F32, parties: int = 1):
+        eng = self.engine
+        numel = tuple(int(x) for x in numel)
+        if numel != self._numel:
+            eng.set_layout(numel)
+            self._numel, self._cap, self._dtype = numel, 0, None
+        if n > self._cap or dtype != self._dtype or parties != self._parties:
+            eng.reserve(max(n, 1), dtype, parties)
+            self._cap, self._dtype, self._parties = max(n, 1), dtype, parties
+        else:
+            eng.reset()
+
+    # ---- bytes in / bytes out: the replaceable slice cycle_manager.py:240-303 -------------------
+    def average_plan_diffs(self, server_config: dict, checkpoint: bytes, diffs: Sequence[bytes],
+                           avg_plan: Optional[Callable] = None, weights=None) -> bytes:
+        if len(diffs) == 0:
+            raise AggregationError("no diffs to average")
+        mode = select_mode(server_config, avg_plan, weights)
+        numel = state_codec.tensor_numels(checkpoint)  # :240
+        self._prepare(numel, len(diffs))
+        for i, d in enumerate(diffs):  # :247-250
+            self.engine.ingest_state(i, d)
+        if mode == WEIGHTED_MEAN:
+            self.engine.set_weights(weights)
+        ckpt = state_codec.flat_params(checkpoint)
+        new = self.engine.fedavg(mode, ckpt)  # :252-296
+        return state_codec.serialize_model_params(checkpoint, new)  # :303
+
+    # ---- tensor lists in / out (what the reference holds after unserialize) ---------------------
+    def average_params(self, server_config: dict, model_params: Sequence[np.ndarray],
+                       diffs: Sequence[Sequence[np.ndarray]], avg_plan: Optional[Callable] = None,
+                       weights=None) -> List[np.ndarray]:
+        if len(diffs) == 0:
+            raise AggregationError("no diffs to average")
+        mode = select_mode(server_config, avg_plan, weights)
+        shapes = [np.shape(p) for p in model_params]
+        numel = [int(np.prod(s)) for s in shapes]
+        self._prepare(numel, len(diffs))
+        for i, d in enumerate(diffs):
+            if len(d) != len(numel):
+                raise AggregationError(f"diff {i} has {len(d)} tensors, model has {len(numel)}")
+            self.engine.ingest(i, np.concatenate([np.asarray(t, np.float32).reshape(-1) for t in d]))
+        if mode == WEIGHTED_MEAN:
+            self.engine.set_weights(weights)
+        flat = np.concatenate([np.asarray(p, np.float32).reshape(-1) for p in model_params])
+        out = self.engine.fedavg(mode, flat)
+        res, off = [], 0
+        for s, n in zip(shapes, numel):
+            res.append(out[off:off + n].reshape(s))
+            off += n
+        return res
+
+    # ---- secure aggregation (PySyft share add + get + float_prec) ------------------------------
+    def secure_aggregate(self, shares: np.ndarray, base: int = 10, precision_fractional: int = 3):
+        """shares: int64 [clients][parties][P].  Returns (int64 wrap-sum [P], float32 decoded [P])."""
+        sh = np.ascontiguousarray(shares, dtype=np.int64)
+        if sh.ndim != 3:
+            raise AggregationError("shares must be [clients][parties][P]")
+        n, s, p = sh.shape
+        self._prepare([p], n, I64, s)
+        for c in range(n):
+            self.engine.ingest(c, sh[c])
+        return self.engine.secagg(base, precision_fractional)
+
+
+def make_average_plan_diffs(aggregator: CycleAggregator, model_manager, process_manager, plan_manager,
+                            original: Callable) -> Callable:
+    """Build a drop-in ``CycleManager._average_plan_diffs(self, server_config, cycle)``.
+
+    DB I/O mirrors ``cycle_manager.py:234-245`` and ``:304-323``; the arithmetic slice
+    ``:240-303`` goes to the engine.  A plan the engine does not implement, or any engine
+    error, runs the reference's ``original`` method unchanged.
+    """
+
+    def _average_plan_diffs(self, server_config: dict, cycle):
+        _model = model_manager.get(fl_process_id=cycle.fl_process_id)
+        _checkpoint = model_manager.load(model_id=_model.id)
+        reports = self._worker_cycles.query(cycle_id=cycle.id, is_completed=True)
+        avg_plan_rec = process_manager.get_plan(fl_process_id=cycle.fl_process_id, is_avg_plan=True)
+        avg_plan = None
+        if avg_plan_rec and avg_plan_rec.value:
+            avg_plan = plan_manager.deserialize_plan(avg_plan_rec.value)
+        try:
+            new_ckpt = aggregator.average_plan_diffs(server_config, _checkpoint.value,
+                                                     [r.diff for r in reports], avg_plan)
+        except PlanNotAcceleratedError as e:
+            logging.info("engine declined (%s): running the reference averaging", e)
+            return original(self, server_config, cycle)
+        model_manager.save(_model.id, new_ckpt)
+        cycle.is_completed = True
+        self._cycles.update()
+        completed = self._cycles.count(fl_process_id=cycle.fl_process_id, is_completed=True)
+        max_cycles = server_config.get("num_cycles", 0)
+        if completed < max_cycles or max_cycles == 0:
+            self.create(cycle.fl_process_id, cycle.version, server_config.get("cycle_length"))
+        else:
+            logging.info("FL is done!")
+
+    return _average_plan_diffs

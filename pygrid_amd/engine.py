@@ -1,0 +1,167 @@
+"""Python handle on one libpygrid_hip context (one GPU, one parameter shard).
+
+This is plumbing over the C ABI: every computation happens in the HIP kernels of
+``pygrid_amd/csrc``.  There is deliberately no CPU implementation here -- an Engine cannot be
+constructed without the library and a visible GPU (``EngineUnavailableError``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .exceptions import AggregationError, EngineUnavailableError, StateParseError
+
+MEAN, ITERATIVE_MEAN, WEIGHTED_MEAN = 0, 1, 2
+F32, I64 = 0, 1
+MODE_NAMES = {MEAN: "mean", ITERATIVE_MEAN: "iterative_mean", WEIGHTED_MEAN: "weighted_mean"}
+
+
+def device_count() -> int:
+    lib = _lib.load()
+    n = C.c_int(0)
+    if lib.pgh_device_count(C.byref(n)) != 0:
+        return 0
+    return n.value
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class Engine:
+    def __init__(self, device: int = 0, pinned_bytes: int = 0):
+        self._lib = _lib.load()
+        h = C.c_void_p()
+        rc = self._lib.pgh_create(int(device), int(pinned_bytes), C.byref(h))
+        if rc != 0:
+            msg = self._lib.pgh_last_error(None).decode()
+            raise EngineUnavailableError(f"pgh_create(device={device}) failed: {msg}")
+        self._h = h
+        self.device = int(device)
+        self.numel: Tuple[int, ...] = ()
+        self.P = 0
+        self.lo = 0
+        self.hi = 0
+        self.dtype = F32
+        self.parties = 1
+
+    # ---- plumbing ----------------------------------------------------------------------------
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self._lib.pgh_last_error(self._h).decode()
+            cls = StateParseError if rc == -5 else AggregationError
+            raise cls(f"{what}: {_lib.STATUS_NAMES.get(rc, rc)}: {msg}", status=rc)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.pgh_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- layout --------------------------------------------------------------------------------
+    @property
+    def p_shard(self) -> int:
+        return self.hi - self.lo
+
+    def set_layout(self, numel: Sequence[int]):
+        arr = (C.c_int64 * len(numel))(*[int(n) for n in numel])
+        self._check(self._lib.pgh_set_layout(self._h, len(numel), arr), "set_layout")
+        self.numel = tuple(int(n) for n in numel)
+        self.P = sum(self.numel)
+        self.lo, self.hi = 0, self.P
+
+    def set_shard(self, lo: int, hi: int):
+        self._check(self._lib.pgh_set_shard(self._h, int(lo), int(hi)), "set_shard")
+        self.lo, self.hi = int(lo), int(hi)
+
+    def reserve(self, max_clients: int, dtype: int = F32, n_parties: int = 1):
+        self._check(self._lib.pgh_reserve(self._h, int(max_clients), int(dtype), int(n_parties)), "reserve")
+        self.dtype = dtype
+        self.parties = 1 if dtype == F32 else int(n_parties)
+
+    def reset(self):
+        self._check(self._lib.pgh_reset(self._h), "reset")
+
+    # ---- ingest --------------------------------------------------------------------------------
+    def ingest(self, client: int, flat: np.ndarray):
+        """Client diff: float32 [P] (dtype F32) or int64 [parties][P] shares (dtype I64)."""
+        if self.dtype == F32:
+            a = np.ascontiguousarray(flat, dtype=np.float32).reshape(-1)
+        else:
+            a = np.ascontiguousarray(flat, dtype=np.int64).reshape(-1)
+        self._check(self._lib.pgh_ingest_raw(self._h, int(client), _ptr(a), a.nbytes, self.dtype),
+                    f"ingest client {client}")
+
+    def ingest_state(self, client: int, pb: bytes):
+        self._check(self._lib.pgh_ingest_state(self._h, int(client), pb, len(pb)), f"ingest_state client {client}")
+
+    def synth_fill(self, seed: int, n_clients: int):
+        self._check(self._lib.pgh_synth_fill(self._h, C.c_uint64(seed), int(n_clients)), "synth_fill")
+
+    def set_weights(self, w: Sequence[float]):
+        a = np.ascontiguousarray(w, dtype=np.float32)
+        self._check(self._lib.pgh_set_weights(self._h, a.ctypes.data_as(C.POINTER(C.c_float)), a.size),
+                    "set_weights")
+
+    # ---- reduction -----------------------------------------------------------------------------
+    def fedavg(self, mode: int, ckpt: np.ndarray) -> np.ndarray:
+        """``ckpt - avg(diffs)`` over this shard (host arrays of p_shard floats)."""
+        c = np.ascontiguousarray(ckpt, dtype=np.float32).reshape(-1)
+        if c.size != self.p_shard:
+            raise AggregationError(f"checkpoint has {c.size} params, shard has {self.p_shard}")
+        out = np.empty_like(c)
+        self._check(self._lib.pgh_fedavg(self._h, int(mode), _ptr(c), _ptr(out)), "fedavg")
+        return out
+
+    def fedavg_device(self, mode: int, d_ckpt: int, d_out: int, stream: int = 0):
+        self._check(self._lib.pgh_fedavg_device(self._h, int(mode), C.c_void_p(d_ckpt), C.c_void_p(d_out),
+                                                C.c_void_p(stream or None)), "fedavg_device")
+
+    def secagg(self, base: int = 10, prec: int = 3, want_sum: bool = True,
+               want_dec: bool = True) -> Tuple[Optional[np.ndarray], Optional[np.ndarray]]:
+        s = np.empty(self.p_shard, dtype=np.int64) if want_sum else None
+        d = np.empty(self.p_shard, dtype=np.float32) if want_dec else None
+        self._check(self._lib.pgh_secagg(self._h, int(base), int(prec), _ptr(s) if s is not None else None,
+                                         _ptr(d) if d is not None else None), "secagg")
+        return s, d
+
+    def secagg_device(self, d_sum: int, d_dec: int, base: int = 10, prec: int = 3, stream: int = 0):
+        self._check(self._lib.pgh_secagg_device(self._h, int(base), int(prec), C.c_void_p(d_sum or None),
+                                                C.c_void_p(d_dec or None), C.c_void_p(stream or None)),
+                    "secagg_device")
+
+    def synth_ckpt_device(self, seed: int, d_ckpt: int, stream: int = 0):
+        self._check(self._lib.pgh_synth_ckpt_device(self._h, C.c_uint64(seed), C.c_void_p(d_ckpt),
+                                                    C.c_void_p(stream or None)), "synth_ckpt_device")
+
+    # ---- observability -------------------------------------------------------------------------
+    def set_variant(self, v: int):
+        self._check(self._lib.pgh_set_variant(self._h, int(v)), "set_variant")
+
+    def stats(self) -> dict:
+        st = _lib.Stats()
+        self._check(self._lib.pgh_stats(self._h, C.byref(st)), "stats")
+        return {name: getattr(st, name) for name, _ in _lib.Stats._fields_}
+
+    def reset_stats(self):
+        self._check(self._lib.pgh_reset_stats(self._h), "reset_stats")
+
+    def slab(self) -> Tuple[int, int]:
+        p = C.c_void_p()
+        ld = C.c_int64()
+        self._check(self._lib.pgh_slab(self._h, C.byref(p), C.byref(ld)), "slab")
+        return p.value or 0, ld.value

@@ -1,0 +1,71 @@
+"""syft State codec, host side: the replacement for ``ModelManager.serialize_model_params`` /
+``unserialize_model_params`` (``apps/node/src/app/main/model_centric/models/model_manager.py:79-103``)
+on the cycle-close path.
+
+The byte work is done in C++ (``pgh_state_scan`` / ``pgh_state_patch`` in libpygrid_hip):
+
+* unserialize = locate each tensor's packed float32 payload and view it (no per-element
+  Python work, unlike syft's ``_unbufferize``);
+* serialize of the new checkpoint = the current checkpoint's bytes with every payload
+  overwritten (``cycle_manager.py:303`` re-serializes the same tensor list, so shapes,
+  order and message layout are unchanged; ids/tags keep their previous values).
+
+Schema: build-owned restatement of syft-proto 0.5.2 (``state_schema.py``); parity unpinned
+until checked against real client bytes (DESIGN.md "State codec").
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .exceptions import StateParseError
+
+
+def scan(pb: bytes) -> List[Tuple[int, int]]:
+    """(byte offset, float count) of every tensor payload, in State order."""
+    lib = _lib.load()
+    n = C.c_int(0)
+    rc = lib.pgh_state_scan(pb, len(pb), 0, None, None, C.byref(n))
+    if rc != 0:
+        raise StateParseError(f"malformed State message ({_lib.STATUS_NAMES.get(rc, rc)})", status=rc)
+    k = n.value
+    offs = (C.c_int64 * max(k, 1))()
+    cnts = (C.c_int64 * max(k, 1))()
+    rc = lib.pgh_state_scan(pb, len(pb), k, offs, cnts, C.byref(n))
+    if rc != 0:
+        raise StateParseError("malformed State message", status=rc)
+    return [(offs[i], cnts[i]) for i in range(k)]
+
+
+def tensor_numels(pb: bytes) -> List[int]:
+    return [c for _, c in scan(pb)]
+
+
+def unserialize_model_params(pb: bytes, shapes: Sequence[Sequence[int]] = None) -> List[np.ndarray]:
+    """float32 copies of every tensor, flat (or reshaped to ``shapes``)."""
+    buf = np.frombuffer(pb, dtype=np.uint8)
+    out = []
+    for t, (off, cnt) in enumerate(scan(pb)):
+        a = buf[off:off + 4 * cnt].view("<f4").astype(np.float32)
+        out.append(a.reshape(shapes[t]) if shapes is not None else a)
+    return out
+
+
+def flat_params(pb: bytes) -> np.ndarray:
+    parts = unserialize_model_params(pb)
+    return np.concatenate(parts) if parts else np.empty(0, np.float32)
+
+
+def serialize_model_params(template: bytes, values: np.ndarray) -> bytes:
+    """New State bytes: ``template`` with all payloads replaced by ``values`` (P floats)."""
+    lib = _lib.load()
+    v = np.ascontiguousarray(values, dtype="<f4").reshape(-1)
+    out = C.create_string_buffer(len(template))
+    rc = lib.pgh_state_patch(template, len(template), v.ctypes.data, v.size, out)
+    if rc != 0:
+        raise StateParseError(f"cannot patch State ({_lib.STATUS_NAMES.get(rc, rc)}): "
+                              f"{v.size} values for this checkpoint?", status=rc)
+    return out.raw

@@ -1,0 +1,62 @@
+"""CPU: the C-ABI library builds, loads and exports every symbol include/pgh_api.h declares;
+the host-only State codec works without a GPU; the engine refuses to run without one."""
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def declared_symbols():
+    text = (ROOT / "include" / "pgh_api.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pgh_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    from pygrid_amd import _lib
+
+    lib = _lib.load()
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_lib.SIGNATURES), "ctypes signatures out of sync with the header"
+    assert lib.pgh_abi_version() == 1
+
+
+def test_library_has_gfx950_code_object():
+    data = (ROOT / "pygrid_amd" / "libpygrid_hip.so").read_bytes()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_library_does_not_link_torch():
+    import subprocess
+
+    out = subprocess.run(["readelf", "-d", str(ROOT / "pygrid_amd" / "libpygrid_hip.so")],
+                         capture_output=True, text=True).stdout
+    assert "torch" not in out and "c10" not in out
+
+
+def test_engine_without_gpu_raises():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    from pygrid_amd import Engine, EngineUnavailableError, device_count
+
+    assert device_count() == 0
+    with pytest.raises(EngineUnavailableError):
+        Engine(0)
+
+
+def test_null_and_bad_arguments_return_status():
+    from pygrid_amd import _lib
+
+    lib = _lib.load()
+    assert lib.pgh_create(0, 0, None) == -1
+    assert lib.pgh_set_layout(None, 1, None) == -1
+    assert lib.pgh_stats(None, None) == -1
+    assert lib.pgh_last_error(None) is not None

@@ -1,0 +1,257 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Bar: bit-exact for everything (fp32 FedAvg included: the kernels fold clients in the
+reference's order with separately rounded IEEE ops).  NaN positions must match; NaN payload
+bits are not compared.
+"""
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+from oracle import coracle
+from oracle import oracle as O
+from oracle.gen_golden import MNIST_SHAPES, mnist_inputs
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+MODES = {"mean": 0, "iter": 1, "weighted": 2}
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def same(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    nan = np.isnan(a)
+    return a.shape == b.shape and np.array_equal(nan, np.isnan(b)) and np.array_equal(bits(a)[~nan], bits(b)[~nan])
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def run_f32(engine, diffs, ckpt, mode, weights=None, numel=None):
+    d = np.asarray(diffs, F)
+    engine.set_layout(numel or [d.shape[1]])
+    engine.reserve(d.shape[0])
+    for c in range(d.shape[0]):
+        engine.ingest(c, d[c])
+    if weights is not None:
+        engine.set_weights(weights)
+    return engine.fedavg(mode, np.asarray(ckpt, F))
+
+
+def test_engine_reports_device(engine):
+    from pygrid_amd import device_count
+
+    assert device_count() >= 1
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+def test_edge_fixtures_all_modes(engine, gold, variant):
+    z = np.load(gold / "edge_f32.npz")
+    engine.set_variant(variant)
+    try:
+        for name in z["names"]:
+            d, c, w = z[f"{name}_diffs"], z[f"{name}_ckpt"], z[f"{name}_w"]
+            for key, mode in MODES.items():
+                got = run_f32(engine, d, c, mode, w if mode == 2 else None)
+                assert same(got, z[f"{name}_{key}"]), (name, key, variant)
+    finally:
+        engine.set_variant(0)
+
+
+def test_kat_avg_plan(engine, gold):
+    kat = json.loads((gold / "kat_avg_plan.json").read_text())
+    numel = [int(np.prod(s)) for s in kat["shapes"]]
+    P = sum(numel)
+    diffs = np.stack([np.full(P, k, F) for k in kat["coeffs"]])
+    out = run_f32(engine, diffs, np.zeros(P, F), 1, numel=numel)
+    assert np.all(-out == F(kat["expected_avg"]))
+
+
+def test_mnist_golden_host_ingest(engine, gold):
+    g = json.loads((gold / "mnist_synth.json").read_text())
+    diffs, ckpt = mnist_inputs(g["seed"], g["n_clients"])
+    numel = [int(np.prod(s)) for s in MNIST_SHAPES]
+    assert sha(run_f32(engine, diffs, ckpt, 0, numel=numel)) == g["sha256_mean"]
+    assert sha(run_f32(engine, diffs, ckpt, 1, numel=numel)) == g["sha256_iter"]
+    assert sha(run_f32(engine, diffs, ckpt, 2, np.asarray(g["weights"], F), numel=numel)) == g["sha256_weighted"]
+
+
+def test_mnist_golden_device_generator(engine, gold):
+    """The on-device synthetic generator reproduces the restated one bit for bit."""
+    import torch
+
+    g = json.loads((gold / "mnist_synth.json").read_text())
+    numel = [int(np.prod(s)) for s in MNIST_SHAPES]
+    engine.set_layout(numel)
+    engine.reserve(g["n_clients"])
+    engine.synth_fill(g["seed"], g["n_clients"])
+    ck = torch.empty(sum(numel), dtype=torch.float32, device="cuda")
+    out = torch.empty_like(ck)
+    engine.synth_ckpt_device(g["seed"], ck.data_ptr())
+    engine.fedavg_device(0, ck.data_ptr(), out.data_ptr())
+    torch.cuda.synchronize()
+    assert sha(ck.cpu().numpy()) == g["sha256_ckpt"]
+    assert sha(out.cpu().numpy()) == g["sha256_mean"]
+    ptr, ld = engine.slab()
+    assert ptr and ld % 64 == 0
+
+
+def test_smpc_vectors(engine, gold):
+    from pygrid_amd.cycle import CycleAggregator
+
+    z = np.load(gold / "smpc_vectors.npz")
+    agg = CycleAggregator(engine)
+    s, _ = agg.secure_aggregate(z["share_shares"])
+    assert np.array_equal(s, z["share_x"])
+    for op in ("add", "sub"):
+        for k in range(3):
+            s, d = agg.secure_aggregate(z[f"{op}{k}_shares"])
+            assert np.array_equal(s, z[f"{op}{k}_sum"])
+            assert np.array_equal(bits(d), bits(z[f"{op}{k}_dec"]))
+            assert np.allclose(d, z[f"{op}{k}_ref"], atol=1e-3)  # the reference's own bar
+
+
+def test_secagg_wrap(engine, gold):
+    from pygrid_amd.cycle import CycleAggregator
+
+    z = np.load(gold / "secagg_wrap.npz")
+    agg = CycleAggregator(engine)
+    s, d = agg.secure_aggregate(z["shares"])
+    assert np.array_equal(s, z["sum"]) and np.array_equal(bits(d), bits(z["dec"]))
+    s2, d2 = agg.secure_aggregate(z["shares"], base=2, precision_fractional=16)
+    assert np.array_equal(s2, z["sum"]) and np.array_equal(bits(d2), bits(z["dec_base2_prec16"]))
+
+
+@pytest.mark.parametrize("variant", [0, 3])
+def test_secagg_synthetic_sampled(engine, variant):
+    """250 clients x 2 parties x 1M params generated on the GPU; bit-exact on a sampled subset."""
+    import torch
+
+    P, N, S = 1_000_003, 250, 2
+    engine.set_layout([P])
+    engine.reserve(N, 1, S)
+    engine.synth_fill(99, N)
+    engine.set_variant(variant)
+    try:
+        s = torch.empty(P, dtype=torch.int64, device="cuda")
+        d = torch.empty(P, dtype=torch.float32, device="cuda")
+        engine.secagg_device(s.data_ptr(), d.data_ptr())
+        torch.cuda.synchronize()
+    finally:
+        engine.set_variant(0)
+    idx = np.unique(np.concatenate([np.arange(0, 64), np.random.default_rng(1).integers(0, P, 2000), [P - 1]]))
+    want = np.zeros(idx.size, np.uint64)
+    with np.errstate(over="ignore"):
+        for c in range(N):
+            want += O.secagg_sum(O.synth_shares(99, c, S, idx.astype(np.uint64))[None]).view(np.uint64)
+    want = want.view(np.int64)
+    got_s = s.cpu().numpy()[idx]
+    got_d = d.cpu().numpy()[idx]
+    assert np.array_equal(got_s, want)
+    assert np.array_equal(bits(got_d), bits(O.fix_prec_decode(want)))
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_resnet18_scale_sampled(engine, mode):
+    """BASELINE config 2 shape (P = 11,689,512, N = 1,000) fully resident; bit-exact against the
+    oracle on 4,096 sampled params x all 1,000 clients (diffs regenerated on the CPU)."""
+    import torch
+
+    P, N, seed = 11_689_512, 1000, 4321
+    engine.set_layout([P])
+    engine.reserve(N)
+    engine.synth_fill(seed, N)
+    w = (np.arange(N) % 7 + 1).astype(F) * F(0.5)
+    if mode == 2:
+        engine.set_weights(w)
+    ck = torch.empty(P, dtype=torch.float32, device="cuda")
+    out = torch.empty_like(ck)
+    engine.synth_ckpt_device(seed, ck.data_ptr())
+    engine.fedavg_device(mode, ck.data_ptr(), out.data_ptr())
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(mode)
+    idx = np.unique(np.concatenate([np.arange(8), rng.integers(0, P, 4088), [P - 1]])).astype(np.int64)
+    d = np.stack([O.synth_diff(seed, c, idx.astype(np.uint64)) for c in range(N)])
+    c = O.synth_ckpt(seed, idx.astype(np.uint64))
+    want = coracle.fedavg(mode, d, c, w if mode == 2 else None)
+    assert same(out.cpu().numpy()[idx], want)
+
+
+def test_shards_concatenate_bit_identically(engine):
+    """Param-axis shards (what each rank of a multi-GPU run computes) equal the unsharded run."""
+    from pygrid_amd import Engine
+    from pygrid_amd.sharding import all_shard_bounds
+
+    rng = np.random.default_rng(5)
+    P, N = 100_003, 37
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    full = run_f32(engine, d, c, 0)
+    parts = []
+    with Engine(engine.device) as e2:
+        e2.set_layout([P])
+        for lo, hi in all_shard_bounds(P, 3):
+            e2.set_shard(lo, hi)
+            e2.reserve(N)
+            for k in range(N):
+                e2.ingest(k, d[k])
+            parts.append(e2.fedavg(0, c[lo:hi]))
+    assert same(np.concatenate(parts), full)
+
+
+def test_state_bytes_roundtrip(engine):
+    """Bytes in, bytes out: State diffs -> engine -> patched checkpoint, parsed back with
+    google.protobuf (independent of the C++ walker)."""
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.state_schema import build_state, parse_state
+
+    rng = np.random.default_rng(8)
+    shapes = [(392, 784), (392,), (10, 392), (10,)]
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for _ in range(3)]
+    agg = CycleAggregator(engine)
+    ck_pb = build_state(ckpt)
+    new_pb = agg.average_plan_diffs({}, ck_pb, [build_state(d, as_param=(i == 1)) for i, d in enumerate(diffs)])
+    assert len(new_pb) == len(ck_pb)
+    for got, want in zip(parse_state(new_pb), O.fedavg_mean(ckpt, diffs)):
+        assert same(got, want)
+
+
+def test_average_params_api(engine):
+    from pygrid_amd.cycle import CycleAggregator
+
+    rng = np.random.default_rng(9)
+    shapes = [(3, 5), (7,), (1,)]
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    diffs = [[rng.standard_normal(s).astype(F) for s in shapes] for _ in range(4)]
+    agg = CycleAggregator(engine)
+    for got, want in zip(agg.average_params({}, ckpt, diffs), O.fedavg_mean(ckpt, diffs)):
+        assert same(got, want)
+    w = [1.0, 2.0, 3.0, 4.0]
+    for got, want in zip(agg.average_params({}, ckpt, diffs, weights=w), O.fedavg_weighted(ckpt, diffs, w)):
+        assert same(got, want)
+
+
+def test_errors_are_loud(engine):
+    from pygrid_amd import AggregationError
+
+    engine.set_layout([10])
+    engine.reserve(3)
+    with pytest.raises(AggregationError):
+        engine.fedavg(0, np.zeros(10, F))  # nothing ingested
+    engine.ingest(0, np.ones(10, F))
+    engine.ingest(2, np.ones(10, F))
+    with pytest.raises(AggregationError, match="missing"):
+        engine.fedavg(0, np.zeros(10, F))
+    with pytest.raises(AggregationError):
+        engine.ingest(1, np.ones(11, F))
+    with pytest.raises(AggregationError):
+        engine.fedavg(7, np.zeros(10, F))
+    with pytest.raises(AggregationError):
+        engine.fedavg(2, np.zeros(10, F))  # weighted without weights
