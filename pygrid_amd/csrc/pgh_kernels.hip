@@ -214,9 +214,13 @@ int cu_count() {
     return cached[dev];
 }
 
-// Grid: variant 0 = one column per lane (grid covers every column once); variant 1 =
-// persistent grid of 4 blocks per CU striding over columns; variants 2/3 = the same two with
-// non-temporal (nt) loads for the once-read diff stream.
+// Variants (A/B in one process: tools/ab_variants.py; profiles/r01/README.md):
+//   0 = nt loads, U=8, one column per lane (grid covers every column once)   <- default
+//   1 = nt loads, U=8, persistent grid (4 blocks per CU) striding over columns
+//   2 / 3 = the same two with plain (default-policy) loads
+//   4 / 5 = plain loads, U=16
+// Even variants: one column per lane; odd: persistent grid.  nt loads won 2-3 % on the
+// once-read diff stream (r01: 6393 vs 6270 GB/s at ResNet-18 x 1000 clients).
 inline unsigned grid_for(int64_t ncol, int variant) {
     const int64_t full = (ncol + BLOCK - 1) / BLOCK;
     if ((variant & 1) == 0) return (unsigned)(full > 0 ? full : 1);
@@ -228,8 +232,8 @@ template <int MODE>
 hipError_t dispatch_fedavg(const FedavgArgs& a, int64_t ncol, hipStream_t s) {
     const unsigned g = grid_for(ncol, a.variant);
     switch (a.variant) {
-    case 0: case 1: k_fedavg<MODE, 8, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
-    case 2: case 3: k_fedavg<MODE, 8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 0: case 1: k_fedavg<MODE, 8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 2: case 3: k_fedavg<MODE, 8, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
     case 4: case 5: k_fedavg<MODE, 16, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
     default: return hipErrorInvalidValue;
     }
@@ -265,8 +269,8 @@ hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s) {
     const int64_t ncol = (a.p + 1) / 2;
     const unsigned g = grid_for(ncol, a.variant);
     switch (a.variant) {
-    case 0: case 1: k_secagg<8, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
-    case 2: case 3: k_secagg<8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 0: case 1: k_secagg<8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 2: case 3: k_secagg<8, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
     case 4: case 5: k_secagg<16, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
     default: return hipErrorInvalidValue;
     }
