@@ -46,6 +46,8 @@ typedef enum {
  * examples/model-centric/01-Create-plan.ipynb:450-454.  PGH_WEIGHTED_MEAN: north_star's
  * weighted FedAvg (no reference counterpart; equals PGH_MEAN bit for bit at w == 1). */
 typedef enum { PGH_MEAN = 0, PGH_ITERATIVE_MEAN = 1, PGH_WEIGHTED_MEAN = 2 } pgh_mode;
+/* Stream kind for pgh_stream_begin besides the three averaging modes. */
+#define PGH_STREAM_SECAGG 16
 
 typedef enum { PGH_F32 = 0, PGH_I64 = 1 } pgh_dtype;
 
@@ -54,13 +56,15 @@ typedef struct {
     double kernel_ms_total;    /* sum over timed launches since the last reset */
     uint64_t kernel_launches;  /* timed launches since the last reset */
     uint64_t kernel_bytes_last;/* algorithmic bytes of the last reduction launch */
+    uint64_t kernel_bytes_total;/* algorithmic bytes over timed launches since the last reset */
     double h2d_ms_total;       /* ingest wall time (host buffer -> HBM), ms */
     uint64_t h2d_bytes_total;  /* bytes moved host -> HBM by ingest */
     double close_ms_last;      /* wall time of the last pgh_fedavg / pgh_secagg (host in/out) */
     int64_t p_shard;           /* params in this context's shard */
     int64_t ld;                /* slab row stride (elements) */
-    int32_t n_clients;         /* clients ingested (contiguous from 0) */
-    int32_t max_clients;       /* slab capacity */
+    int64_t n_folded;          /* stream mode: clients folded into the running state */
+    int32_t n_clients;         /* clients ingested since the last reset */
+    int32_t max_clients;       /* slab capacity (slots) */
 } pgh_stats_t;
 
 /* ---- context lifecycle ------------------------------------------------------------------ */
@@ -71,6 +75,9 @@ int pgh_device_count(int* n);
 int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out);
 void pgh_destroy(pgh_ctx* ctx);
 const char* pgh_last_error(const pgh_ctx* ctx);   /* ctx may be NULL (creation errors) */
+/* Page-locked host buffers: ingest DMAs them straight to HBM (no staging copy). */
+int pgh_host_alloc(size_t bytes, void** out);
+int pgh_host_free(void* p);
 
 /* ---- layout ------------------------------------------------------------------------------
  * Flat parameter vector = tensors concatenated in State order
@@ -78,8 +85,10 @@ const char* pgh_last_error(const pgh_ctx* ctx);   /* ctx may be NULL (creation e
 int pgh_set_layout(pgh_ctx* ctx, int n_tensors, const int64_t* numel);
 /* Restrict this context to the flat range [lo, hi) (param-axis shard).  Default: [0, P). */
 int pgh_set_shard(pgh_ctx* ctx, int64_t lo, int64_t hi);
-/* Allocate the HBM slab: max_clients rows of the shard, dtype PGH_F32 (fp32 diffs) or
- * PGH_I64 (n_parties int64 shares per client).  Forgets previously ingested clients. */
+/* Allocate the HBM slab: max_clients slots of the shard, dtype PGH_F32 (fp32 diffs) or
+ * PGH_I64 (n_parties int64 share rows per client).  Forgets previously ingested clients.
+ * RESIDENT use: client k lives in slot k (k < max_clients).  STREAM use (pgh_stream_begin):
+ * client k goes to slot k % max_clients, so the slab is a ring and N may exceed it. */
 int pgh_reserve(pgh_ctx* ctx, int max_clients, int dtype, int n_parties);
 /* Forget ingested clients and weights (start of a new cycle); keeps allocations. */
 int pgh_reset(pgh_ctx* ctx);
@@ -95,6 +104,8 @@ int pgh_ingest_state(pgh_ctx* ctx, int client, const uint8_t* pb, size_t n);
 /* Fill slab rows [0, n_clients) with the deterministic synthetic diffs (or shares) of
  * SURVEY.md 8(d) for this shard, generated on the GPU (oracle/oracle.py restates them). */
 int pgh_synth_fill(pgh_ctx* ctx, uint64_t seed, int n_clients);
+/* Ingest synthetic clients [client0, client0 + n) generated on the GPU (either use). */
+int pgh_synth_ingest(pgh_ctx* ctx, uint64_t seed, int client0, int n);
 /* Per-client weights for PGH_WEIGHTED_MEAN (n == clients ingested at reduction time). */
 int pgh_set_weights(pgh_ctx* ctx, const float* w, int n);
 
@@ -111,12 +122,26 @@ int pgh_secagg_device(pgh_ctx* ctx, int base, int prec, int64_t* d_sum, float* d
 /* Fill a device buffer with the synthetic checkpoint of this shard (P_shard floats). */
 int pgh_synth_ckpt_device(pgh_ctx* ctx, uint64_t seed, float* d_ckpt, void* stream);
 
+/* ---- STREAM use: fold clients in order as they arrive ---------------------------------------
+ * After pgh_stream_begin, every run of >= fold_batch consecutive clients at the fold front is
+ * folded into the running state (same op order as RESIDENT: bit-identical results) and its slots
+ * are freed; H2D of later clients overlaps those folds.  kind = a pgh_mode or PGH_STREAM_SECAGG;
+ * fold_batch <= 0 means half the slots.  Clients may arrive out of order within the ring. */
+int pgh_stream_begin(pgh_ctx* ctx, int kind, int fold_batch);
+int pgh_stream_flush(pgh_ctx* ctx);               /* fold the ready run now */
+/* Fold what is left and write out = ckpt - avg (all clients [0, n) must have arrived). */
+int pgh_stream_finish(pgh_ctx* ctx, const float* ckpt, float* out);
+int pgh_stream_finish_device(pgh_ctx* ctx, const float* d_ckpt, float* d_out, void* stream);
+int pgh_stream_finish_secagg(pgh_ctx* ctx, int base, int prec, int64_t* sum_out, float* dec_out);
+int pgh_stream_finish_secagg_device(pgh_ctx* ctx, int base, int prec, int64_t* d_sum, float* d_dec, void* stream);
+
 /* ---- tuning and observability -------------------------------------------------------------- */
 int pgh_set_variant(pgh_ctx* ctx, int variant);   /* kernel variant, for A/B measurement */
 int pgh_stats(pgh_ctx* ctx, pgh_stats_t* out);     /* synchronises pending timing events */
 int pgh_reset_stats(pgh_ctx* ctx);
 /* Device pointer of the slab and its row stride, for callers that drive the kernels. */
 int pgh_slab(pgh_ctx* ctx, void** d_slab, int64_t* ld);
+int pgh_sync(pgh_ctx* ctx);                       /* wait for the context's streams */
 
 /* ---- State codec (host only; replaces syft serde at model_manager.py:79-103) ------------- */
 /* Locate each tensor's packed float32 payload in a State message: byte offset and element

@@ -12,10 +12,10 @@ Nothing here computes on the CPU: without the built library and a GPU the engine
 """
 from .exceptions import (AggregationError, EngineUnavailableError, PlanNotAcceleratedError, PyGridError,
                          StateParseError)
-from .engine import F32, I64, ITERATIVE_MEAN, MEAN, WEIGHTED_MEAN, Engine, device_count
+from .engine import F32, I64, ITERATIVE_MEAN, MEAN, STREAM_SECAGG, WEIGHTED_MEAN, Engine, PinnedBuffer, device_count
 
 __all__ = [
     "AggregationError", "EngineUnavailableError", "PlanNotAcceleratedError", "PyGridError", "StateParseError",
-    "Engine", "device_count", "MEAN", "ITERATIVE_MEAN", "WEIGHTED_MEAN", "F32", "I64",
+    "Engine", "PinnedBuffer", "device_count", "STREAM_SECAGG", "MEAN", "ITERATIVE_MEAN", "WEIGHTED_MEAN", "F32", "I64",
 ]
 __version__ = "0.1.0"

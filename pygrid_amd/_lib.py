@@ -24,11 +24,13 @@ class Stats(C.Structure):
         ("kernel_ms_total", C.c_double),
         ("kernel_launches", C.c_uint64),
         ("kernel_bytes_last", C.c_uint64),
+        ("kernel_bytes_total", C.c_uint64),
         ("h2d_ms_total", C.c_double),
         ("h2d_bytes_total", C.c_uint64),
         ("close_ms_last", C.c_double),
         ("p_shard", C.c_int64),
         ("ld", C.c_int64),
+        ("n_folded", C.c_int64),
         ("n_clients", C.c_int32),
         ("max_clients", C.c_int32),
     ]
@@ -44,6 +46,8 @@ SIGNATURES = {
     "pgh_create": (_i, [_i, _sz, C.POINTER(_vp)]),
     "pgh_destroy": (None, [_vp]),
     "pgh_last_error": (C.c_char_p, [_vp]),
+    "pgh_host_alloc": (_i, [_sz, C.POINTER(_vp)]),
+    "pgh_host_free": (_i, [_vp]),
     "pgh_set_layout": (_i, [_vp, _i, _P64]),
     "pgh_set_shard": (_i, [_vp, _i64, _i64]),
     "pgh_reserve": (_i, [_vp, _i, _i, _i]),
@@ -51,12 +55,20 @@ SIGNATURES = {
     "pgh_ingest_raw": (_i, [_vp, _i, _vp, _sz, _i]),
     "pgh_ingest_state": (_i, [_vp, _i, C.c_char_p, _sz]),
     "pgh_synth_fill": (_i, [_vp, _u64, _i]),
+    "pgh_synth_ingest": (_i, [_vp, _u64, _i, _i]),
     "pgh_set_weights": (_i, [_vp, C.POINTER(C.c_float), _i]),
     "pgh_fedavg": (_i, [_vp, _i, _vp, _vp]),
     "pgh_fedavg_device": (_i, [_vp, _i, _vp, _vp, _vp]),
     "pgh_secagg": (_i, [_vp, _i, _i, _vp, _vp]),
     "pgh_secagg_device": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pgh_synth_ckpt_device": (_i, [_vp, _u64, _vp, _vp]),
+    "pgh_stream_begin": (_i, [_vp, _i, _i]),
+    "pgh_stream_flush": (_i, [_vp]),
+    "pgh_stream_finish": (_i, [_vp, _vp, _vp]),
+    "pgh_stream_finish_device": (_i, [_vp, _vp, _vp, _vp]),
+    "pgh_stream_finish_secagg": (_i, [_vp, _i, _i, _vp, _vp]),
+    "pgh_stream_finish_secagg_device": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
+    "pgh_sync": (_i, [_vp]),
     "pgh_set_variant": (_i, [_vp, _i]),
     "pgh_stats": (_i, [_vp, C.POINTER(Stats)]),
     "pgh_reset_stats": (_i, [_vp]),

@@ -1,44 +1,62 @@
 // libpygrid_hip: C-ABI context around the gfx950 aggregation kernels.
 //
 // One pgh_ctx = one GPU = one parameter shard.  It owns
-//   * the HBM slab [max_clients x rows_per_client][ld] holding every reported diff of the
-//     cycle (fp32) or every share (int64), rows padded to 256 B,
-//   * the [P_shard] device vectors (checkpoint, output, running state, weights),
-//   * a 2-slot pinned host ring through which ingest streams host bytes into the slab with
-//     hipMemcpyAsync on a dedicated copy stream (overlapping the next slot's host memcpy),
+//   * the HBM slab: R slots x rows_per_client rows of ld elements (fp32 diffs, or
+//     n_parties int64 share rows per client), rows padded to 256 B;
+//   * the [P_shard] device vectors (checkpoint, output, running fold state, weights);
+//   * a 2-slot pinned host ring through which pageable host bytes reach the slab
+//     (multi-threaded host memcpy into a pinned slot overlapping the previous slot's DMA on a
+//     dedicated copy stream); page-locked caller buffers are DMA'd directly;
 //   * HIP event pairs around every reduction launch (pgh_stats reports kernel time).
 //
+// Two ways to use the slab:
+//   RESIDENT  client k lives in slot k until the context is reset; pgh_fedavg / pgh_secagg fold
+//             all clients [0, n) in one launch (repeatable: the diffs stay resident).
+//   STREAM    (pgh_stream_begin .. pgh_stream_finish) client k goes to slot k % R; every run of
+//             consecutive clients starting at the fold front is folded into the running state
+//             (in client order, so fp32 results are bit-identical to RESIDENT) and its slots
+//             freed.  Lets N x P exceed HBM and overlaps H2D ingest with reduction (SURVEY 8(d)
+//             configs 3-5) and folds diffs as they are reported.
+//
 // Reference mapping: ingest = the N x unserialize_model_params loop of
-// cycle_manager.py:247-250; pgh_fedavg = :252-296; pgh_secagg = PySyft share add + .get() +
-// float_prec (test_basic_syft_operations.py:417-424).  Errors map to negative status codes and
-// a message (the Python shim raises a PyGridError subclass, as tasks/cycle.py:33-37 expects).
+// cycle_manager.py:247-250; fedavg = :252-296; secagg = PySyft share add + .get() + float_prec
+// (test_basic_syft_operations.py:417-424).  Errors are negative status codes plus a message (the
+// Python shim raises a PyGridError subclass, as tasks/cycle.py:33-37 expects).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pgh_api.h"
 #include "pgh_kernels.h"
 #include "pgh_state.h"
 
+namespace {
+constexpr int KIND_SECAGG = 3;  // stream kind besides the three fedavg modes
+}
+
 struct pgh_ctx {
     int device = 0;
     hipStream_t stream = nullptr;  // reductions
-    hipStream_t copy = nullptr;    // ingest H2D
+    hipStream_t copy = nullptr;    // ingest H2D and on-device synthetic fill
     hipEvent_t copy_done = nullptr;
+    hipEvent_t fold_done = nullptr;
+    hipEvent_t xsync = nullptr;    // caller-stream <-> context-stream ordering
+    bool fold_pending = false;
 
     std::vector<int64_t> numel;
     int64_t P = 0, lo = 0, hi = 0, pg = 0, ld = 0;
     bool layout = false;
 
-    int max_clients = 0, dtype = PGH_F32, parties = 1;
+    int slots = 0, dtype = PGH_F32, parties = 1;
     void* d_slab = nullptr;
     size_t slab_bytes = 0;
-    size_t vec_cap = 0;  // elements of each [P_shard] vector (= ld)
     float* d_ckpt = nullptr;
     float* d_out = nullptr;
     float* d_acc = nullptr;
@@ -46,17 +64,25 @@ struct pgh_ctx {
     int64_t* d_sum = nullptr;
     float* d_dec = nullptr;
     float* d_w = nullptr;
+    size_t w_cap = 0;
 
     uint8_t* h_pin[2] = {nullptr, nullptr};
     size_t pin_slot = 0;
     hipEvent_t pin_ev[2] = {nullptr, nullptr};
     bool pin_used[2] = {false, false};
     int pin_next = 0;
+    int copy_threads = 8;
 
-    std::vector<uint8_t> have;
+    std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
     std::vector<float> weights;
-    int variant = 0;
+    bool weights_on_device = false;
 
+    bool streaming = false;
+    int kind = 0;
+    int fold_batch = 1;
+    int64_t folded = 0;  // stream: clients [0, folded) are in the running state
+
+    int variant = 0;
     struct Timed { hipEvent_t a, b; uint64_t bytes; };
     std::vector<Timed> pending;
     std::vector<hipEvent_t> pool;
@@ -79,12 +105,18 @@ int fail(pgh_ctx* c, int code, const char* fmt, ...) {
     return code;
 }
 
-#define CK(c, expr)                                                                        \
-    do {                                                                                   \
-        hipError_t e_ = (expr);                                                            \
-        if (e_ != hipSuccess)                                                              \
+#define CK(c, expr)                                                                            \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
             return fail((c), PGH_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
-                        __FILE__, __LINE__);                                               \
+                        __FILE__, __LINE__);                                                   \
+    } while (0)
+
+#define RC(expr)            \
+    do {                    \
+        int r_ = (expr);    \
+        if (r_) return r_;  \
     } while (0)
 
 struct DeviceGuard {  // select the context's GPU for the call, restore the caller's after
@@ -103,8 +135,11 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+size_t esize(int dtype) { return dtype == PGH_F32 ? 4 : 8; }
+
 void free_slab(pgh_ctx* c) {
-    (void)hipDeviceSynchronize();
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->copy) (void)hipStreamSynchronize(c->copy);
     (void)hipFree(c->d_slab); c->d_slab = nullptr; c->slab_bytes = 0;
     (void)hipFree(c->d_ckpt); c->d_ckpt = nullptr;
     (void)hipFree(c->d_out); c->d_out = nullptr;
@@ -112,30 +147,31 @@ void free_slab(pgh_ctx* c) {
     (void)hipFree(c->d_uacc); c->d_uacc = nullptr;
     (void)hipFree(c->d_sum); c->d_sum = nullptr;
     (void)hipFree(c->d_dec); c->d_dec = nullptr;
-    (void)hipFree(c->d_w); c->d_w = nullptr;
-    c->vec_cap = 0;
-    c->max_clients = 0;
-    c->have.clear();
+    (void)hipFree(c->d_w); c->d_w = nullptr; c->w_cap = 0;
+    c->slots = 0;
+    c->slot_client.clear();
+    c->streaming = false;
+    c->folded = 0;
+    c->fold_pending = false;
+    c->weights_on_device = false;
 }
 
-// Clients ingested must be exactly {0..n-1}: the fold order is the client order.
-int contiguous_clients(pgh_ctx* c, int* n_out) {
-    int n = 0;
-    while (n < (int)c->have.size() && c->have[n]) ++n;
-    for (int k = n; k < (int)c->have.size(); ++k)
-        if (c->have[k]) return fail(c, PGH_E_STATE, "client %d is missing but client %d was ingested", n, k);
-    if (n == 0) return fail(c, PGH_E_STATE, "no diffs ingested");
-    *n_out = n;
-    return PGH_OK;
-}
-
-int check_ready(pgh_ctx* c, int dtype) {
+int check_ready(pgh_ctx* c) {
     if (!c) return PGH_E_ARG;
     if (!c->layout) return fail(c, PGH_E_STATE, "pgh_set_layout has not been called");
     if (!c->d_slab) return fail(c, PGH_E_STATE, "pgh_reserve has not been called");
-    if (c->dtype != dtype)
-        return fail(c, PGH_E_STATE, "slab holds dtype %d, call needs %d", c->dtype, dtype);
     return PGH_OK;
+}
+
+int check_dtype(pgh_ctx* c, int dtype) {
+    RC(check_ready(c));
+    if (c->dtype != dtype) return fail(c, PGH_E_STATE, "slab holds dtype %d, call needs %d", c->dtype, dtype);
+    return PGH_OK;
+}
+
+uint8_t* slot_row(pgh_ctx* c, int slot, int party) {
+    const size_t row = (size_t)slot * c->parties + party;
+    return (uint8_t*)c->d_slab + row * (size_t)c->ld * esize(c->dtype);
 }
 
 hipEvent_t take_event(pgh_ctx* c) {
@@ -154,6 +190,7 @@ int collect_timings(pgh_ctx* c) {
         c->st.kernel_ms_total += ms;
         c->st.kernel_launches += 1;
         c->st.kernel_bytes_last = t.bytes;
+        c->st.kernel_bytes_total += t.bytes;
         c->pool.push_back(t.a);
         c->pool.push_back(t.b);
     }
@@ -164,10 +201,7 @@ int collect_timings(pgh_ctx* c) {
 // Bracket a launch with an event pair on `s`.
 template <class F>
 int timed_launch(pgh_ctx* c, hipStream_t s, uint64_t bytes, F&& launch) {
-    if (c->pending.size() >= 4096) {
-        int rc = collect_timings(c);
-        if (rc) return rc;
-    }
+    if (c->pending.size() >= 4096) RC(collect_timings(c));
     hipEvent_t a = take_event(c), b = take_event(c);
     if (!a || !b) return fail(c, PGH_E_HIP, "hipEventCreate failed");
     CK(c, hipEventRecord(a, s));
@@ -181,93 +215,258 @@ int timed_launch(pgh_ctx* c, hipStream_t s, uint64_t bytes, F&& launch) {
     return PGH_OK;
 }
 
-// host -> HBM through the pinned ring on the copy stream
-int stage_h2d(pgh_ctx* c, void* dst, const uint8_t* src, size_t n) {
+void par_memcpy(uint8_t* dst, const uint8_t* src, size_t n, int threads) {
+    if (n < (8u << 20) || threads <= 1) { std::memcpy(dst, src, n); return; }
+    std::vector<std::thread> th;
+    const size_t part = ((n + threads - 1) / threads + 4095) & ~(size_t)4095;
+    for (int t = 0; t < threads; ++t) {
+        const size_t off = (size_t)t * part;
+        if (off >= n) break;
+        const size_t m = std::min(part, n - off);
+        th.emplace_back([=] { std::memcpy(dst + off, src + off, m); });
+    }
+    for (auto& x : th) x.join();
+}
+
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+    return attr.type == hipMemoryTypeHost;
+}
+
+// host bytes -> HBM on the copy stream.  Page-locked sources are DMA'd directly (the call
+// then waits for the copy: the caller's buffer is only borrowed); pageable sources go through
+// the pinned ring, so the host memcpy of one slot overlaps the DMA of the other.
+int stage_h2d(pgh_ctx* c, void* dst, const uint8_t* src, size_t n, bool pinned_src) {
     const double t0 = now_ms();
-    size_t off = 0;
-    while (off < n) {
-        const int slot = c->pin_next;
-        c->pin_next ^= 1;
-        if (c->pin_used[slot]) CK(c, hipEventSynchronize(c->pin_ev[slot]));
-        const size_t m = (n - off < c->pin_slot) ? (n - off) : c->pin_slot;
-        std::memcpy(c->h_pin[slot], src + off, m);
-        CK(c, hipMemcpyAsync((uint8_t*)dst + off, c->h_pin[slot], m, hipMemcpyHostToDevice, c->copy));
-        CK(c, hipEventRecord(c->pin_ev[slot], c->copy));
-        c->pin_used[slot] = true;
-        off += m;
+    if (pinned_src) {
+        CK(c, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->copy));
+        CK(c, hipStreamSynchronize(c->copy));
+    } else {
+        size_t off = 0;
+        while (off < n) {
+            const int slot = c->pin_next;
+            c->pin_next ^= 1;
+            if (c->pin_used[slot]) CK(c, hipEventSynchronize(c->pin_ev[slot]));
+            const size_t m = std::min(n - off, c->pin_slot);
+            par_memcpy(c->h_pin[slot], src + off, m, c->copy_threads);
+            CK(c, hipMemcpyAsync((uint8_t*)dst + off, c->h_pin[slot], m, hipMemcpyHostToDevice, c->copy));
+            CK(c, hipEventRecord(c->pin_ev[slot], c->copy));
+            c->pin_used[slot] = true;
+            off += m;
+        }
     }
     c->st.h2d_ms_total += now_ms() - t0;
     c->st.h2d_bytes_total += n;
     return PGH_OK;
 }
 
-// The reduction stream waits for every ingest copy issued so far.
+// Stream `s` waits for every ingest copy / synthetic fill issued so far.
 int order_after_ingest(pgh_ctx* c, hipStream_t s) {
     CK(c, hipEventRecord(c->copy_done, c->copy));
     CK(c, hipStreamWaitEvent(s, c->copy_done, 0));
     return PGH_OK;
 }
 
-int run_fedavg(pgh_ctx* c, int mode, const float* d_ckpt, float* d_out, hipStream_t s) {
-    int n = 0;
-    int rc = contiguous_clients(c, &n);
-    if (rc) return rc;
-    if (mode != PGH_MEAN && mode != PGH_ITERATIVE_MEAN && mode != PGH_WEIGHTED_MEAN)
-        return fail(c, PGH_E_ARG, "unknown averaging mode %d", mode);
-    float divisor = (float)n;  // th.div(sum, len(diffs)), cycle_manager.py:288
-    if (mode == PGH_WEIGHTED_MEAN) {
-        if ((int)c->weights.size() != n)
-            return fail(c, PGH_E_STATE, "weighted mean needs %d weights, have %zu", n, c->weights.size());
-        float t = c->weights[0];
-        for (int k = 1; k < n; ++k) t = t + c->weights[k];  // left fold, float32
-        if (!(t != 0.f)) return fail(c, PGH_E_ARG, "sum of weights is zero");
-        divisor = t;
-        CK(c, hipMemcpyAsync(c->d_w, c->weights.data(), sizeof(float) * n, hipMemcpyHostToDevice, s));
-    }
-    rc = order_after_ingest(c, s);
-    if (rc) return rc;
-    pgh::FedavgArgs a{};
-    a.diffs = (const float*)c->d_slab;
-    a.ld = c->ld;
-    a.n_rows = n;
-    a.client0 = 0;
-    a.p = c->pg;
-    a.weights = c->d_w;
-    a.acc = c->d_acc;
-    a.ckpt = d_ckpt;
-    a.out = d_out;
-    a.divisor = divisor;
-    a.flags = pgh::FL_FIRST | pgh::FL_FINAL;
-    a.mode = mode;
-    a.variant = c->variant;
-    const uint64_t bytes = 4ull * (uint64_t)n * (uint64_t)c->pg + 8ull * (uint64_t)c->pg;
-    return timed_launch(c, s, bytes, [&] { return pgh::launch_fedavg(a, s); });
+// Before the copy stream overwrites a slot, it waits for the last fold that read slots.
+int order_before_overwrite(pgh_ctx* c) {
+    if (c->fold_pending) CK(c, hipStreamWaitEvent(c->copy, c->fold_done, 0));
+    return PGH_OK;
 }
 
-int run_secagg(pgh_ctx* c, int base, int prec, int64_t* d_sum, float* d_dec, hipStream_t s) {
-    int n = 0;
-    int rc = contiguous_clients(c, &n);
-    if (rc) return rc;
+int sync_weights(pgh_ctx* c, hipStream_t s) {
+    if (c->weights_on_device || c->weights.empty()) return PGH_OK;
+    if (c->weights.size() > c->w_cap) {
+        (void)hipFree(c->d_w);
+        c->d_w = nullptr;
+        c->w_cap = 0;
+        if (hipMalloc((void**)&c->d_w, sizeof(float) * c->weights.size()) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(c, PGH_E_OOM, "weight vector allocation failed");
+        }
+        c->w_cap = c->weights.size();
+    }
+    CK(c, hipMemcpyAsync(c->d_w, c->weights.data(), sizeof(float) * c->weights.size(), hipMemcpyHostToDevice, s));
+    CK(c, hipStreamSynchronize(s));  // c->weights may change after return
+    c->weights_on_device = true;
+    return PGH_OK;
+}
+
+int fixed_point_divisor(pgh_ctx* c, int base, int prec, float* div) {
     if (base < 2 || prec < 0 || prec > 18) return fail(c, PGH_E_ARG, "bad fixed-point base %d / precision %d", base, prec);
     long double scale = 1;
     for (int k = 0; k < prec; ++k) scale *= base;
     if (scale > 9.2e18L) return fail(c, PGH_E_ARG, "base**prec overflows int64");
-    rc = order_after_ingest(c, s);
-    if (rc) return rc;
-    pgh::SecaggArgs a{};
-    a.shares = (const int64_t*)c->d_slab;
-    a.ld = c->ld;
-    a.n_rows = n * c->parties;
-    a.p = c->pg;
-    a.acc = c->d_uacc;
-    a.sum_out = d_sum;
-    a.dec_out = d_dec;
-    a.divisor = (float)(int64_t)scale;  // python int base**prec, promoted to float32
-    a.flags = pgh::FL_FIRST | pgh::FL_FINAL;
-    a.variant = c->variant;
-    const uint64_t bytes = 8ull * (uint64_t)a.n_rows * (uint64_t)c->pg + (d_sum ? 8ull * c->pg : 0) +
-                           (d_dec ? 4ull * c->pg : 0);
-    return timed_launch(c, s, bytes, [&] { return pgh::launch_secagg(a, s); });
+    *div = (float)(int64_t)scale;  // python int base**prec, promoted to float32 by the division
+    return PGH_OK;
+}
+
+float weight_total(const std::vector<float>& w, int64_t n) {  // left fold, float32
+    float t = w[0];
+    for (int64_t k = 1; k < n; ++k) t = t + w[k];
+    return t;
+}
+
+// Fold slots holding clients [c0, c0 + n) (slot order may wrap) into the running state.
+// FIRST when c0 == 0; FINAL writes out (fedavg: ckpt - avg; secagg: sum/dec) instead of the state.
+struct FinalArgs {
+    const float* ckpt = nullptr;
+    float* out = nullptr;
+    int64_t* sum = nullptr;
+    float* dec = nullptr;
+    float divisor = 1.f;
+};
+
+int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const FinalArgs& fa, hipStream_t s) {
+    RC(order_after_ingest(c, s));
+    if (kind == PGH_WEIGHTED_MEAN && n > 0) {
+        if ((int64_t)c->weights.size() < c0 + n)
+            return fail(c, PGH_E_STATE, "weighted mean: %zu weights for %lld clients", c->weights.size(),
+                        (long long)(c0 + n));
+        RC(sync_weights(c, s));
+    }
+    const int R = c->slots;
+    int64_t done = 0;
+    do {
+        const int slot = (int)((c0 + done) % R);
+        const int64_t seg = std::min<int64_t>(n - done, (int64_t)(R - slot));
+        const bool first = (c0 + done == 0);
+        const bool last = (done + seg == n);
+        const int flags = (first ? pgh::FL_FIRST : 0) | (final && last ? pgh::FL_FINAL : 0);
+        const uint64_t pg = (uint64_t)c->pg;
+        if (kind == KIND_SECAGG) {
+            pgh::SecaggArgs a{};
+            a.shares = (const int64_t*)slot_row(c, slot, 0);
+            a.ld = c->ld;
+            a.n_rows = (int)(seg * c->parties);
+            a.p = c->pg;
+            a.acc = c->d_uacc;
+            a.sum_out = fa.sum;
+            a.dec_out = fa.dec;
+            a.divisor = fa.divisor;
+            a.flags = flags;
+            a.variant = c->variant;
+            const uint64_t bytes = 8ull * (uint64_t)a.n_rows * pg + (first ? 0 : 8 * pg) +
+                                   ((flags & pgh::FL_FINAL) ? (fa.sum ? 8 * pg : 0) + (fa.dec ? 4 * pg : 0) : 8 * pg);
+            RC(timed_launch(c, s, bytes, [&] { return pgh::launch_secagg(a, s); }));
+        } else {
+            pgh::FedavgArgs a{};
+            a.diffs = (const float*)slot_row(c, slot, 0);
+            a.ld = c->ld;
+            a.n_rows = (int)seg;
+            a.client0 = c0 + done;
+            a.p = c->pg;
+            a.weights = c->d_w ? c->d_w + (c0 + done) : nullptr;
+            a.acc = c->d_acc;
+            a.ckpt = fa.ckpt;
+            a.out = fa.out;
+            a.divisor = fa.divisor;
+            a.flags = flags;
+            a.mode = kind;
+            a.variant = c->variant;
+            const uint64_t bytes = 4ull * (uint64_t)seg * pg + (first ? 0 : 4 * pg) +
+                                   ((flags & pgh::FL_FINAL) ? 8 * pg : 4 * pg);
+            RC(timed_launch(c, s, bytes, [&] { return pgh::launch_fedavg(a, s); }));
+        }
+        done += seg;
+    } while (done < n);
+    CK(c, hipEventRecord(c->fold_done, s));
+    c->fold_pending = true;
+    return PGH_OK;
+}
+
+// Length of the run of ingested clients starting at `from` (slot ring order).
+int64_t ready_run(pgh_ctx* c, int64_t from) {
+    int64_t n = 0;
+    while (n < c->slots && c->slot_client[(size_t)((from + n) % c->slots)] == from + n) ++n;
+    return n;
+}
+
+// Every ingested client must belong to the contiguous run starting at `from`.
+int check_no_gaps(pgh_ctx* c, int64_t from, int64_t run) {
+    for (int s = 0; s < c->slots; ++s) {
+        const int64_t k = c->slot_client[(size_t)s];
+        if (k >= 0 && (k < from || k >= from + run))
+            return fail(c, PGH_E_STATE, "client %lld is missing but client %lld was ingested",
+                        (long long)(from + run), (long long)k);
+    }
+    return PGH_OK;
+}
+
+// STREAM: fold the ready run when it reaches the batch size (or always, when forced).
+int maybe_fold(pgh_ctx* c, bool force) {
+    const int64_t run = ready_run(c, c->folded);
+    if (run == 0 || (!force && run < c->fold_batch)) return PGH_OK;
+    RC(fold_run(c, c->kind, c->folded, run, false, FinalArgs{}, c->stream));
+    for (int64_t k = 0; k < run; ++k) c->slot_client[(size_t)((c->folded + k) % c->slots)] = -1;
+    c->folded += run;
+    c->st.n_folded = c->folded;
+    return PGH_OK;
+}
+
+// Claim the slot for `client` (both modes) before bytes are written to it.
+int claim_slot(pgh_ctx* c, int64_t client, int* slot_out) {
+    if (client < 0) return fail(c, PGH_E_ARG, "negative client index");
+    if (!c->streaming) {
+        if (client >= c->slots)
+            return fail(c, PGH_E_ARG, "client %lld outside slab capacity %d", (long long)client, c->slots);
+        *slot_out = (int)client;
+        return PGH_OK;
+    }
+    if (client < c->folded) return fail(c, PGH_E_STATE, "client %lld was already folded", (long long)client);
+    const int slot = (int)(client % c->slots);
+    const int64_t held = c->slot_client[(size_t)slot];
+    if (held >= 0 && held != client)
+        return fail(c, PGH_E_STATE, "ring full: slot %d still holds unfolded client %lld (fold front %lld)", slot,
+                    (long long)held, (long long)c->folded);
+    RC(order_before_overwrite(c));
+    *slot_out = slot;
+    return PGH_OK;
+}
+
+int mark_ingested(pgh_ctx* c, int64_t client, int slot) {
+    if (c->slot_client[(size_t)slot] != client) c->st.n_clients += 1;
+    c->slot_client[(size_t)slot] = client;
+    return c->streaming ? maybe_fold(c, false) : PGH_OK;
+}
+
+// RESIDENT: clients [0, n) all present, nothing else.
+int resident_count(pgh_ctx* c, int64_t* n_out) {
+    if (c->streaming) return fail(c, PGH_E_STATE, "context is streaming: finish with pgh_stream_finish*");
+    int64_t n = ready_run(c, 0);
+    RC(check_no_gaps(c, 0, n));
+    if (n == 0) return fail(c, PGH_E_STATE, "no diffs ingested");
+    *n_out = n;
+    return PGH_OK;
+}
+
+int fedavg_divisor(pgh_ctx* c, int mode, int64_t n, float* div) {
+    if (mode == PGH_WEIGHTED_MEAN) {
+        if ((int64_t)c->weights.size() < n)
+            return fail(c, PGH_E_STATE, "weighted mean needs %lld weights, have %zu", (long long)n, c->weights.size());
+        const float t = weight_total(c->weights, n);
+        if (!(t != 0.f)) return fail(c, PGH_E_ARG, "sum of weights is zero");
+        *div = t;
+    } else {
+        *div = (float)n;  // th.div(sum, len(diffs)), cycle_manager.py:288
+    }
+    return PGH_OK;
+}
+
+bool valid_mode(int m) { return m == PGH_MEAN || m == PGH_ITERATIVE_MEAN || m == PGH_WEIGHTED_MEAN; }
+
+// caller stream `cs` -> context stream ordering, and back
+int join_in(pgh_ctx* c, hipStream_t cs) {
+    if (cs == c->stream) return PGH_OK;
+    CK(c, hipEventRecord(c->xsync, cs));
+    CK(c, hipStreamWaitEvent(c->stream, c->xsync, 0));
+    return PGH_OK;
+}
+int join_out(pgh_ctx* c, hipStream_t cs) {
+    if (cs == c->stream) return PGH_OK;
+    CK(c, hipEventRecord(c->xsync, c->stream));
+    CK(c, hipStreamWaitEvent(cs, c->xsync, 0));
+    return PGH_OK;
 }
 
 }  // namespace
@@ -287,6 +486,22 @@ int pgh_device_count(int* n) {
 
 const char* pgh_last_error(const pgh_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
+int pgh_host_alloc(size_t bytes, void** out) {
+    if (!out || !bytes) return fail(nullptr, PGH_E_ARG, "bad pinned allocation request");
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        *out = nullptr;
+        return fail(nullptr, PGH_E_OOM, "pinned host allocation of %zu bytes failed", bytes);
+    }
+    return PGH_OK;
+}
+
+int pgh_host_free(void* p) {
+    if (p && hipHostFree(p) != hipSuccess) return fail(nullptr, PGH_E_HIP, "hipHostFree failed");
+    return PGH_OK;
+}
+
 int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (!out) return fail(nullptr, PGH_E_ARG, "out is NULL");
     *out = nullptr;
@@ -300,9 +515,13 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (pinned_bytes == 0) pinned_bytes = 256ull << 20;
     c->pin_slot = (pinned_bytes / 2) & ~(size_t)4095;
     if (c->pin_slot < 4096) c->pin_slot = 4096;
+    const unsigned hw = std::thread::hardware_concurrency();
+    c->copy_threads = (int)std::max(1u, std::min(8u, hw ? hw : 1u));
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&c->fold_done, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&c->xsync, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->pin_ev[0], hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->pin_ev[1], hipEventDisableTiming) == hipSuccess;
     if (!ok) { pgh_destroy(c); return fail(nullptr, PGH_E_HIP, "stream/event creation failed"); }
@@ -318,8 +537,6 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
 void pgh_destroy(pgh_ctx* c) {
     if (!c) return;
     DeviceGuard g(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->copy) (void)hipStreamSynchronize(c->copy);
     free_slab(c);
     for (auto& t : c->pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto e : c->pool) (void)hipEventDestroy(e);
@@ -327,7 +544,8 @@ void pgh_destroy(pgh_ctx* c) {
         if (c->h_pin[k]) (void)hipHostFree(c->h_pin[k]);
         if (c->pin_ev[k]) (void)hipEventDestroy(c->pin_ev[k]);
     }
-    if (c->copy_done) (void)hipEventDestroy(c->copy_done);
+    for (hipEvent_t e : {c->copy_done, c->fold_done, c->xsync})
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
     delete c;
@@ -353,8 +571,8 @@ int pgh_set_layout(pgh_ctx* c, int n_tensors, const int64_t* numel) {
 int pgh_set_shard(pgh_ctx* c, int64_t lo, int64_t hi) {
     if (!c) return PGH_E_ARG;
     if (!c->layout) return fail(c, PGH_E_STATE, "pgh_set_layout has not been called");
-    if (lo < 0 || hi > c->P || lo >= hi) return fail(c, PGH_E_ARG, "shard [%lld,%lld) outside [0,%lld)",
-                                                    (long long)lo, (long long)hi, (long long)c->P);
+    if (lo < 0 || hi > c->P || lo >= hi)
+        return fail(c, PGH_E_ARG, "shard [%lld,%lld) outside [0,%lld)", (long long)lo, (long long)hi, (long long)c->P);
     DeviceGuard g(c->device);
     free_slab(c);
     c->lo = lo;
@@ -375,115 +593,137 @@ int pgh_reserve(pgh_ctx* c, int max_clients, int dtype, int n_parties) {
     if (n_parties < 1) return fail(c, PGH_E_ARG, "n_parties must be >= 1");
     DeviceGuard g(c->device);
     free_slab(c);
-    const size_t esz = dtype == PGH_F32 ? 4 : 8;
     const size_t rows = (size_t)max_clients * (size_t)n_parties;
-    const size_t bytes = rows * (size_t)c->ld * esz;
+    const size_t bytes = rows * (size_t)c->ld * esize(dtype);
     if (hipMalloc(&c->d_slab, bytes) != hipSuccess) {
         c->d_slab = nullptr;
         (void)hipGetLastError();
         return fail(c, PGH_E_OOM, "slab allocation of %zu bytes (%zu rows x %lld) failed", bytes, rows, (long long)c->ld);
     }
     c->slab_bytes = bytes;
-    c->vec_cap = (size_t)c->ld;
-    const size_t v4 = c->vec_cap * 4, v8 = c->vec_cap * 8;
+    const size_t v4 = (size_t)c->ld * 4, v8 = (size_t)c->ld * 8;
     bool ok = hipMalloc((void**)&c->d_ckpt, v4) == hipSuccess && hipMalloc((void**)&c->d_out, v4) == hipSuccess &&
               hipMalloc((void**)&c->d_acc, v4) == hipSuccess && hipMalloc((void**)&c->d_uacc, v8) == hipSuccess &&
-              hipMalloc((void**)&c->d_sum, v8) == hipSuccess && hipMalloc((void**)&c->d_dec, v4) == hipSuccess &&
-              hipMalloc((void**)&c->d_w, sizeof(float) * (size_t)max_clients) == hipSuccess;
+              hipMalloc((void**)&c->d_sum, v8) == hipSuccess && hipMalloc((void**)&c->d_dec, v4) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
         free_slab(c);
         return fail(c, PGH_E_OOM, "device vector allocation failed");
     }
-    c->max_clients = max_clients;
+    c->slots = max_clients;
     c->dtype = dtype;
     c->parties = n_parties;
-    c->have.assign((size_t)max_clients, 0);
+    c->slot_client.assign((size_t)max_clients, -1);
     c->weights.clear();
+    c->weights_on_device = false;
     c->st.max_clients = max_clients;
     c->st.n_clients = 0;
+    c->st.n_folded = 0;
     return PGH_OK;
 }
 
 int pgh_reset(pgh_ctx* c) {
     if (!c) return PGH_E_ARG;
-    std::fill(c->have.begin(), c->have.end(), 0);
+    DeviceGuard g(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    std::fill(c->slot_client.begin(), c->slot_client.end(), -1);
     c->weights.clear();
+    c->weights_on_device = false;
+    c->streaming = false;
+    c->folded = 0;
+    c->fold_pending = false;
     c->st.n_clients = 0;
+    c->st.n_folded = 0;
     return PGH_OK;
 }
 
 int pgh_ingest_raw(pgh_ctx* c, int client, const void* flat, size_t nbytes, int dtype) {
-    int rc = check_ready(c, dtype);
-    if (rc) return rc;
+    RC(check_dtype(c, dtype));
     if (!flat) return fail(c, PGH_E_ARG, "flat is NULL");
-    if (client < 0 || client >= c->max_clients)
-        return fail(c, PGH_E_ARG, "client %d outside slab capacity %d", client, c->max_clients);
-    const size_t esz = dtype == PGH_F32 ? 4 : 8;
-    const size_t want = (size_t)c->P * esz * (size_t)c->parties;
+    const size_t es = esize(dtype);
+    const size_t want = (size_t)c->P * es * (size_t)c->parties;
     if (nbytes != want) return fail(c, PGH_E_ARG, "client %d: got %zu bytes, layout needs %zu", client, nbytes, want);
     DeviceGuard g(c->device);
+    int slot = 0;
+    RC(claim_slot(c, client, &slot));
+    const bool pinned = is_pinned(flat);
     const uint8_t* src = (const uint8_t*)flat;
-    for (int s = 0; s < c->parties; ++s) {
-        const size_t row = (size_t)client * c->parties + s;
-        uint8_t* dst = (uint8_t*)c->d_slab + row * (size_t)c->ld * esz;
-        rc = stage_h2d(c, dst, src + ((size_t)s * c->P + c->lo) * esz, (size_t)c->pg * esz);
-        if (rc) return rc;
-    }
-    if (!c->have[client]) c->st.n_clients += 1;
-    c->have[client] = 1;
-    return PGH_OK;
+    for (int s = 0; s < c->parties; ++s)
+        RC(stage_h2d(c, slot_row(c, slot, s), src + ((size_t)s * c->P + c->lo) * es, (size_t)c->pg * es, pinned));
+    return mark_ingested(c, client, slot);
 }
 
 int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
-    int rc = check_ready(c, PGH_F32);
-    if (rc) return rc;
+    RC(check_dtype(c, PGH_F32));
     if (!pb && n) return fail(c, PGH_E_ARG, "pb is NULL");
-    if (client < 0 || client >= c->max_clients)
-        return fail(c, PGH_E_ARG, "client %d outside slab capacity %d", client, c->max_clients);
     c->scratch.resize((size_t)c->P);
     std::string msg;
-    rc = pgh_state::decode_f32(pb, n, c->numel, c->scratch.data(), &msg);
+    int rc = pgh_state::decode_f32(pb, n, c->numel, c->scratch.data(), &msg);
     if (rc) return fail(c, rc, "client %d State: %s", client, msg.c_str());
     return pgh_ingest_raw(c, client, c->scratch.data(), (size_t)c->P * 4, PGH_F32);
 }
 
-int pgh_synth_fill(pgh_ctx* c, uint64_t seed, int n_clients) {
-    int rc = check_ready(c, c ? c->dtype : 0);
-    if (rc) return rc;
-    if (n_clients <= 0 || n_clients > c->max_clients)
-        return fail(c, PGH_E_ARG, "n_clients %d outside (0,%d]", n_clients, c->max_clients);
+int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
+    RC(check_ready(c));
+    if (n <= 0 || client0 < 0) return fail(c, PGH_E_ARG, "bad client range %d + %d", client0, n);
     DeviceGuard g(c->device);
-    hipError_t e;
-    if (c->dtype == PGH_F32)
-        e = pgh::launch_synth_f32((float*)c->d_slab, n_clients, c->ld, c->pg, seed, pgh::STREAM_DIFF, 0, c->lo,
-                                  pgh::DIFF_SCALE, c->copy);
-    else
-        e = pgh::launch_synth_shares((int64_t*)c->d_slab, n_clients, c->parties, c->ld, c->pg, seed, 0, c->lo,
-                                     1000.0f, c->copy);
-    if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic fill failed: %s", hipGetErrorString(e));
-    for (int k = 0; k < n_clients; ++k) c->have[k] = 1;
-    for (int k = n_clients; k < c->max_clients; ++k) c->have[k] = 0;
-    c->st.n_clients = n_clients;
+    int k = 0;
+    while (k < n) {
+        const int64_t client = (int64_t)client0 + k;
+        int slot = 0;
+        RC(claim_slot(c, client, &slot));
+        // contiguous run of slots from `slot`, all claimable
+        int run = 1;
+        while (k + run < n && slot + run < c->slots) {
+            const int64_t cl = client + run;
+            if (c->streaming) {
+                const int64_t held = c->slot_client[(size_t)(slot + run)];
+                if (held >= 0 && held != cl) break;
+            } else if (cl >= c->slots) {
+                break;
+            }
+            ++run;
+        }
+        hipError_t e;
+        if (c->dtype == PGH_F32)
+            e = pgh::launch_synth_f32((float*)slot_row(c, slot, 0), run, c->ld, c->pg, seed, pgh::STREAM_DIFF, client,
+                                      c->lo, pgh::DIFF_SCALE, c->copy);
+        else
+            e = pgh::launch_synth_shares((int64_t*)slot_row(c, slot, 0), run, c->parties, c->ld, c->pg, seed, client,
+                                         c->lo, 1000.0f, c->copy);
+        if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic fill failed: %s", hipGetErrorString(e));
+        for (int j = 0; j < run; ++j) {
+            if (c->slot_client[(size_t)(slot + j)] != client + j) c->st.n_clients += 1;
+            c->slot_client[(size_t)(slot + j)] = client + j;
+        }
+        if (c->streaming) RC(maybe_fold(c, false));
+        k += run;
+    }
     return PGH_OK;
+}
+
+int pgh_synth_fill(pgh_ctx* c, uint64_t seed, int n_clients) {
+    RC(check_ready(c));
+    if (c->streaming) return fail(c, PGH_E_STATE, "pgh_synth_fill is for resident slabs; use pgh_synth_ingest");
+    if (n_clients <= 0 || n_clients > c->slots)
+        return fail(c, PGH_E_ARG, "n_clients %d outside (0,%d]", n_clients, c->slots);
+    RC(pgh_reset(c));
+    return pgh_synth_ingest(c, seed, 0, n_clients);
 }
 
 int pgh_synth_ckpt_device(pgh_ctx* c, uint64_t seed, float* d_ckpt, void* stream) {
     if (!c) return PGH_E_ARG;
     if (!c->layout) return fail(c, PGH_E_STATE, "pgh_set_layout has not been called");
-    if (!d_ckpt) return fail(c, PGH_E_ARG, "d_ckpt is NULL");
+    if (!d_ckpt || ((uintptr_t)d_ckpt & 15)) return fail(c, PGH_E_ARG, "d_ckpt must be a 16-byte aligned device pointer");
     DeviceGuard g(c->device);
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    // one row of exactly P_shard elements (ld = P_shard rounded to 4 would overrun the buffer)
-    if (c->pg % 4 == 0) {
-        hipError_t e = pgh::launch_synth_f32(d_ckpt, 1, c->pg, c->pg, seed, pgh::STREAM_CKPT, 0, c->lo,
-                                             pgh::CKPT_SCALE, s);
+    if (c->pg % 4 == 0) {  // one row of exactly P_shard elements
+        hipError_t e = pgh::launch_synth_f32(d_ckpt, 1, c->pg, c->pg, seed, pgh::STREAM_CKPT, 0, c->lo, pgh::CKPT_SCALE, s);
         if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic checkpoint failed: %s", hipGetErrorString(e));
         return PGH_OK;
     }
     if (!c->d_ckpt) return fail(c, PGH_E_STATE, "pgh_reserve has not been called");
-    hipError_t e = pgh::launch_synth_f32(c->d_ckpt, 1, c->ld, c->pg, seed, pgh::STREAM_CKPT, 0, c->lo,
-                                         pgh::CKPT_SCALE, s);
+    hipError_t e = pgh::launch_synth_f32(c->d_ckpt, 1, c->ld, c->pg, seed, pgh::STREAM_CKPT, 0, c->lo, pgh::CKPT_SCALE, s);
     if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic checkpoint failed: %s", hipGetErrorString(e));
     CK(c, hipMemcpyAsync(d_ckpt, c->d_ckpt, sizeof(float) * c->pg, hipMemcpyDeviceToDevice, s));
     return PGH_OK;
@@ -492,30 +732,43 @@ int pgh_synth_ckpt_device(pgh_ctx* c, uint64_t seed, float* d_ckpt, void* stream
 int pgh_set_weights(pgh_ctx* c, const float* w, int n) {
     if (!c) return PGH_E_ARG;
     if (!w || n <= 0) return fail(c, PGH_E_ARG, "need a non-empty weight vector");
-    if (n > c->max_clients) return fail(c, PGH_E_ARG, "%d weights for a %d-client slab", n, c->max_clients);
+    if (c->streaming && c->folded > 0) {
+        for (int64_t k = 0; k < c->folded && k < n && k < (int64_t)c->weights.size(); ++k)
+            if (std::memcmp(&w[k], &c->weights[(size_t)k], 4) != 0)
+                return fail(c, PGH_E_STATE, "weight of already folded client %lld changed", (long long)k);
+        if (n < c->folded) return fail(c, PGH_E_STATE, "fewer weights than folded clients");
+    }
     c->weights.assign(w, w + n);
+    c->weights_on_device = false;
     return PGH_OK;
 }
 
+// ---- RESIDENT reductions -------------------------------------------------------------------------
+
 int pgh_fedavg_device(pgh_ctx* c, int mode, const float* d_ckpt, float* d_out, void* stream) {
-    int rc = check_ready(c, PGH_F32);
-    if (rc) return rc;
+    RC(check_dtype(c, PGH_F32));
+    if (!valid_mode(mode)) return fail(c, PGH_E_ARG, "unknown averaging mode %d", mode);
     if (!d_ckpt || !d_out) return fail(c, PGH_E_ARG, "d_ckpt / d_out is NULL");
     if (((uintptr_t)d_ckpt | (uintptr_t)d_out) & 15) return fail(c, PGH_E_ARG, "device buffers must be 16-byte aligned");
     DeviceGuard g(c->device);
-    return run_fedavg(c, mode, d_ckpt, d_out, stream ? (hipStream_t)stream : c->stream);
+    int64_t n = 0;
+    RC(resident_count(c, &n));
+    FinalArgs fa;
+    fa.ckpt = d_ckpt;
+    fa.out = d_out;
+    RC(fedavg_divisor(c, mode, n, &fa.divisor));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return fold_run(c, mode, 0, n, true, fa, s);
 }
 
 int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
-    int rc = check_ready(c, PGH_F32);
-    if (rc) return rc;
+    RC(check_dtype(c, PGH_F32));
     if (!ckpt || !out) return fail(c, PGH_E_ARG, "ckpt / out is NULL");
     DeviceGuard g(c->device);
     const double t0 = now_ms();
     const size_t bytes = sizeof(float) * (size_t)c->pg;
     CK(c, hipMemcpyAsync(c->d_ckpt, ckpt, bytes, hipMemcpyHostToDevice, c->stream));
-    rc = run_fedavg(c, mode, c->d_ckpt, c->d_out, c->stream);
-    if (rc) return rc;
+    RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
     CK(c, hipMemcpyAsync(out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
     c->st.close_ms_last = now_ms() - t0;
@@ -523,25 +776,121 @@ int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
 }
 
 int pgh_secagg_device(pgh_ctx* c, int base, int prec, int64_t* d_sum, float* d_dec, void* stream) {
-    int rc = check_ready(c, PGH_I64);
-    if (rc) return rc;
+    RC(check_dtype(c, PGH_I64));
     DeviceGuard g(c->device);
-    return run_secagg(c, base, prec, d_sum, d_dec, stream ? (hipStream_t)stream : c->stream);
+    int64_t n = 0;
+    RC(resident_count(c, &n));
+    FinalArgs fa;
+    fa.sum = d_sum;
+    fa.dec = d_dec;
+    RC(fixed_point_divisor(c, base, prec, &fa.divisor));
+    return fold_run(c, KIND_SECAGG, 0, n, true, fa, stream ? (hipStream_t)stream : c->stream);
 }
 
 int pgh_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out) {
-    int rc = check_ready(c, PGH_I64);
-    if (rc) return rc;
+    RC(check_dtype(c, PGH_I64));
     DeviceGuard g(c->device);
     const double t0 = now_ms();
-    rc = run_secagg(c, base, prec, sum_out ? c->d_sum : nullptr, dec_out ? c->d_dec : nullptr, c->stream);
-    if (rc) return rc;
+    RC(pgh_secagg_device(c, base, prec, sum_out ? c->d_sum : nullptr, dec_out ? c->d_dec : nullptr, c->stream));
     if (sum_out) CK(c, hipMemcpyAsync(sum_out, c->d_sum, 8ull * c->pg, hipMemcpyDeviceToHost, c->stream));
     if (dec_out) CK(c, hipMemcpyAsync(dec_out, c->d_dec, 4ull * c->pg, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
     c->st.close_ms_last = now_ms() - t0;
     return collect_timings(c);
 }
+
+// ---- STREAM reductions ---------------------------------------------------------------------------
+
+int pgh_stream_begin(pgh_ctx* c, int kind, int fold_batch) {
+    RC(check_ready(c));
+    if (kind == PGH_STREAM_SECAGG) {
+        if (c->dtype != PGH_I64) return fail(c, PGH_E_STATE, "secagg stream needs an int64 slab");
+    } else if (!valid_mode(kind) || c->dtype != PGH_F32) {
+        return fail(c, PGH_E_ARG, "stream kind %d does not match the slab", kind);
+    }
+    DeviceGuard g(c->device);
+    RC(pgh_reset(c));
+    c->streaming = true;
+    c->kind = kind == PGH_STREAM_SECAGG ? KIND_SECAGG : kind;
+    c->fold_batch = fold_batch <= 0 ? std::max(1, c->slots / 2) : std::min(fold_batch, c->slots);
+    return PGH_OK;
+}
+
+int pgh_stream_flush(pgh_ctx* c) {
+    RC(check_ready(c));
+    if (!c->streaming) return fail(c, PGH_E_STATE, "not streaming");
+    DeviceGuard g(c->device);
+    return maybe_fold(c, true);
+}
+
+namespace {
+int stream_finish(pgh_ctx* c, FinalArgs fa, hipStream_t cs, bool fedavg, int mode_or_base) {
+    if (!c->streaming) return fail(c, PGH_E_STATE, "not streaming (call pgh_stream_begin first)");
+    const int64_t run = ready_run(c, c->folded);
+    RC(check_no_gaps(c, c->folded, run));
+    const int64_t n = c->folded + run;
+    if (n == 0) return fail(c, PGH_E_STATE, "no diffs ingested");
+    if (fedavg) RC(fedavg_divisor(c, mode_or_base, n, &fa.divisor));
+    RC(join_in(c, cs));
+    RC(fold_run(c, c->kind, c->folded, run, true, fa, c->stream));
+    RC(join_out(c, cs));
+    for (int64_t k = 0; k < run; ++k) c->slot_client[(size_t)((c->folded + k) % c->slots)] = -1;
+    c->folded = n;
+    c->st.n_folded = n;
+    c->streaming = false;
+    return PGH_OK;
+}
+}  // namespace
+
+int pgh_stream_finish_device(pgh_ctx* c, const float* d_ckpt, float* d_out, void* stream) {
+    RC(check_dtype(c, PGH_F32));
+    if (!d_ckpt || !d_out || (((uintptr_t)d_ckpt | (uintptr_t)d_out) & 15))
+        return fail(c, PGH_E_ARG, "d_ckpt / d_out must be 16-byte aligned device pointers");
+    DeviceGuard g(c->device);
+    FinalArgs fa;
+    fa.ckpt = d_ckpt;
+    fa.out = d_out;
+    return stream_finish(c, fa, stream ? (hipStream_t)stream : c->stream, true, c->kind);
+}
+
+int pgh_stream_finish(pgh_ctx* c, const float* ckpt, float* out) {
+    RC(check_dtype(c, PGH_F32));
+    if (!ckpt || !out) return fail(c, PGH_E_ARG, "ckpt / out is NULL");
+    DeviceGuard g(c->device);
+    const double t0 = now_ms();
+    const size_t bytes = sizeof(float) * (size_t)c->pg;
+    CK(c, hipMemcpyAsync(c->d_ckpt, ckpt, bytes, hipMemcpyHostToDevice, c->stream));
+    RC(pgh_stream_finish_device(c, c->d_ckpt, c->d_out, c->stream));
+    CK(c, hipMemcpyAsync(out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
+    CK(c, hipStreamSynchronize(c->stream));
+    c->st.close_ms_last = now_ms() - t0;
+    return collect_timings(c);
+}
+
+int pgh_stream_finish_secagg_device(pgh_ctx* c, int base, int prec, int64_t* d_sum, float* d_dec, void* stream) {
+    RC(check_dtype(c, PGH_I64));
+    DeviceGuard g(c->device);
+    FinalArgs fa;
+    fa.sum = d_sum;
+    fa.dec = d_dec;
+    RC(fixed_point_divisor(c, base, prec, &fa.divisor));
+    return stream_finish(c, fa, stream ? (hipStream_t)stream : c->stream, false, base);
+}
+
+int pgh_stream_finish_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out) {
+    RC(check_dtype(c, PGH_I64));
+    DeviceGuard g(c->device);
+    const double t0 = now_ms();
+    RC(pgh_stream_finish_secagg_device(c, base, prec, sum_out ? c->d_sum : nullptr, dec_out ? c->d_dec : nullptr,
+                                       c->stream));
+    if (sum_out) CK(c, hipMemcpyAsync(sum_out, c->d_sum, 8ull * c->pg, hipMemcpyDeviceToHost, c->stream));
+    if (dec_out) CK(c, hipMemcpyAsync(dec_out, c->d_dec, 4ull * c->pg, hipMemcpyDeviceToHost, c->stream));
+    CK(c, hipStreamSynchronize(c->stream));
+    c->st.close_ms_last = now_ms() - t0;
+    return collect_timings(c);
+}
+
+// ---- observability -------------------------------------------------------------------------------
 
 int pgh_set_variant(pgh_ctx* c, int variant) {
     if (!c) return PGH_E_ARG;
@@ -553,8 +902,7 @@ int pgh_set_variant(pgh_ctx* c, int variant) {
 int pgh_stats(pgh_ctx* c, pgh_stats_t* out) {
     if (!c || !out) return PGH_E_ARG;
     DeviceGuard g(c->device);
-    int rc = collect_timings(c);
-    if (rc) return rc;
+    RC(collect_timings(c));
     *out = c->st;
     return PGH_OK;
 }
@@ -562,12 +910,14 @@ int pgh_stats(pgh_ctx* c, pgh_stats_t* out) {
 int pgh_reset_stats(pgh_ctx* c) {
     if (!c) return PGH_E_ARG;
     DeviceGuard g(c->device);
-    int rc = collect_timings(c);
-    if (rc) return rc;
-    const int64_t pg = c->st.p_shard, ld = c->st.ld;
-    const int32_t n = c->st.n_clients, m = c->st.max_clients;
+    RC(collect_timings(c));
+    pgh_stats_t keep = c->st;
     c->st = pgh_stats_t{};
-    c->st.p_shard = pg; c->st.ld = ld; c->st.n_clients = n; c->st.max_clients = m;
+    c->st.p_shard = keep.p_shard;
+    c->st.ld = keep.ld;
+    c->st.n_clients = keep.n_clients;
+    c->st.max_clients = keep.max_clients;
+    c->st.n_folded = keep.n_folded;
     return PGH_OK;
 }
 
@@ -575,6 +925,14 @@ int pgh_slab(pgh_ctx* c, void** d_slab, int64_t* ld) {
     if (!c || !d_slab || !ld) return PGH_E_ARG;
     *d_slab = c->d_slab;
     *ld = c->ld;
+    return PGH_OK;
+}
+
+int pgh_sync(pgh_ctx* c) {
+    if (!c) return PGH_E_ARG;
+    DeviceGuard g(c->device);
+    CK(c, hipStreamSynchronize(c->copy));
+    CK(c, hipStreamSynchronize(c->stream));
     return PGH_OK;
 }
 

@@ -15,6 +15,7 @@ from . import _lib
 from .exceptions import AggregationError, EngineUnavailableError, StateParseError
 
 MEAN, ITERATIVE_MEAN, WEIGHTED_MEAN = 0, 1, 2
+STREAM_SECAGG = 16
 F32, I64 = 0, 1
 MODE_NAMES = {MEAN: "mean", ITERATIVE_MEAN: "iterative_mean", WEIGHTED_MEAN: "weighted_mean"}
 
@@ -29,6 +30,32 @@ def device_count() -> int:
 
 def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
+
+
+class PinnedBuffer:
+    """Page-locked host memory (pgh_host_alloc) viewed as a numpy array; ingest DMAs it directly."""
+
+    def __init__(self, shape, dtype=np.float32):
+        self._lib = _lib.load()
+        n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        p = C.c_void_p()
+        if self._lib.pgh_host_alloc(n, C.byref(p)) != 0:
+            raise AggregationError(self._lib.pgh_last_error(None).decode())
+        self._p = p
+        buf = (C.c_uint8 * n).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=dtype).reshape(shape)
+
+    def free(self):
+        if getattr(self, "_p", None):
+            self.array = None
+            self._lib.pgh_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class Engine:
@@ -112,6 +139,9 @@ class Engine:
     def synth_fill(self, seed: int, n_clients: int):
         self._check(self._lib.pgh_synth_fill(self._h, C.c_uint64(seed), int(n_clients)), "synth_fill")
 
+    def synth_ingest(self, seed: int, client0: int, n: int):
+        self._check(self._lib.pgh_synth_ingest(self._h, C.c_uint64(seed), int(client0), int(n)), "synth_ingest")
+
     def set_weights(self, w: Sequence[float]):
         a = np.ascontiguousarray(w, dtype=np.float32)
         self._check(self._lib.pgh_set_weights(self._h, a.ctypes.data_as(C.POINTER(C.c_float)), a.size),
@@ -147,6 +177,40 @@ class Engine:
     def synth_ckpt_device(self, seed: int, d_ckpt: int, stream: int = 0):
         self._check(self._lib.pgh_synth_ckpt_device(self._h, C.c_uint64(seed), C.c_void_p(d_ckpt),
                                                     C.c_void_p(stream or None)), "synth_ckpt_device")
+
+    # ---- stream use: fold clients in order as they arrive -----------------------------------------
+    def stream_begin(self, kind: int, fold_batch: int = 0):
+        self._check(self._lib.pgh_stream_begin(self._h, int(kind), int(fold_batch)), "stream_begin")
+
+    def stream_flush(self):
+        self._check(self._lib.pgh_stream_flush(self._h), "stream_flush")
+
+    def stream_finish(self, ckpt: np.ndarray) -> np.ndarray:
+        c = np.ascontiguousarray(ckpt, dtype=np.float32).reshape(-1)
+        if c.size != self.p_shard:
+            raise AggregationError(f"checkpoint has {c.size} params, shard has {self.p_shard}")
+        out = np.empty_like(c)
+        self._check(self._lib.pgh_stream_finish(self._h, _ptr(c), _ptr(out)), "stream_finish")
+        return out
+
+    def stream_finish_device(self, d_ckpt: int, d_out: int, stream: int = 0):
+        self._check(self._lib.pgh_stream_finish_device(self._h, C.c_void_p(d_ckpt), C.c_void_p(d_out),
+                                                       C.c_void_p(stream or None)), "stream_finish_device")
+
+    def stream_finish_secagg(self, base: int = 10, prec: int = 3):
+        s = np.empty(self.p_shard, dtype=np.int64)
+        d = np.empty(self.p_shard, dtype=np.float32)
+        self._check(self._lib.pgh_stream_finish_secagg(self._h, int(base), int(prec), _ptr(s), _ptr(d)),
+                    "stream_finish_secagg")
+        return s, d
+
+    def stream_finish_secagg_device(self, d_sum: int, d_dec: int, base: int = 10, prec: int = 3, stream: int = 0):
+        self._check(self._lib.pgh_stream_finish_secagg_device(
+            self._h, int(base), int(prec), C.c_void_p(d_sum or None), C.c_void_p(d_dec or None),
+            C.c_void_p(stream or None)), "stream_finish_secagg_device")
+
+    def sync(self):
+        self._check(self._lib.pgh_sync(self._h), "sync")
 
     # ---- observability -------------------------------------------------------------------------
     def set_variant(self, v: int):
