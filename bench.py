@@ -2,16 +2,22 @@
 """Benchmark of the PyGrid cycle-close aggregation hot path on MI355X.
 
 Metric (BASELINE.json): client-diff GB/s aggregated (% of HBM peak) at 1/2/4/8 MI355X; cycle
-close ms.  Workload at N = 1: BASELINE configs[1], ResNet-18 (11,689,512 params) fp32 FedAvg
-over 1,000 synthetic client diffs resident on one MI355X (46.8 GB).  A "step" is one cycle
-close of that workload: the fused mean + apply kernel over all [1000][P] diffs, producing the
-new checkpoint (for N > 1 also the RCCL all-gather that assembles it).
+close ms.  Default workload (N = 1: BASELINE configs[1]): ResNet-18 (11,689,512 params) fp32
+FedAvg over 1,000 synthetic client diffs resident on one MI355X (46.8 GB).  A "step" is one cycle
+close of that workload: the fused mean + apply kernel over all [1000][P] diffs producing the new
+checkpoint (for N > 1 also the RCCL all-gather that assembles it).
 
-Scaling: weak.  Rank r owns a 11,689,512-param shard of a (N x 11.69M)-param model (the
-parameter-axis sharding of SURVEY.md 8(e)), all 1,000 clients, so per-GPU work is fixed.
+Scaling: weak.  Rank r owns a P_g-param shard of a (N x P_g)-param model (the parameter-axis
+sharding of SURVEY.md 8(e)) and all clients, so per-GPU work is fixed as N grows.
 
-    python bench.py [--gpus N --steps K --warmup W] [--workload resnet18-fedavg|resnet18-iterative|
-                     resnet18-weighted|resnet18-secagg] [--variant V] [--no-cpu-baseline]
+Other BASELINE configs (--workload), each printed as its own JSON line of the same shape:
+  resnet18-iterative / resnet18-weighted   config 2 with the iterative plan / weighted FedAvg
+  resnet18-secagg        config 3: 1,000 clients x 2-party int64 shares (187 GB) resident
+  c4-stream              config 4 per-GPU shard: 12.5M params x 10,000 clients (500 GB) streamed
+                         through a 1,000-slot HBM ring, chunks generated on the GPU
+  c5-ingest              config 5 per-GPU shard: 125M params x 64 clients iterative, diffs streamed
+                         host (pinned) -> HBM over PCIe, folded while the next ones copy
+  mnist-state            config 1: 3 clients' State protobuf bytes -> new checkpoint bytes
 """
 from __future__ import annotations
 
@@ -26,13 +32,17 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
+METRIC = "client-diff GB/s aggregated (% of HBM peak) at 1/2/4/8 MI355X; cycle close ms"
 RESNET18_P = 11_689_512
+# name: (mode, dtype, clients, parties, params per GPU)
 WORKLOADS = {
-    # name: (mode, dtype, default clients, parties)
-    "resnet18-fedavg": (0, 0, 1000, 1),
-    "resnet18-iterative": (1, 0, 1000, 1),
-    "resnet18-weighted": (2, 0, 1000, 1),
-    "resnet18-secagg": (None, 1, 1000, 2),
+    "resnet18-fedavg": (0, 0, 1000, 1, RESNET18_P),
+    "resnet18-iterative": (1, 0, 1000, 1, RESNET18_P),
+    "resnet18-weighted": (2, 0, 1000, 1, RESNET18_P),
+    "resnet18-secagg": (None, 1, 1000, 2, RESNET18_P),
+    "c4-stream": (0, 0, 10_000, 1, 12_500_000),
+    "c5-ingest": (1, 0, 64, 1, 125_000_000),
+    "mnist-state": (0, 0, 3, 1, 311_650),
 }
 
 
@@ -43,24 +53,22 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="resnet18-fedavg", choices=sorted(WORKLOADS))
     ap.add_argument("--clients", type=int, default=None)
-    ap.add_argument("--params", type=int, default=RESNET18_P, help="params per GPU shard")
-    ap.add_argument("--variant", type=int, default=int(os.environ.get("PGH_VARIANT", "0")))
+    ap.add_argument("--params", type=int, default=None, help="params per GPU shard")
+    ap.add_argument("--variant", type=int, default=None)
+    ap.add_argument("--ring", type=int, default=None, help="stream workloads: HBM ring slots")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     return ap.parse_args()
 
 
-def cpu_baseline(P: int, seed: int, budget_s: float):
+def cpu_baseline(P: int, seed: int, budget_s: float, n: int = 32):
     """The oracle's restatement of cycle_manager.py:276-296 (allocating float32 adds, one thread,
     like the reference node's th.set_num_threads(1), main/__init__.py:8) on a bounded sample:
-    the same P-param shard, 32 synthetic clients, repeated until `budget_s` of CPU work."""
-    import numpy as np
-
+    the same P-param shard, `n` synthetic clients, repeated until `budget_s` of CPU work."""
     from oracle import coracle
     from oracle import oracle as O
 
-    n = 32
     diffs = [[coracle.synth_f32(seed, O.STREAM_DIFF, c, 0, P, float(O.DIFF_SCALE))] for c in range(n)]
     ckpt = [coracle.synth_f32(seed, O.STREAM_CKPT, 0, 0, P, float(O.CKPT_SCALE))]
     reps, t0 = 0, time.perf_counter()
@@ -74,17 +82,16 @@ def cpu_baseline(P: int, seed: int, budget_s: float):
     return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": f"oracle numpy restatement of cycle_manager.py:276-296, P={P}, {n} clients, "
                       f"{reps} passes in {el:.1f}s, 1 thread",
-            "cycle_close_ms_extrapolated_1000_clients": round(el / reps / n * 1000 * 1000, 1)}
+            "cycle_close_ms_per_1000_clients": round(el / reps / n * 1000 * 1000, 1)}
 
 
-def load_traffic(workload: str, variant: int, per_launch_bytes: float):
+def load_traffic(workload: str, variant: int):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/), if present."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
         return None, None
     try:
-        d = json.loads(f.read_text())
-        e = d.get(workload, {}).get(str(variant))
+        e = json.loads(f.read_text()).get(workload, {}).get(str(variant))
         if e is None:
             return None, None
         return float(e["hbm_bytes_per_launch"]), e.get("source")
@@ -92,38 +99,96 @@ def load_traffic(workload: str, variant: int, per_launch_bytes: float):
         return None, None
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+class Ctx:
+    """Per-rank setup shared by the workloads."""
 
-    from pygrid_amd import Engine
-    from pygrid_amd.sharding import gather_flat, shard_bounds
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus and self.rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {self.world}", file=sys.stderr)
+        torch.cuda.set_device(self.local)
+        if self.world > 1:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
 
-    mode, dtype, n_default, parties = WORKLOADS[args.workload]
-    N = args.clients or n_default
-    Pg = args.params
-    P = Pg * world
-    lo, hi = shard_bounds(P, world, rank)
-    pg = hi - lo
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
 
-    eng = Engine(local)
-    eng.set_layout([P])
-    eng.set_shard(lo, hi)
+    def max_over_ranks(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def timed(ctx, step, steps, warmup, eng):
+    torch = ctx.torch
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    eng.reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    el = time.perf_counter() - t0
+    return ctx.max_over_ranks(el), eng.stats()
+
+
+def record(ctx, args, name, value, el, dt, config, roofline, extra=None):
+    rec = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": ctx.world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dt,
+        "data": "synthetic (on-device counter-based generator, SURVEY.md 8(d); restated in oracle/oracle.py)",
+        "config": config,
+        "pct_hbm_peak_per_gpu": round(100 * value / ctx.world / HBM_PEAK_GBS, 2),
+        "cycle_close_ms": round(el / args.steps * 1e3, 4),
+        "roofline": roofline, "cpu_baseline": None,
+    }
+    if extra:
+        rec.update(extra)
+    return rec
+
+
+def roofline_of(st, workload, variant, kernel):
+    ms = st["kernel_ms_total"] / max(st["kernel_launches"], 1)
+    alg = st["kernel_bytes_total"] / max(st["kernel_launches"], 1)
+    achieved = alg / (ms / 1e3) / 1e9
+    traffic, src = load_traffic(workload, variant)
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
+            "kernel_ms_avg": round(ms, 4), "alg_bytes_per_launch": int(alg), "launches": st["kernel_launches"],
+            "traffic_source": src}
+
+
+def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
+    torch = ctx.torch
+    from pygrid_amd.sharding import gather_flat
+
     eng.reserve(N, dtype, parties)
-    eng.set_variant(args.variant)
     eng.synth_fill(args.seed, N)
-    stream = torch.cuda.current_stream()
-    sp = stream.cuda_stream
+    sp = torch.cuda.current_stream().cuda_stream
     if dtype == 0:
         ckpt = torch.empty(pg, dtype=torch.float32, device="cuda")
         out = torch.empty_like(ckpt)
@@ -133,95 +198,195 @@ def main():
 
         def step():
             eng.fedavg_device(mode, ckpt.data_ptr(), out.data_ptr(), sp)
-            if world > 1:
-                gather_flat(out, P, world, rank)
-        diff_bytes = 4 * N * pg
-        alg_bytes = 4 * N * pg + 8 * pg
-        dt = "f32"
+            if ctx.world > 1:
+                gather_flat(out, P, ctx.world, ctx.rank)
+        diff_bytes, dt, kernel = 4 * N * pg, "f32", "k_fedavg"
     else:
         s_out = torch.empty(pg, dtype=torch.int64, device="cuda")
         d_out = torch.empty(pg, dtype=torch.float32, device="cuda")
 
         def step():
             eng.secagg_device(s_out.data_ptr(), d_out.data_ptr(), 10, 3, sp)
-            if world > 1:
-                gather_flat(d_out, P, world, rank)
-        diff_bytes = 8 * parties * N * pg
-        alg_bytes = diff_bytes + 8 * pg + 4 * pg
-        dt = "int64"
+            if ctx.world > 1:
+                gather_flat(d_out, P, ctx.world, ctx.rank)
+        diff_bytes, dt, kernel = 8 * parties * N * pg, "int64", "k_secagg"
+    torch.cuda.synchronize()
+    el, st = timed(ctx, step, args.steps, args.warmup, eng)
+    value = diff_bytes * ctx.world * args.steps / el / 1e9
+    cfg = {"workload": f"{args.workload}: P_shard={pg} params/GPU x {N} clients"
+                       + (f" x {parties} parties int64" if dtype == 1 else " fp32") + ", resident in HBM",
+           "clients": N, "params_per_gpu": pg, "params_total": P,
+           "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
+           "kernel_variant": args.variant if args.variant is not None else 0}
+    rec = record(ctx, args, args.workload, value, el, dt, cfg,
+                 roofline_of(st, args.workload, cfg["kernel_variant"], kernel))
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline and dtype == 0 and mode == 0:
+        try:
+            rec["cpu_baseline"] = cpu_baseline(pg, args.seed, args.cpu_seconds)
+        except Exception as e:  # noqa: BLE001
+            rec["cpu_baseline"] = {"error": str(e)}
+    return rec
+
+
+def run_c4(ctx, args, eng, N, pg, P):
+    """Config 4 shard: N clients streamed through an R-slot ring; each chunk generated on the GPU
+    (stand-in for arriving data), folded in client order while the next chunk is generated."""
+    torch = ctx.torch
+    from pygrid_amd.sharding import gather_flat
+
+    R = args.ring or 1000
+    chunk = R // 2
+    eng.reserve(R)
+    ckpt = torch.empty(pg, dtype=torch.float32, device="cuda")
+    out = torch.empty_like(ckpt)
+    sp = torch.cuda.current_stream().cuda_stream
+    eng.synth_ckpt_device(args.seed, ckpt.data_ptr(), sp)
     torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        step()
+    def step():
+        eng.stream_begin(0, chunk)
+        for c0 in range(0, N, chunk):
+            eng.synth_ingest(args.seed, c0, min(chunk, N - c0))
+        eng.stream_finish_device(ckpt.data_ptr(), out.data_ptr(), sp)
+        if ctx.world > 1:
+            gather_flat(out, P, ctx.world, ctx.rank)
+    el, st = timed(ctx, step, args.steps, args.warmup, eng)
+    diff_bytes = 4 * N * pg
+    value = diff_bytes * ctx.world * args.steps / el / 1e9
+    kern_gbs = ctx.sum_over_ranks(4 * N * pg * args.steps / (st["kernel_ms_total"] / 1e3) / 1e9)
+    cfg = {"workload": f"c4-stream: P_shard={pg} params/GPU x {N} clients fp32 (SURVEY 8(d) config 4 shard), "
+                       f"{R}-slot HBM ring, {chunk}-client chunks generated on-device",
+           "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R,
+           "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
+           "kernel_variant": args.variant if args.variant is not None else 0}
+    extra = {"fold_kernel_client_diff_GBps_aggregated": round(kern_gbs, 1),
+             "note": "value includes on-device generation of every chunk (writes 4 B/param/client) "
+                     "competing for HBM with the fold; the fold kernels alone are fold_kernel_*"}
+    return record(ctx, args, "c4-stream", value, el, "f32", cfg,
+                  roofline_of(st, "c4-stream", cfg["kernel_variant"], "k_fedavg"), extra)
+
+
+def run_c5(ctx, args, eng, N, pg, P):
+    """Config 5 shard: iterative plan over N clients whose diffs arrive from page-locked host
+    memory; every H2D copy overlaps the fold of the previously copied clients."""
+    torch = ctx.torch
+    import numpy as np
+
+    from pygrid_amd import PinnedBuffer
+    from pygrid_amd.sharding import gather_flat
+
+    R = args.ring or 8
+    n_host = 4  # distinct host buffers, re-sent as different clients
+    bufs = [PinnedBuffer((pg,)) for _ in range(n_host)]  # shard-sized host diffs
+    rng = np.random.default_rng(args.seed + ctx.rank)
+    for b in bufs:
+        b.array[:] = rng.standard_normal(pg, dtype=np.float32) * np.float32(1e-2)
+    eng.reserve(R)
+    ckpt = torch.empty(pg, dtype=torch.float32, device="cuda")
+    out = torch.empty_like(ckpt)
+    sp = torch.cuda.current_stream().cuda_stream
+    eng.synth_ckpt_device(args.seed, ckpt.data_ptr(), sp)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    eng.reset_stats()
+
+    def step():
+        eng.stream_begin(1, 2)
+        for k in range(N):
+            eng.ingest(k, bufs[k % n_host].array)
+        eng.stream_finish_device(ckpt.data_ptr(), out.data_ptr(), sp)
+        if ctx.world > 1:
+            gather_flat(out, P, ctx.world, ctx.rank)
+    el, st = timed(ctx, step, args.steps, args.warmup, eng)
+    diff_bytes = 4 * N * pg
+    value = diff_bytes * ctx.world * args.steps / el / 1e9
+    kern_gbs = 4 * N * pg * args.steps / (st["kernel_ms_total"] / 1e3) / 1e9
+    ingest_gbs = st["h2d_bytes_total"] / (st["h2d_ms_total"] / 1e3) / 1e9 if st["h2d_ms_total"] else None
+    cfg = {"workload": f"c5-ingest: P_shard={pg} params/GPU x {N} clients fp32 iterative plan (SURVEY 8(d) "
+                       f"config 5 shard), pinned host -> HBM over PCIe, {R}-slot ring, fold batch 2",
+           "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R,
+           "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
+           "kernel_variant": args.variant if args.variant is not None else 0}
+    extra = {"bound_by": "PCIe host->device (Gen5 x16, 63 GB/s spec per GPU)",
+             "ingest_GBps_per_gpu": round(ingest_gbs, 2) if ingest_gbs else None,
+             "fold_kernel_client_diff_GBps_per_gpu": round(kern_gbs, 1)}
+    rec = record(ctx, args, "c5-ingest", value, el, "f32", cfg,
+                 roofline_of(st, "c5-ingest", cfg["kernel_variant"], "k_fedavg"), extra)
+    for b in bufs:
+        b.free()
+    return rec
+
+
+def run_mnist_state(ctx, args, eng):
+    """Config 1: bytes in, bytes out (State protobuf diffs -> new checkpoint bytes), 3 clients."""
+    import numpy as np
+
+    from oracle.gen_golden import MNIST_SHAPES, mnist_inputs, split
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.state_schema import build_state
+
+    diffs, ckpt = mnist_inputs(args.seed, 3)
+    ck_pb = build_state(split(ckpt, MNIST_SHAPES))
+    d_pb = [build_state(split(d, MNIST_SHAPES)) for d in diffs]
+    agg = CycleAggregator(eng)
+    for _ in range(args.warmup):
+        agg.average_plan_diffs({}, ck_pb, d_pb)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+        new = agg.average_plan_diffs({}, ck_pb, d_pb)
     el = time.perf_counter() - t0
     st = eng.stats()
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    kernel_ms = st["kernel_ms_total"] / max(st["kernel_launches"], 1)
+    P = ckpt.size
+    value = 4 * 3 * P * args.steps / el / 1e9
+    cfg = {"workload": "mnist-state: MNIST 784-392-10 (P=311,650), 3 clients, State bytes -> checkpoint bytes "
+                       "(decode + H2D + fused mean/apply + D2H + encode)", "clients": 3, "params_per_gpu": P,
+           "params_total": P, "parallelism": "single GPU", "kernel_variant": 0}
+    rec = record(ctx, args, "mnist-state", value, el, "f32", cfg,
+                 roofline_of(st, "mnist-state", 0, "k_fedavg"),
+                 {"new_checkpoint_bytes": len(new),
+                  "note": "latency-bound: host protobuf scan, 3 H2D copies and a 0.3M-param kernel"})
+    if not args.no_cpu_baseline:
+        from oracle import oracle as O
+        ds = [split(d, MNIST_SHAPES) for d in diffs]
+        ck = split(ckpt, MNIST_SHAPES)
+        t0, reps = time.perf_counter(), 0
+        while time.perf_counter() - t0 < 2.0:
+            O.fedavg_mean(ck, ds)
+            reps += 1
+        cel = (time.perf_counter() - t0) / reps
+        rec["cpu_baseline"] = {"value": round(4 * 3 * P / cel / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle numpy mean+apply on the decoded tensors, {reps} reps "
+                                         f"(syft protobuf decode not timed: syft is absent)",
+                               "cycle_close_ms": round(cel * 1e3, 3)}
+    return rec
 
-    total_diff_bytes = diff_bytes * world * args.steps  # every rank processed the same shard size
-    value = total_diff_bytes / el / 1e9
-    achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
-    traffic, traffic_src = load_traffic(args.workload, args.variant, alg_bytes)
 
-    if rank == 0:
-        rec = {
-            "metric": "client-diff GB/s aggregated (% of HBM peak) at 1/2/4/8 MI355X; cycle close ms",
-            "value": round(value, 2),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(el / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": dt,
-            "data": "synthetic (on-device counter-based generator, SURVEY.md 8(d); restated in oracle/oracle.py)",
-            "config": {
-                "workload": f"{args.workload}: P_shard={pg} params/GPU x {N} clients"
-                            + (f" x {parties} parties int64" if dtype == 1 else " fp32") + ", resident in HBM",
-                "clients": N, "params_per_gpu": pg, "params_total": P,
-                "parallelism": f"param-shard{world}" + (" + RCCL all-gather" if world > 1 else ""),
-                "kernel_variant": args.variant,
-            },
-            "pct_hbm_peak_per_gpu": round(100 * value / world / HBM_PEAK_GBS, 2),
-            "cycle_close_ms": round(el / args.steps * 1e3, 4),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "kernel": "k_fedavg" if dtype == 0 else "k_secagg",
-                "kernel_ms_avg": round(kernel_ms, 4),
-                "alg_bytes_per_launch": alg_bytes,
-                "traffic_source": traffic_src,
-            },
-            "cpu_baseline": None,
-        }
-        if world == 1 and not args.no_cpu_baseline and dtype == 0:
-            try:
-                rec["cpu_baseline"] = cpu_baseline(pg, args.seed, args.cpu_seconds)
-            except Exception as e:  # noqa: BLE001
-                rec["cpu_baseline"] = {"error": str(e)}
+def main():
+    args = parse()
+    ctx = Ctx(args)
+    from pygrid_amd import Engine
+    from pygrid_amd.sharding import shard_bounds
+
+    mode, dtype, n_default, parties, pg_default = WORKLOADS[args.workload]
+    N = args.clients or n_default
+    Pg = args.params or pg_default
+    P = Pg * ctx.world
+    lo, hi = shard_bounds(P, ctx.world, ctx.rank)
+    eng = Engine(ctx.local)
+    eng.set_layout([P])
+    eng.set_shard(lo, hi)
+    if args.variant is not None:
+        eng.set_variant(args.variant)
+    if args.workload == "c4-stream":
+        rec = run_c4(ctx, args, eng, N, hi - lo, P)
+    elif args.workload == "c5-ingest":
+        rec = run_c5(ctx, args, eng, N, hi - lo, P)
+    elif args.workload == "mnist-state":
+        rec = run_mnist_state(ctx, args, eng)
+    else:
+        rec = run_resident(ctx, args, eng, mode, dtype, N, parties, hi - lo, P, lo, hi)
+    if ctx.rank == 0:
         print(json.dumps(rec), flush=True)
     eng.close()
-    if world > 1:
-        dist.destroy_process_group()
+    ctx.close()
 
 
 if __name__ == "__main__":

@@ -95,8 +95,9 @@ int pgh_reset(pgh_ctx* ctx);
 
 /* ---- ingest (the diffs of cycle_manager.py:243-250) -------------------------------------- */
 /* Client `client`'s already-decoded flat diff.  PGH_F32: `flat` holds P float32 (the whole
- * model; the shard slice is taken).  PGH_I64: n_parties x P int64 shares, party-major.
- * Copied via the pinned ring into slab row `client` with hipMemcpyAsync. */
+ * model; the shard slice is taken) or P_shard float32 (this shard only).  PGH_I64: n_parties x
+ * P (or x P_shard) int64 shares, party-major.  Pageable memory is staged through the pinned
+ * ring; page-locked memory (pgh_host_alloc, hipHostRegister) is DMA'd directly. */
 int pgh_ingest_raw(pgh_ctx* ctx, int client, const void* flat, size_t nbytes, int dtype);
 /* Client diff as syft State protobuf bytes (model_manager.py:94-103 wire format, build-owned
  * schema restatement: DESIGN.md "State codec"); fp32 tensors only. */

@@ -641,15 +641,20 @@ int pgh_ingest_raw(pgh_ctx* c, int client, const void* flat, size_t nbytes, int 
     RC(check_dtype(c, dtype));
     if (!flat) return fail(c, PGH_E_ARG, "flat is NULL");
     const size_t es = esize(dtype);
-    const size_t want = (size_t)c->P * es * (size_t)c->parties;
-    if (nbytes != want) return fail(c, PGH_E_ARG, "client %d: got %zu bytes, layout needs %zu", client, nbytes, want);
+    const size_t whole = (size_t)c->P * es * (size_t)c->parties;  // the whole model: take the slice
+    const size_t shard = (size_t)c->pg * es * (size_t)c->parties; // this shard only
+    if (nbytes != whole && nbytes != shard)
+        return fail(c, PGH_E_ARG, "client %d: got %zu bytes, layout needs %zu (model) or %zu (shard)", client, nbytes,
+                    whole, shard);
     DeviceGuard g(c->device);
     int slot = 0;
     RC(claim_slot(c, client, &slot));
     const bool pinned = is_pinned(flat);
     const uint8_t* src = (const uint8_t*)flat;
+    const size_t row_elems = nbytes == whole ? (size_t)c->P : (size_t)c->pg;
+    const size_t first = nbytes == whole ? (size_t)c->lo : 0;
     for (int s = 0; s < c->parties; ++s)
-        RC(stage_h2d(c, slot_row(c, slot, s), src + ((size_t)s * c->P + c->lo) * es, (size_t)c->pg * es, pinned));
+        RC(stage_h2d(c, slot_row(c, slot, s), src + ((size_t)s * row_elems + first) * es, (size_t)c->pg * es, pinned));
     return mark_ingested(c, client, slot);
 }
 
