@@ -1,0 +1,96 @@
+"""CPU, world_size 2 (gloo): the multi-GPU path's host logic.
+
+Each rank owns the parameter shard ``shard_bounds(P, world, rank)`` for every client, folds it
+(here the oracle stands in for the rank's GPU: it is the checker, the sharding and the
+collective are the code under test), and ``gather_flat`` assembles the new checkpoint with one
+all-gather.  The result must equal the unsharded fold bit for bit.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pygrid_amd.sharding import all_shard_bounds, gather_flat, shard_bounds
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, P, N, mode, q):
+    from oracle import coracle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(1234)  # every rank sees the same clients
+        d = (rng.standard_normal((N, P)) * 1e-2).astype(np.float32)
+        c = rng.standard_normal(P).astype(np.float32)
+        lo, hi = shard_bounds(P, world, rank)
+        if hi > lo:
+            w = np.linspace(0.5, 2.0, N).astype(np.float32)
+            part = coracle.fedavg(mode, np.ascontiguousarray(d[:, lo:hi]), c[lo:hi], w if mode == 2 else None)
+        else:
+            part = np.empty(0, np.float32)
+        full = gather_flat(torch.from_numpy(part), P, world, rank)
+        # timing contract of bench.py: max over ranks
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        q.put((rank, full.numpy().tobytes(), float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("P,N,mode", [(10_007, 5, 0), (130, 3, 1), (64, 4, 2), (1, 2, 0)])
+def test_sharded_fold_and_gather_is_bit_identical(P, N, mode):
+    from oracle import coracle
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, P, N, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(1234)
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(np.float32)
+    c = rng.standard_normal(P).astype(np.float32)
+    w = np.linspace(0.5, 2.0, N).astype(np.float32)
+    want = coracle.fedavg(mode, d, c, w if mode == 2 else None)
+    for rank, blob, tmax in res:
+        got = np.frombuffer(blob, dtype=np.float32)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), rank
+        assert tmax == 2.0
+
+
+@pytest.mark.parametrize("P", [1, 63, 64, 65, 10_000, 11_689_512, 100_000_000])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_bounds_partition(P, world):
+    b = all_shard_bounds(P, world)
+    assert b[0][0] == 0 and b[-1][1] == P
+    for (lo, hi), (lo2, _) in zip(b, b[1:]):
+        assert hi == lo2 and lo <= hi
+    for lo, hi in b:
+        assert lo % 64 == 0 or lo == P
+    sizes = [hi - lo for lo, hi in b]
+    assert max(sizes) - min(x for x in sizes if x > 0 or P < world * 64) <= max(sizes)
+
+
+def test_weak_scaling_shards_equal():
+    """bench.py's weak scaling: P = world x P_g, every rank's shard within one alignment unit of P_g."""
+    Pg = 11_689_512
+    for world in (1, 2, 4, 8):
+        for lo, hi in all_shard_bounds(world * Pg, world):
+            assert abs((hi - lo) - Pg) < 64 * world

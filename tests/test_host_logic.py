@@ -1,0 +1,211 @@
+"""CPU: host-side logic of the drop-in -- readiness predicate, plan dispatch, the
+_average_plan_diffs wiring, and the State codec (host-only C++ in libpygrid_hip)."""
+import itertools
+import types
+
+import numpy as np
+import pytest
+import torch as th
+
+from oracle import oracle as O
+from pygrid_amd import ITERATIVE_MEAN, MEAN, WEIGHTED_MEAN, PlanNotAcceleratedError, StateParseError
+from pygrid_amd import cycle, state
+from pygrid_amd.state_schema import build_state, classes, parse_state
+
+F = np.float32
+
+
+# ---- readiness (cycle_manager.py:196-210) ------------------------------------------------------
+def test_ready_to_average_matches_oracle_exhaustively():
+    opts = [None, 0, 1, 3]
+    for mn, mx, recv, end, now in itertools.product(opts, opts, [0, 1, 2, 3, 4], [None, 5], [4, 5, 6]):
+        cfg = {}
+        if mn is not None:
+            cfg["min_diffs"] = mn
+        if mx is not None:
+            cfg["max_diffs"] = mx
+        assert cycle.ready_to_average(cfg, recv, end, now) == O.ready_to_average(cfg, recv, end, now)
+
+
+# ---- plan dispatch (SURVEY 8(b) dispatch rule) ---------------------------------------------------
+def canonical_plan(avg, item, num):  # 01-Create-plan.ipynb:450-454
+    new_avg = []
+    for i, param in enumerate(avg):
+        new_avg.append((avg[i] * num + item[i]) / (num + 1))
+    return new_avg
+
+
+def reassociated_plan(avg, item, num):  # mathematically equal, rounds differently
+    return [avg[i] * (num / (num + 1)) + item[i] / (num + 1) for i in range(len(avg))]
+
+
+def test_select_mode_dispatch():
+    assert cycle.select_mode({}, None) == MEAN
+    assert cycle.select_mode({"iterative_plan": True}, None) == MEAN
+    assert cycle.select_mode({"iterative_plan": True}, canonical_plan) == ITERATIVE_MEAN
+    assert cycle.select_mode({}, None, weights=[1, 2]) == WEIGHTED_MEAN
+    with pytest.raises(PlanNotAcceleratedError):
+        cycle.select_mode({"iterative_plan": False}, canonical_plan)  # :270-271 user-defined plan
+    with pytest.raises(PlanNotAcceleratedError):
+        cycle.select_mode({"iterative_plan": True}, reassociated_plan)
+    with pytest.raises(PlanNotAcceleratedError):
+        cycle.select_mode({"iterative_plan": True}, lambda a, b, n: [x * 2 for x in a])
+    with pytest.raises(PlanNotAcceleratedError):
+        cycle.select_mode({"iterative_plan": True}, lambda a, b, n: 1 / 0)
+
+
+def test_canonical_probe_uses_reference_calling_convention():
+    seen = []
+
+    def plan(avg, item, num):
+        seen.append((type(avg), num.dtype, tuple(num.shape)))
+        return canonical_plan(avg, item, num)
+
+    assert cycle.is_canonical_iterative_plan(plan)
+    assert seen[0] == (list, th.int64, (1,))  # avg_plan(list(diff_avg), diff, th.tensor([i + 1]))
+
+
+# ---- _average_plan_diffs wiring (cycle_manager.py:234-245, :304-323) -----------------------------
+class FakeWarehouse:
+    def __init__(self, rows=None):
+        self.rows = rows or []
+        self.updates = 0
+
+    def query(self, **kw):
+        return [r for r in self.rows if all(getattr(r, k) == v for k, v in kw.items())]
+
+    def count(self, **kw):
+        return len(self.query(**kw))
+
+    def update(self):
+        self.updates += 1
+
+
+def _fake_node(avg_plan_value=None, num_cycles=0):
+    ns = types.SimpleNamespace
+    model = ns(id=7)
+    ckpt = ns(value=b"CKPT")
+    saved = []
+    model_manager = ns(get=lambda **kw: model, load=lambda **kw: ckpt, save=lambda mid, data: saved.append((mid, data)))
+    plan_rec = ns(value=avg_plan_value) if avg_plan_value else None
+    process_manager = ns(get_plan=lambda **kw: plan_rec)
+    plan_manager = ns(deserialize_plan=lambda b: canonical_plan if b == b"CANON" else reassociated_plan)
+    reports = [ns(cycle_id=3, is_completed=True, diff=b"D%d" % k) for k in range(3)]
+    cyc = ns(id=3, fl_process_id=11, version="1.0", is_completed=False)
+    created = []
+    self_ = ns(_worker_cycles=FakeWarehouse(reports), _cycles=FakeWarehouse([cyc]),
+               create=lambda pid, ver, length: created.append((pid, ver, length)))
+    return model_manager, process_manager, plan_manager, self_, cyc, saved, created
+
+
+class FakeAggregator:
+    def __init__(self):
+        self.calls = []
+
+    def average_plan_diffs(self, server_config, checkpoint, diffs, avg_plan=None):
+        cycle.select_mode(server_config, avg_plan)  # same dispatch as the real one
+        self.calls.append((checkpoint, list(diffs), avg_plan))
+        return b"NEW"
+
+
+def test_wiring_hardcoded_path():
+    mm, pm, plm, self_, cyc, saved, created = _fake_node()
+    agg = FakeAggregator()
+    fn = cycle.make_average_plan_diffs(agg, mm, pm, plm, original=None)
+    fn(self_, {"cycle_length": 60}, cyc)
+    assert agg.calls == [(b"CKPT", [b"D0", b"D1", b"D2"], None)]
+    assert saved == [(7, b"NEW")]
+    assert cyc.is_completed and self_._cycles.updates == 1
+    assert created == [(11, "1.0", 60)]  # num_cycles 0 -> next cycle created (:315-320)
+
+
+def test_wiring_declines_to_reference_for_unknown_plans():
+    mm, pm, plm, self_, cyc, saved, created = _fake_node(avg_plan_value=b"OTHER")
+    ran = []
+    fn = cycle.make_average_plan_diffs(FakeAggregator(), mm, pm, plm,
+                                       original=lambda s, cfg, c: ran.append((cfg, c)))
+    fn(self_, {"iterative_plan": True}, cyc)
+    assert ran and saved == []
+
+
+def test_wiring_iterative_plan_accelerated_and_fl_done():
+    mm, pm, plm, self_, cyc, saved, created = _fake_node(avg_plan_value=b"CANON")
+    self_._cycles.rows[0].is_completed = True  # count(is_completed=True) -> 1 == num_cycles
+    agg = FakeAggregator()
+    fn = cycle.make_average_plan_diffs(agg, mm, pm, plm, original=None)
+    fn(self_, {"iterative_plan": True, "num_cycles": 1}, cyc)
+    assert agg.calls[0][2] is canonical_plan and saved == [(7, b"NEW")] and created == []
+
+
+# ---- State codec (host-only C++) -----------------------------------------------------------------
+SHAPES = [(392, 784), (392,), (10, 392), (10,)]
+
+
+def _tensors(seed=0):
+    rng = np.random.default_rng(seed)
+    return [rng.standard_normal(s).astype(F) for s in SHAPES]
+
+
+@pytest.mark.parametrize("as_param", [False, True])
+def test_state_scan_and_unserialize(as_param):
+    ts = _tensors()
+    pb = build_state(ts, as_param=as_param)
+    spans = state.scan(pb)
+    assert [c for _, c in spans] == [t.size for t in ts]
+    for got, want in zip(state.unserialize_model_params(pb, SHAPES), ts):
+        assert np.array_equal(got, want)
+
+
+def test_state_patch_roundtrips_through_google_protobuf():
+    ts = _tensors(1)
+    pb = build_state(ts, ids=[11, 22, 33, 44])
+    new = np.arange(sum(t.size for t in ts), dtype=F) * F(0.5)
+    out = state.serialize_model_params(pb, new)
+    assert len(out) == len(pb)
+    parsed = parse_state(out)
+    off = 0
+    for t, p in zip(ts, parsed):
+        assert p.shape == t.shape
+        assert np.array_equal(p.reshape(-1), new[off:off + t.size])
+        off += t.size
+    st = classes()["State"]()
+    st.ParseFromString(out)  # ids / tags / shapes untouched
+    assert [ph.id.id_int for ph in st.placeholders] == [11, 22, 33, 44]
+
+
+def test_state_scan_skips_unknown_fields_and_zero_size():
+    cls = classes()
+    st = cls["State"]()
+    st.ParseFromString(build_state([np.zeros((0,), F), np.ones(3, F)]))
+    t = st.tensors[1].torch_tensor
+    t.description = "x" * 300  # a long unknown-to-the-walker string field
+    t.tags.extend(["a", "b"])
+    pb = st.SerializeToString()
+    assert [c for _, c in state.scan(pb)] == [0, 3]
+    assert np.array_equal(state.flat_params(pb), np.ones(3, F))
+
+
+@pytest.mark.parametrize("mutate", ["truncate", "dtype", "shape"])
+def test_state_errors(mutate):
+    cls = classes()
+    pb = build_state([np.ones((2, 3), F)])
+    if mutate == "truncate":
+        pb = pb[:-3]
+    else:
+        st = cls["State"]()
+        st.ParseFromString(pb)
+        td = st.tensors[0].torch_tensor.contents_data
+        if mutate == "dtype":
+            td.dtype = "float64"
+        else:
+            del td.shape.dims[:]
+            td.shape.dims.extend([4, 2])
+        pb = st.SerializeToString()
+    with pytest.raises(StateParseError):
+        state.scan(pb)
+
+
+def test_state_patch_rejects_wrong_value_count():
+    pb = build_state([np.ones(5, F)])
+    with pytest.raises(StateParseError):
+        state.serialize_model_params(pb, np.zeros(4, F))
