@@ -18,6 +18,8 @@ Other BASELINE configs (--workload), each printed as its own JSON line of the sa
   c5-ingest              config 5 per-GPU shard: 125M params x 64 clients iterative, diffs streamed
                          host (pinned) -> HBM over PCIe, folded while the next ones copy
   mnist-state            config 1: 3 clients' State protobuf bytes -> new checkpoint bytes
+  resnet18-state         ResNet-18 (62 tensors) x 100 clients, State bytes on the host -> new
+                         checkpoint bytes: the whole cycle close a node runs (PCIe-inclusive)
 """
 from __future__ import annotations
 
@@ -43,6 +45,7 @@ WORKLOADS = {
     "c4-stream": (0, 0, 10_000, 1, 12_500_000),
     "c5-ingest": (1, 0, 64, 1, 125_000_000),
     "mnist-state": (0, 0, 3, 1, 311_650),
+    "resnet18-state": (0, 0, 100, 1, RESNET18_P),
 }
 
 
@@ -217,7 +220,7 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
                        + (f" x {parties} parties int64" if dtype == 1 else " fp32") + ", resident in HBM",
            "clients": N, "params_per_gpu": pg, "params_total": P,
            "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
-           "kernel_variant": args.variant if args.variant is not None else 0}
+           "kernel_variant": args.variant if args.variant is not None else 6}
     rec = record(ctx, args, args.workload, value, el, dt, cfg,
                  roofline_of(st, args.workload, cfg["kernel_variant"], kernel))
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline and dtype == 0 and mode == 0:
@@ -258,7 +261,7 @@ def run_c4(ctx, args, eng, N, pg, P):
                        f"{R}-slot HBM ring, {chunk}-client chunks generated on-device",
            "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R,
            "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
-           "kernel_variant": args.variant if args.variant is not None else 0}
+           "kernel_variant": args.variant if args.variant is not None else 6}
     extra = {"fold_kernel_client_diff_GBps_aggregated": round(kern_gbs, 1),
              "note": "value includes on-device generation of every chunk (writes 4 B/param/client) "
                      "competing for HBM with the fold; the fold kernels alone are fold_kernel_*"}
@@ -304,7 +307,7 @@ def run_c5(ctx, args, eng, N, pg, P):
                        f"config 5 shard), pinned host -> HBM over PCIe, {R}-slot ring, fold batch 2",
            "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R,
            "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
-           "kernel_variant": args.variant if args.variant is not None else 0}
+           "kernel_variant": args.variant if args.variant is not None else 6}
     extra = {"bound_by": "PCIe host->device (Gen5 x16, 63 GB/s spec per GPU)",
              "ingest_GBps_per_gpu": round(ingest_gbs, 2) if ingest_gbs else None,
              "fold_kernel_client_diff_GBps_per_gpu": round(kern_gbs, 1)}
@@ -338,9 +341,9 @@ def run_mnist_state(ctx, args, eng):
     value = 4 * 3 * P * args.steps / el / 1e9
     cfg = {"workload": "mnist-state: MNIST 784-392-10 (P=311,650), 3 clients, State bytes -> checkpoint bytes "
                        "(decode + H2D + fused mean/apply + D2H + encode)", "clients": 3, "params_per_gpu": P,
-           "params_total": P, "parallelism": "single GPU", "kernel_variant": 0}
+           "params_total": P, "parallelism": "single GPU", "kernel_variant": 6}
     rec = record(ctx, args, "mnist-state", value, el, "f32", cfg,
-                 roofline_of(st, "mnist-state", 0, "k_fedavg"),
+                 roofline_of(st, "mnist-state", 6, "k_fedavg"),
                  {"new_checkpoint_bytes": len(new),
                   "note": "latency-bound: host protobuf scan, 3 H2D copies and a 0.3M-param kernel"})
     if not args.no_cpu_baseline:
@@ -357,6 +360,43 @@ def run_mnist_state(ctx, args, eng):
                                          f"(syft protobuf decode not timed: syft is absent)",
                                "cycle_close_ms": round(cel * 1e3, 3)}
     return rec
+
+
+def run_resnet18_state(ctx, args, eng, N):
+    """Bytes in, bytes out at ResNet-18 size: N clients' State protobuf diffs (host memory) ->
+    new checkpoint bytes.  Includes payload location, host->HBM over PCIe, fused mean/apply,
+    HBM->host and the checkpoint patch: what `_average_plan_diffs` costs the node."""
+    import numpy as np
+
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.state_schema import build_state_fast
+    from pygrid_amd.workloads import RESNET18_SHAPES
+
+    rng = np.random.default_rng(args.seed)
+    ck_pb = build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in RESNET18_SHAPES])
+    distinct = [build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2)
+                                  for s in RESNET18_SHAPES]) for _ in range(4)]
+    d_pb = [distinct[k % 4] for k in range(N)]  # 4 distinct messages re-sent (host memory)
+    agg = CycleAggregator(eng)
+    for _ in range(args.warmup):
+        agg.average_plan_diffs({}, ck_pb, d_pb)
+    eng.reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        new = agg.average_plan_diffs({}, ck_pb, d_pb)
+    el = time.perf_counter() - t0
+    st = eng.stats()
+    P = RESNET18_P
+    value = 4 * N * P * args.steps / el / 1e9
+    cfg = {"workload": f"resnet18-state: ResNet-18 (62 tensors, P={P}) x {N} clients, State protobuf bytes in host "
+                       "memory -> new checkpoint bytes (scan + host->HBM + fused mean/apply + HBM->host + patch)",
+           "clients": N, "params_per_gpu": P, "params_total": P, "parallelism": "single GPU", "kernel_variant": 6}
+    extra = {"h2d_GBps": round(st["h2d_bytes_total"] / (st["h2d_ms_total"] / 1e3) / 1e9, 2) if st["h2d_ms_total"] else None,
+             "h2d_ms_per_close": round(st["h2d_ms_total"] / args.steps, 2),
+             "new_checkpoint_bytes": len(new),
+             "note": "PCIe-inclusive cycle close from host bytes (never `value` for the resident configs)"}
+    return record(ctx, args, "resnet18-state", value, el, "f32", cfg,
+                  roofline_of(st, "resnet18-state", 6, "k_fedavg"), extra)
 
 
 def main():
@@ -381,6 +421,8 @@ def main():
         rec = run_c5(ctx, args, eng, N, hi - lo, P)
     elif args.workload == "mnist-state":
         rec = run_mnist_state(ctx, args, eng)
+    elif args.workload == "resnet18-state":
+        rec = run_resnet18_state(ctx, args, eng, N)
     else:
         rec = run_resident(ctx, args, eng, mode, dtype, N, parties, hi - lo, P, lo, hi)
     if ctx.rank == 0:

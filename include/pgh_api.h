@@ -137,7 +137,9 @@ int pgh_stream_finish_secagg(pgh_ctx* ctx, int base, int prec, int64_t* sum_out,
 int pgh_stream_finish_secagg_device(pgh_ctx* ctx, int base, int prec, int64_t* d_sum, float* d_dec, void* stream);
 
 /* ---- tuning and observability -------------------------------------------------------------- */
-int pgh_set_variant(pgh_ctx* ctx, int variant);   /* kernel variant, for A/B measurement */
+/* Kernel variant for A/B measurement (table in csrc/pgh_kernels.hip); -1 = the default. */
+#define PGH_DEFAULT_VARIANT 6
+int pgh_set_variant(pgh_ctx* ctx, int variant);
 int pgh_stats(pgh_ctx* ctx, pgh_stats_t* out);     /* synchronises pending timing events */
 int pgh_reset_stats(pgh_ctx* ctx);
 /* Device pointer of the slab and its row stride, for callers that drive the kernels. */

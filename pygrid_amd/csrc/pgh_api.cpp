@@ -82,12 +82,11 @@ struct pgh_ctx {
     int fold_batch = 1;
     int64_t folded = 0;  // stream: clients [0, folded) are in the running state
 
-    int variant = 0;
+    int variant = PGH_DEFAULT_VARIANT;
     struct Timed { hipEvent_t a, b; uint64_t bytes; };
     std::vector<Timed> pending;
     std::vector<hipEvent_t> pool;
     pgh_stats_t st{};
-    std::vector<float> scratch;  // State decode staging
     std::string err;
 };
 
@@ -237,25 +236,47 @@ bool is_pinned(const void* p) {
 // host bytes -> HBM on the copy stream.  Page-locked sources are DMA'd directly (the call
 // then waits for the copy: the caller's buffer is only borrowed); pageable sources go through
 // the pinned ring, so the host memcpy of one slot overlaps the DMA of the other.
-int stage_h2d(pgh_ctx* c, void* dst, const uint8_t* src, size_t n, bool pinned_src) {
+struct Piece {
+    const uint8_t* src;
+    size_t n;
+};
+
+// Concatenated host pieces -> HBM at `dst`, through the pinned ring: each slot is filled by
+// (multi-threaded) host copies of as many pieces as fit, then DMA'd while the next slot fills.
+int stage_pieces_h2d(pgh_ctx* c, uint8_t* dst, const std::vector<Piece>& pieces) {
     const double t0 = now_ms();
-    if (pinned_src) {
-        CK(c, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->copy));
-        CK(c, hipStreamSynchronize(c->copy));
-    } else {
-        size_t off = 0;
-        while (off < n) {
-            const int slot = c->pin_next;
-            c->pin_next ^= 1;
-            if (c->pin_used[slot]) CK(c, hipEventSynchronize(c->pin_ev[slot]));
-            const size_t m = std::min(n - off, c->pin_slot);
-            par_memcpy(c->h_pin[slot], src + off, m, c->copy_threads);
-            CK(c, hipMemcpyAsync((uint8_t*)dst + off, c->h_pin[slot], m, hipMemcpyHostToDevice, c->copy));
-            CK(c, hipEventRecord(c->pin_ev[slot], c->copy));
-            c->pin_used[slot] = true;
-            off += m;
+    size_t total = 0, done = 0, pi = 0, poff = 0;
+    for (auto& p : pieces) total += p.n;
+    while (done < total) {
+        const int slot = c->pin_next;
+        c->pin_next ^= 1;
+        if (c->pin_used[slot]) CK(c, hipEventSynchronize(c->pin_ev[slot]));
+        size_t fill = 0;
+        while (fill < c->pin_slot && pi < pieces.size()) {
+            const size_t m = std::min(pieces[pi].n - poff, c->pin_slot - fill);
+            par_memcpy(c->h_pin[slot] + fill, pieces[pi].src + poff, m, c->copy_threads);
+            fill += m;
+            poff += m;
+            if (poff == pieces[pi].n) { ++pi; poff = 0; }
         }
+        CK(c, hipMemcpyAsync(dst + done, c->h_pin[slot], fill, hipMemcpyHostToDevice, c->copy));
+        CK(c, hipEventRecord(c->pin_ev[slot], c->copy));
+        c->pin_used[slot] = true;
+        done += fill;
     }
+    c->st.h2d_ms_total += now_ms() - t0;
+    c->st.h2d_bytes_total += total;
+    return PGH_OK;
+}
+
+// host bytes -> HBM on the copy stream.  Page-locked sources are DMA'd directly (the call
+// then waits for the copy: the caller's buffer is only borrowed); pageable sources go through
+// the pinned ring, so the host memcpy of one slot overlaps the DMA of the other.
+int stage_h2d(pgh_ctx* c, void* dst, const uint8_t* src, size_t n, bool pinned_src) {
+    if (!pinned_src) return stage_pieces_h2d(c, (uint8_t*)dst, {Piece{src, n}});
+    const double t0 = now_ms();
+    CK(c, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->copy));
+    CK(c, hipStreamSynchronize(c->copy));
     c->st.h2d_ms_total += now_ms() - t0;
     c->st.h2d_bytes_total += n;
     return PGH_OK;
@@ -661,11 +682,30 @@ int pgh_ingest_raw(pgh_ctx* c, int client, const void* flat, size_t nbytes, int 
 int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
     RC(check_dtype(c, PGH_F32));
     if (!pb && n) return fail(c, PGH_E_ARG, "pb is NULL");
-    c->scratch.resize((size_t)c->P);
+    std::vector<pgh_state::Span> spans;
     std::string msg;
-    int rc = pgh_state::decode_f32(pb, n, c->numel, c->scratch.data(), &msg);
+    int rc = pgh_state::scan(pb, n, &spans, &msg);
     if (rc) return fail(c, rc, "client %d State: %s", client, msg.c_str());
-    return pgh_ingest_raw(c, client, c->scratch.data(), (size_t)c->P * 4, PGH_F32);
+    if (spans.size() != c->numel.size())
+        return fail(c, PGH_E_PARSE, "client %d State holds %zu tensors, layout has %zu", client, spans.size(),
+                    c->numel.size());
+    // The shard's slice of the concatenated payloads, as pieces of the message itself: the
+    // float32 payload bytes go straight from the protobuf buffer into the pinned ring.
+    std::vector<Piece> pieces;
+    int64_t off = 0;
+    for (size_t t = 0; t < spans.size(); ++t) {
+        if (spans[t].count != c->numel[t])
+            return fail(c, PGH_E_PARSE, "client %d tensor %zu holds %lld floats, layout %lld", client, t,
+                        (long long)spans[t].count, (long long)c->numel[t]);
+        const int64_t a = std::max(off, c->lo), b = std::min(off + spans[t].count, c->hi);
+        if (a < b) pieces.push_back(Piece{pb + spans[t].offset + 4 * (size_t)(a - off), 4 * (size_t)(b - a)});
+        off += spans[t].count;
+    }
+    DeviceGuard g(c->device);
+    int slot = 0;
+    RC(claim_slot(c, client, &slot));
+    RC(stage_pieces_h2d(c, slot_row(c, slot, 0), pieces));
+    return mark_ingested(c, client, slot);
 }
 
 int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
@@ -899,8 +939,8 @@ int pgh_stream_finish_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, f
 
 int pgh_set_variant(pgh_ctx* c, int variant) {
     if (!c) return PGH_E_ARG;
-    if (variant < 0 || variant > 5) return fail(c, PGH_E_ARG, "variant %d outside [0,5]", variant);
-    c->variant = variant;
+    if (variant < -1 || variant > 10) return fail(c, PGH_E_ARG, "variant %d outside [-1,10]", variant);
+    c->variant = variant < 0 ? PGH_DEFAULT_VARIANT : variant;
     return PGH_OK;
 }
 

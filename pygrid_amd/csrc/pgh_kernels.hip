@@ -86,43 +86,65 @@ __device__ __forceinline__ f32x4 fold(f32x4 acc, f32x4 v, int64_t k, const float
     }
 }
 
-// One 16-byte column: 4 consecutive params of the shard, all rows of the chunk, in order.
-template <int MODE, int U, bool NT>
-__device__ __forceinline__ void fedavg_column(const FedavgArgs& a, int64_t q) {
-    const float* col = a.diffs + 4 * q;
+// W 16-byte columns per lane (q0, q0 + TB, ...: each load instruction of a wave still reads one
+// contiguous KiB), all rows of the chunk, in order.  4 consecutive params per column.
+template <int MODE, int U, int W, bool NT>
+__device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, int64_t qstep) {
     const int n = a.n_rows;
-    f32x4 acc;
+    f32x4 acc[W];
     int r;
     if (a.flags & FL_FIRST) {
-        acc = ld4<NT>(col);                                    // fold starts at d0, not 0
-        if constexpr (MODE == MODE_WEIGHTED) acc = acc * a.weights[0];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            acc[w] = ld4<NT>(a.diffs + 4 * (q0 + w * qstep));  // fold starts at d0, not 0
+            if constexpr (MODE == MODE_WEIGHTED) acc[w] = acc[w] * a.weights[0];
+        }
         r = 1;
     } else {
-        acc = ld4_tail(a.acc, q, a.p);
+#pragma unroll
+        for (int w = 0; w < W; ++w) acc[w] = ld4_tail(a.acc, q0 + w * qstep, a.p);
         r = 0;
     }
     for (; r + U <= n; r += U) {
-        f32x4 v[U];
+        f32x4 v[U][W];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = ld4<NT>(col + (size_t)(r + u) * a.ld);
+        for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc = fold<MODE>(acc, v[u], a.client0 + r + u, a.weights, r + u);
+            for (int w = 0; w < W; ++w) v[u][w] = ld4<NT>(a.diffs + (size_t)(r + u) * a.ld + 4 * (q0 + w * qstep));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int w = 0; w < W; ++w) acc[w] = fold<MODE>(acc[w], v[u][w], a.client0 + r + u, a.weights, r + u);
     }
-    for (; r < n; ++r) acc = fold<MODE>(acc, ld4<NT>(col + (size_t)r * a.ld), a.client0 + r, a.weights, r);
-
-    if (a.flags & FL_FINAL) {
-        const f32x4 avg = (MODE == MODE_ITERATIVE) ? acc : acc / a.divisor;  // th.div, :288
-        st4_tail(a.out, q, a.p, ld4_tail(a.ckpt, q, a.p) - avg);             // :293-296
-    } else {
-        st4_tail(a.acc, q, a.p, acc);
+    for (; r < n; ++r)
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            acc[w] = fold<MODE>(acc[w], ld4<NT>(a.diffs + (size_t)r * a.ld + 4 * (q0 + w * qstep)), a.client0 + r,
+                                a.weights, r);
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const int64_t q = q0 + w * qstep;
+        if (a.flags & FL_FINAL) {
+            const f32x4 avg = (MODE == MODE_ITERATIVE) ? acc[w] : acc[w] / a.divisor;  // th.div, :288
+            st4_tail(a.out, q, a.p, ld4_tail(a.ckpt, q, a.p) - avg);                   // :293-296
+        } else {
+            st4_tail(a.acc, q, a.p, acc[w]);
+        }
     }
 }
 
-template <int MODE, int U, bool NT>
-__global__ __launch_bounds__(BLOCK) void k_fedavg(FedavgArgs a, int64_t ncol) {
-    const int64_t stride = (int64_t)gridDim.x * BLOCK;
-    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < ncol; q += stride)
-        fedavg_column<MODE, U, NT>(a, q);
+// Grid-stride over tiles of TB x W columns; a partial last tile goes one column per lane.
+template <int MODE, int U, int W, bool NT, int TB>
+__global__ __launch_bounds__(TB) void k_fedavg(FedavgArgs a, int64_t ncol) {
+    const int64_t tile = (int64_t)TB * W;
+    for (int64_t t0 = (int64_t)blockIdx.x * tile; t0 < ncol; t0 += (int64_t)gridDim.x * tile) {
+        const int64_t q0 = t0 + threadIdx.x;
+        if (t0 + tile <= ncol) {
+            fedavg_columns<MODE, U, W, NT>(a, q0, TB);
+        } else {
+            for (int64_t q = q0; q < ncol && q < t0 + tile; q += TB) fedavg_columns<MODE, U, 1, NT>(a, q, TB);
+        }
+    }
 }
 
 template <int U, bool NT>
@@ -214,30 +236,52 @@ int cu_count() {
     return cached[dev];
 }
 
-// Variants (A/B in one process: tools/ab_variants.py; profiles/r01/README.md):
-//   0 = nt loads, U=8, one column per lane (grid covers every column once)   <- default
-//   1 = nt loads, U=8, persistent grid (4 blocks per CU) striding over columns
-//   2 / 3 = the same two with plain (default-policy) loads
-//   4 / 5 = plain loads, U=16
-// Even variants: one column per lane; odd: persistent grid.  nt loads won 2-3 % on the
-// once-read diff stream (r01: 6393 vs 6270 GB/s at ResNet-18 x 1000 clients).
-inline unsigned grid_for(int64_t ncol, int variant) {
-    const int64_t full = (ncol + BLOCK - 1) / BLOCK;
-    if ((variant & 1) == 0) return (unsigned)(full > 0 ? full : 1);
+// Variants (A/B in one process: tools/ab_variants.py; profiles/r01/README.md).
+//   id  loads  U (rows in flight)  W (columns per lane)  block  grid
+//   0   nt     8                   1                     256    one lane per column
+//   1   nt     8                   1                     256    persistent, 4 blocks/CU
+//   2   plain  8                   1                     256    one lane per column
+//   3   plain  8                   1                     256    persistent
+//   4   plain  16                  1                     256    one lane per column
+//   5   plain  16                  1                     256    persistent
+//   6   nt     16                  1                     256    one lane per column   <- default
+//   7   nt     4                   2                     256    one lane per W columns
+//   8   nt     8                   2                     256    one lane per W columns
+//   9   nt     8                   1                     512    one lane per column
+//   10  nt     4                   1                     256    one lane per column
+// nt loads won 2-3 % on the once-read diff stream (r01: 6393 vs 6270 GB/s, ResNet-18 x 1000);
+// r01c: every nt variant within 1 %, 6 best or tied on K1 (6448), K2 (6415) and K3 (6238 GB/s).
+constexpr int N_VARIANTS = 11;
+
+inline unsigned grid_for(int64_t ncol, int64_t tile, bool persistent) {
+    const int64_t full = (ncol + tile - 1) / tile;
+    if (!persistent) return (unsigned)(full > 0 ? full : 1);
     const int64_t pers = (int64_t)cu_count() * 4;
     return (unsigned)(full < pers ? (full > 0 ? full : 1) : pers);
 }
 
+template <int MODE, int U, int W, bool NT, int TB>
+hipError_t go_fedavg(const FedavgArgs& a, int64_t ncol, bool persistent, hipStream_t s) {
+    k_fedavg<MODE, U, W, NT, TB><<<grid_for(ncol, (int64_t)TB * W, persistent), TB, 0, s>>>(a, ncol);
+    return hipGetLastError();
+}
+
 template <int MODE>
 hipError_t dispatch_fedavg(const FedavgArgs& a, int64_t ncol, hipStream_t s) {
-    const unsigned g = grid_for(ncol, a.variant);
     switch (a.variant) {
-    case 0: case 1: k_fedavg<MODE, 8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
-    case 2: case 3: k_fedavg<MODE, 8, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
-    case 4: case 5: k_fedavg<MODE, 16, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 0: return go_fedavg<MODE, 8, 1, true, 256>(a, ncol, false, s);
+    case 1: return go_fedavg<MODE, 8, 1, true, 256>(a, ncol, true, s);
+    case 2: return go_fedavg<MODE, 8, 1, false, 256>(a, ncol, false, s);
+    case 3: return go_fedavg<MODE, 8, 1, false, 256>(a, ncol, true, s);
+    case 4: return go_fedavg<MODE, 16, 1, false, 256>(a, ncol, false, s);
+    case 5: return go_fedavg<MODE, 16, 1, false, 256>(a, ncol, true, s);
+    case 6: return go_fedavg<MODE, 16, 1, true, 256>(a, ncol, false, s);
+    case 7: return go_fedavg<MODE, 4, 2, true, 256>(a, ncol, false, s);
+    case 8: return go_fedavg<MODE, 8, 2, true, 256>(a, ncol, false, s);
+    case 9: return go_fedavg<MODE, 8, 1, true, 512>(a, ncol, false, s);
+    case 10: return go_fedavg<MODE, 4, 1, true, 256>(a, ncol, false, s);
     default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 }  // namespace
@@ -267,12 +311,14 @@ hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s) {
     if (!(a.flags & FL_FINAL) && !a.acc) return hipErrorInvalidValue;
     if (!(a.flags & FL_FIRST) && !a.acc) return hipErrorInvalidValue;
     const int64_t ncol = (a.p + 1) / 2;
-    const unsigned g = grid_for(ncol, a.variant);
-    switch (a.variant) {
-    case 0: case 1: k_secagg<8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    if (a.variant < 0 || a.variant >= N_VARIANTS) return hipErrorInvalidValue;
+    const unsigned g = grid_for(ncol, BLOCK, a.variant == 1 || a.variant == 3 || a.variant == 5);
+    switch (a.variant) {  // same load policy / depth as the fedavg variant of that id
     case 2: case 3: k_secagg<8, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
     case 4: case 5: k_secagg<16, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
-    default: return hipErrorInvalidValue;
+    case 6: k_secagg<16, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 7: case 10: k_secagg<4, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    default: k_secagg<8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
     }
     return hipGetLastError();
 }

@@ -3,10 +3,10 @@
 syft-proto (``apps/node/poetry.lock:1731-1734``) is not in the image and no ``.proto`` file
 or serialized fixture exists under the reference, so these field numbers are the build's
 restatement, flagged "parity unpinned" in DESIGN.md.  They must agree with the constants in
-``csrc/pgh_state.h``; ``tests/test_state_codec.py`` checks the C++ walker against Google's
+``csrc/pgh_state.h``; ``tests/test_host_logic.py`` checks the C++ walker against Google's
 protobuf runtime driven by this schema.
 
-``descriptor()`` builds the messages with ``google.protobuf`` at run time (the runtime is
+``classes()`` builds the messages with ``google.protobuf`` at run time (the runtime is
 importable here; ``protoc`` is not), which the tests use to produce State bytes the way a
 client's syft stack would.
 """
@@ -124,3 +124,47 @@ def parse_state(pb: bytes):
         shape = tuple(tt.contents_data.shape.dims)
         out.append(np.asarray(tt.contents_data.contents_float32, dtype=np.float32).reshape(shape))
     return out
+
+
+def _varint(x: int) -> bytes:
+    out = bytearray()
+    x &= (1 << 64) - 1
+    while True:
+        b = x & 0x7F
+        x >>= 7
+        if x:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _field(num: int, wt: int, payload: bytes = b"", value: int = None) -> bytes:
+    key = _varint((num << 3) | wt)
+    if wt == 0:
+        return key + _varint(value)
+    return key + _varint(len(payload)) + payload
+
+
+def build_state_fast(tensors, ids=None) -> bytes:
+    """Byte-identical to ``build_state(tensors, ids)`` (as_param=False) without going through
+    per-element Python protobuf calls: the float payload is spliced in as raw little-endian
+    bytes.  For building large synthetic diffs (bench, tests)."""
+    import numpy as np
+
+    parts = []
+    for k, t in enumerate(tensors):
+        tid = ids[k] if ids is not None else 1000 + k
+        pid = _field(2, 0, value=tid) if tid else b""
+        ph = _field(1, 2, pid) + _field(2, 2, f"#state-{k}".encode())
+        parts.append(_field(1, 2, ph))
+    for k, t in enumerate(tensors):
+        a = np.ascontiguousarray(t, dtype="<f4")
+        tid = ids[k] if ids is not None else 1000 + k
+        dims = b"".join(_varint(d) for d in a.shape)
+        td = (_field(1, 2, _field(1, 2, dims) if dims else b"") + _field(2, 2, b"float32")
+              + (_field(12, 2, a.tobytes()) if a.size else b""))
+        tt = (_field(1, 2, _field(2, 0, value=tid) if tid else b"") + _field(2, 0, value=SERIALIZER_ALL)
+              + _field(4, 2, td))
+        parts.append(_field(2, 2, _field(1, 2, tt)))
+    return b"".join(parts)

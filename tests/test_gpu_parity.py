@@ -50,7 +50,7 @@ def test_engine_reports_device(engine):
     assert device_count() >= 1
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", list(range(11)))
 def test_edge_fixtures_all_modes(engine, gold, variant):
     z = np.load(gold / "edge_f32.npz")
     engine.set_variant(variant)
@@ -61,7 +61,24 @@ def test_edge_fixtures_all_modes(engine, gold, variant):
                 got = run_f32(engine, d, c, mode, w if mode == 2 else None)
                 assert same(got, z[f"{name}_{key}"]), (name, key, variant)
     finally:
-        engine.set_variant(0)
+        engine.set_variant(-1)
+
+
+@pytest.mark.parametrize("variant", list(range(11)))
+def test_variants_mid_size(engine, variant):
+    """Full tiles and a partial last tile for every variant (W = 2 tiles are 512 columns)."""
+    rng = np.random.default_rng(variant)
+    P, N = 100_003, 19
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    w = rng.uniform(0.5, 2.0, N).astype(F)
+    engine.set_variant(variant)
+    try:
+        for mode in (0, 1, 2):
+            got = run_f32(engine, d, c, mode, w if mode == 2 else None)
+            assert same(got, coracle.fedavg(mode, d, c, w if mode == 2 else None)), (variant, mode)
+    finally:
+        engine.set_variant(-1)
 
 
 def test_kat_avg_plan(engine, gold):
@@ -128,7 +145,7 @@ def test_secagg_wrap(engine, gold):
     assert np.array_equal(s2, z["sum"]) and np.array_equal(bits(d2), bits(z["dec_base2_prec16"]))
 
 
-@pytest.mark.parametrize("variant", [0, 3])
+@pytest.mark.parametrize("variant", [0, 3, 6, 7])
 def test_secagg_synthetic_sampled(engine, variant):
     """250 clients x 2 parties x 1M params generated on the GPU; bit-exact on a sampled subset."""
     import torch
@@ -144,7 +161,7 @@ def test_secagg_synthetic_sampled(engine, variant):
         engine.secagg_device(s.data_ptr(), d.data_ptr())
         torch.cuda.synchronize()
     finally:
-        engine.set_variant(0)
+        engine.set_variant(-1)
     idx = np.unique(np.concatenate([np.arange(0, 64), np.random.default_rng(1).integers(0, P, 2000), [P - 1]]))
     want = np.zeros(idx.size, np.uint64)
     with np.errstate(over="ignore"):

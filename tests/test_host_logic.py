@@ -209,3 +209,11 @@ def test_state_patch_rejects_wrong_value_count():
     pb = build_state([np.ones(5, F)])
     with pytest.raises(StateParseError):
         state.serialize_model_params(pb, np.zeros(4, F))
+
+
+def test_build_state_fast_is_byte_identical():
+    from pygrid_amd.state_schema import build_state_fast
+
+    for ts in (_tensors(3), [np.zeros((0,), F), np.ones((2, 3), F), np.array([1.5], F)]):
+        assert build_state_fast(ts) == build_state(ts)
+        assert build_state_fast(ts, ids=[7, 0, 99, 5][:len(ts)]) == build_state(ts, ids=[7, 0, 99, 5][:len(ts)])
