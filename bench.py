@@ -59,6 +59,7 @@ def parse():
     ap.add_argument("--params", type=int, default=None, help="params per GPU shard")
     ap.add_argument("--variant", type=int, default=None)
     ap.add_argument("--ring", type=int, default=None, help="stream workloads: HBM ring slots")
+    ap.add_argument("--gather-chunks", type=int, default=8, help="N > 1: fold ranges overlapped with all-gather")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -115,9 +116,16 @@ class Ctx:
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         if self.world != args.gpus and self.rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE {self.world}", file=sys.stderr)
-        torch.cuda.set_device(self.local)
+        # PGH_BENCH_DEVICE / PGH_DIST_BACKEND only exist to rehearse the N > 1 path with several
+        # ranks on one GPU over gloo; the driver's runs use one GPU per rank and RCCL ("nccl").
+        self.device = int(os.environ.get("PGH_BENCH_DEVICE", self.local))
+        self.backend = os.environ.get("PGH_DIST_BACKEND", "nccl")
+        torch.cuda.set_device(self.device)
         if self.world > 1:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.device))
+            else:
+                dist.init_process_group(self.backend)
 
     def barrier(self):
         if self.world > 1:
@@ -198,11 +206,18 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
         eng.synth_ckpt_device(args.seed, ckpt.data_ptr(), sp)
         if mode == 2:
             eng.set_weights([(c % 7 + 1) * 0.5 for c in range(N)])
+        if ctx.world > 1:
+            # fold the shard in 8 param ranges; RCCL all-gathers range i beside the fold of i + 1
+            from pygrid_amd.sharding import OverlappedGather
+            og = OverlappedGather(P, ctx.world, ctx.rank, chunks=args.gather_chunks)
+            lp = og.local.data_ptr()
 
-        def step():
-            eng.fedavg_device(mode, ckpt.data_ptr(), out.data_ptr(), sp)
-            if ctx.world > 1:
-                gather_flat(out, P, ctx.world, ctx.rank)
+            def step():
+                og.run(lambda off, n: eng.fedavg_device_range(mode, off, n, ckpt.data_ptr(), lp, sp))
+                og.assemble()
+        else:
+            def step():
+                eng.fedavg_device(mode, ckpt.data_ptr(), out.data_ptr(), sp)
         diff_bytes, dt, kernel = 4 * N * pg, "f32", "k_fedavg"
     else:
         s_out = torch.empty(pg, dtype=torch.int64, device="cuda")
@@ -219,7 +234,9 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
     cfg = {"workload": f"{args.workload}: P_shard={pg} params/GPU x {N} clients"
                        + (f" x {parties} parties int64" if dtype == 1 else " fp32") + ", resident in HBM",
            "clients": N, "params_per_gpu": pg, "params_total": P,
-           "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
+           "parallelism": f"param-shard{ctx.world}" + (
+               f" + RCCL all-gather ({args.gather_chunks} ranges overlapped with the fold)" if ctx.world > 1 and dtype == 0
+               else " + RCCL all-gather" if ctx.world > 1 else ""),
            "kernel_variant": args.variant if args.variant is not None else 6}
     rec = record(ctx, args, args.workload, value, el, dt, cfg,
                  roofline_of(st, args.workload, cfg["kernel_variant"], kernel))
@@ -411,7 +428,7 @@ def main():
     Pg = args.params or pg_default
     P = Pg * ctx.world
     lo, hi = shard_bounds(P, ctx.world, ctx.rank)
-    eng = Engine(ctx.local)
+    eng = Engine(ctx.device)
     eng.set_layout([P])
     eng.set_shard(lo, hi)
     if args.variant is not None:

@@ -116,6 +116,11 @@ int pgh_fedavg(pgh_ctx* ctx, int mode, const float* ckpt, float* out);
 /* Same with device pointers (16-byte aligned, P_shard floats) on caller stream `stream`
  * (a hipStream_t; NULL = the context's own stream).  Nothing is copied to the host. */
 int pgh_fedavg_device(pgh_ctx* ctx, int mode, const float* d_ckpt, float* d_out, void* stream);
+/* Only the shard-relative param range [off, off + len) (off a multiple of 4): lets a caller
+ * overlap the collective that ships finished ranges with the fold of the next one.  d_ckpt and
+ * d_out are the shard base pointers. */
+int pgh_fedavg_device_range(pgh_ctx* ctx, int mode, int64_t off, int64_t len, const float* d_ckpt, float* d_out,
+                            void* stream);
 /* Z_2^64 share sum over all clients x parties, then decode float32(sum) / base**prec.
  * sum_out (int64) and dec_out (float32) are host arrays of P_shard; either may be NULL. */
 int pgh_secagg(pgh_ctx* ctx, int base, int prec, int64_t* sum_out, float* dec_out);

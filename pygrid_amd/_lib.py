@@ -59,6 +59,7 @@ SIGNATURES = {
     "pgh_set_weights": (_i, [_vp, C.POINTER(C.c_float), _i]),
     "pgh_fedavg": (_i, [_vp, _i, _vp, _vp]),
     "pgh_fedavg_device": (_i, [_vp, _i, _vp, _vp, _vp]),
+    "pgh_fedavg_device_range": (_i, [_vp, _i, _i64, _i64, _vp, _vp, _vp]),
     "pgh_secagg": (_i, [_vp, _i, _i, _vp, _vp]),
     "pgh_secagg_device": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pgh_synth_ckpt_device": (_i, [_vp, _u64, _vp, _vp]),

@@ -331,11 +331,13 @@ float weight_total(const std::vector<float>& w, int64_t n) {  // left fold, floa
 // Fold slots holding clients [c0, c0 + n) (slot order may wrap) into the running state.
 // FIRST when c0 == 0; FINAL writes out (fedavg: ckpt - avg; secagg: sum/dec) instead of the state.
 struct FinalArgs {
-    const float* ckpt = nullptr;
+    const float* ckpt = nullptr;  // shard base pointers; the launch touches [off, off + len)
     float* out = nullptr;
     int64_t* sum = nullptr;
     float* dec = nullptr;
     float divisor = 1.f;
+    int64_t off = 0;   // param range within the shard
+    int64_t len = -1;  // -1 = to the end of the shard
 };
 
 int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const FinalArgs& fa, hipStream_t s) {
@@ -347,6 +349,11 @@ int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const Fina
         RC(sync_weights(c, s));
     }
     const int R = c->slots;
+    const int64_t off = fa.off;
+    const int64_t len = fa.len < 0 ? c->pg - off : fa.len;
+    if (off < 0 || (off & 3) || len <= 0 || off + len > c->pg)
+        return fail(c, PGH_E_ARG, "param range [%lld,+%lld) outside the shard or not 4-aligned", (long long)off,
+                    (long long)len);
     int64_t done = 0;
     do {
         const int slot = (int)((c0 + done) % R);
@@ -354,16 +361,16 @@ int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const Fina
         const bool first = (c0 + done == 0);
         const bool last = (done + seg == n);
         const int flags = (first ? pgh::FL_FIRST : 0) | (final && last ? pgh::FL_FINAL : 0);
-        const uint64_t pg = (uint64_t)c->pg;
+        const uint64_t pg = (uint64_t)len;
         if (kind == KIND_SECAGG) {
             pgh::SecaggArgs a{};
-            a.shares = (const int64_t*)slot_row(c, slot, 0);
+            a.shares = (const int64_t*)slot_row(c, slot, 0) + off;
             a.ld = c->ld;
             a.n_rows = (int)(seg * c->parties);
-            a.p = c->pg;
-            a.acc = c->d_uacc;
-            a.sum_out = fa.sum;
-            a.dec_out = fa.dec;
+            a.p = len;
+            a.acc = c->d_uacc + off;
+            a.sum_out = fa.sum ? fa.sum + off : nullptr;
+            a.dec_out = fa.dec ? fa.dec + off : nullptr;
             a.divisor = fa.divisor;
             a.flags = flags;
             a.variant = c->variant;
@@ -372,15 +379,15 @@ int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const Fina
             RC(timed_launch(c, s, bytes, [&] { return pgh::launch_secagg(a, s); }));
         } else {
             pgh::FedavgArgs a{};
-            a.diffs = (const float*)slot_row(c, slot, 0);
+            a.diffs = (const float*)slot_row(c, slot, 0) + off;
             a.ld = c->ld;
             a.n_rows = (int)seg;
             a.client0 = c0 + done;
-            a.p = c->pg;
+            a.p = len;
             a.weights = c->d_w ? c->d_w + (c0 + done) : nullptr;
-            a.acc = c->d_acc;
-            a.ckpt = fa.ckpt;
-            a.out = fa.out;
+            a.acc = c->d_acc + off;
+            a.ckpt = fa.ckpt ? fa.ckpt + off : nullptr;
+            a.out = fa.out ? fa.out + off : nullptr;
             a.divisor = fa.divisor;
             a.flags = flags;
             a.mode = kind;
@@ -804,6 +811,24 @@ int pgh_fedavg_device(pgh_ctx* c, int mode, const float* d_ckpt, float* d_out, v
     RC(fedavg_divisor(c, mode, n, &fa.divisor));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     return fold_run(c, mode, 0, n, true, fa, s);
+}
+
+int pgh_fedavg_device_range(pgh_ctx* c, int mode, int64_t off, int64_t len, const float* d_ckpt, float* d_out,
+                            void* stream) {
+    RC(check_dtype(c, PGH_F32));
+    if (!valid_mode(mode)) return fail(c, PGH_E_ARG, "unknown averaging mode %d", mode);
+    if (!d_ckpt || !d_out || (((uintptr_t)d_ckpt | (uintptr_t)d_out) & 15))
+        return fail(c, PGH_E_ARG, "d_ckpt / d_out must be 16-byte aligned device pointers");
+    DeviceGuard g(c->device);
+    int64_t n = 0;
+    RC(resident_count(c, &n));
+    FinalArgs fa;
+    fa.ckpt = d_ckpt;
+    fa.out = d_out;
+    fa.off = off;
+    fa.len = len;
+    RC(fedavg_divisor(c, mode, n, &fa.divisor));
+    return fold_run(c, mode, 0, n, true, fa, stream ? (hipStream_t)stream : c->stream);
 }
 
 int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {

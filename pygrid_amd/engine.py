@@ -162,6 +162,12 @@ class Engine:
         self._check(self._lib.pgh_fedavg_device(self._h, int(mode), C.c_void_p(d_ckpt), C.c_void_p(d_out),
                                                 C.c_void_p(stream or None)), "fedavg_device")
 
+    def fedavg_device_range(self, mode: int, off: int, length: int, d_ckpt: int, d_out: int, stream: int = 0):
+        """Fold only the shard-relative param range [off, off + length) (off % 4 == 0)."""
+        self._check(self._lib.pgh_fedavg_device_range(self._h, int(mode), int(off), int(length), C.c_void_p(d_ckpt),
+                                                      C.c_void_p(d_out), C.c_void_p(stream or None)),
+                    "fedavg_device_range")
+
     def secagg(self, base: int = 10, prec: int = 3, want_sum: bool = True,
                want_dec: bool = True) -> Tuple[Optional[np.ndarray], Optional[np.ndarray]]:
         s = np.empty(self.p_shard, dtype=np.int64) if want_sum else None

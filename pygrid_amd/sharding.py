@@ -53,7 +53,7 @@ def gather_flat(shard, P: int, world: int, rank: int, align: int = ALIGN, group=
         send = torch.zeros(s, dtype=shard.dtype, device=shard.device)
         send[: hi - lo].copy_(shard)
     recv = torch.empty(world * s, dtype=shard.dtype, device=shard.device)
-    if hasattr(dist, "all_gather_into_tensor") and send.device.type != "cpu":
+    if send.device.type != "cpu" and dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(recv, send, group=group)
     else:
         dist.all_gather(list(recv.chunk(world)), send, group=group)
@@ -61,3 +61,57 @@ def gather_flat(shard, P: int, world: int, rank: int, align: int = ALIGN, group=
         return recv
     parts = [recv[r * s: r * s + (b - a)] for r, (a, b) in enumerate(all_shard_bounds(P, world, align))]
     return torch.cat(parts)
+
+
+class OverlappedGather:
+    """All-gather the new checkpoint chunk by chunk while later chunks are still being folded.
+
+    The shard is split into ``chunks`` aligned param ranges.  For each range the caller's
+    ``fold_range(off, n)`` enqueues the fold of shard-relative ``[off, off + n)`` into
+    ``self.local`` on the current stream, then an async ``all_gather_into_tensor`` of that range
+    is issued: RCCL's stream waits for that fold only, so gather i runs beside fold i + 1 and
+    only the last range's gather is exposed.  ``assemble()`` returns the flat P-vector.
+    """
+
+    def __init__(self, P: int, world: int, rank: int, chunks: int = 4, device="cuda", dtype=None, group=None,
+                 align: int = ALIGN):
+        import torch
+
+        dtype = dtype or torch.float32
+        self.P, self.world, self.rank, self.group = P, world, rank, group
+        self.s = shard_size(P, world, align)
+        self.lo, self.hi = shard_bounds(P, world, rank, align)
+        self.pg = self.hi - self.lo
+        c = -(-self.s // max(1, chunks))
+        c = -(-c // align) * align
+        self.ranges = [(a, min(a + c, self.s)) for a in range(0, self.s, c)]
+        self.local = torch.zeros(self.s, dtype=dtype, device=device)
+        self.recv = [torch.empty(world * (b - a), dtype=dtype, device=device) for a, b in self.ranges]
+
+    def run(self, fold_range):
+        import torch.distributed as dist
+
+        works = []
+        for (a, b), r in zip(self.ranges, self.recv):
+            n = min(b, self.pg) - a
+            if n > 0:
+                fold_range(a, n)
+            if self.world > 1:
+                if r.device.type != "cpu" and dist.get_backend(self.group) == "nccl":
+                    works.append(dist.all_gather_into_tensor(r, self.local[a:b], group=self.group, async_op=True))
+                else:
+                    works.append(dist.all_gather(list(r.chunk(self.world)), self.local[a:b], group=self.group,
+                                                 async_op=True))
+            else:
+                r.copy_(self.local[a:b])
+        for w in works:
+            w.wait()
+
+    def assemble(self):
+        import torch
+
+        out = torch.empty(self.world * self.s, dtype=self.local.dtype, device=self.local.device)
+        grid = out.view(self.world, self.s)
+        for (a, b), r in zip(self.ranges, self.recv):
+            grid[:, a:b].copy_(r.view(self.world, b - a))
+        return out[: self.P]

@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pygrid_amd.sharding import all_shard_bounds, gather_flat, shard_bounds
+from pygrid_amd.sharding import OverlappedGather, all_shard_bounds, gather_flat, shard_bounds
 
 
 def _free_port():
@@ -41,6 +41,17 @@ def _worker(rank, world, port, P, N, mode, q):
         else:
             part = np.empty(0, np.float32)
         full = gather_flat(torch.from_numpy(part), P, world, rank)
+        # chunked fold + overlapped all-gather (what bench.py runs at N > 1)
+        og = OverlappedGather(P, world, rank, chunks=3, device="cpu")
+
+        def fold_range(off, n):
+            w = np.linspace(0.5, 2.0, N).astype(np.float32)
+            og.local[off:off + n] = torch.from_numpy(coracle.fedavg(
+                mode, np.ascontiguousarray(d[:, lo + off:lo + off + n]), c[lo + off:lo + off + n],
+                w if mode == 2 else None))
+        og.run(fold_range)
+        full2 = og.assemble()
+        assert torch.equal(full2.view(torch.int32), full.view(torch.int32))
         # timing contract of bench.py: max over ranks
         t = torch.tensor([float(rank + 1)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

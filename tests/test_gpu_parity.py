@@ -272,3 +272,24 @@ def test_errors_are_loud(engine):
         engine.fedavg(7, np.zeros(10, F))
     with pytest.raises(AggregationError):
         engine.fedavg(2, np.zeros(10, F))  # weighted without weights
+
+
+def test_fedavg_device_range_pieces_equal_whole(engine):
+    """Folding the shard in param ranges (the multi-GPU overlap path) equals one fold."""
+    import torch
+
+    from pygrid_amd.sharding import OverlappedGather
+
+    rng = np.random.default_rng(12)
+    P, N = 200_003, 9
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    whole = run_f32(engine, d, c, 1)
+    ck = torch.from_numpy(c).cuda()
+    og = OverlappedGather(P, 1, 0, chunks=5)
+    lp = og.local.data_ptr()
+    og.run(lambda off, n: engine.fedavg_device_range(1, off, n, ck.data_ptr(), lp))
+    assert same(og.assemble().cpu().numpy(), whole)
+    from pygrid_amd import AggregationError
+    with pytest.raises(AggregationError):
+        engine.fedavg_device_range(1, 2, 10, ck.data_ptr(), lp)  # misaligned range
