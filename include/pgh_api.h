@@ -114,7 +114,8 @@ int pgh_set_weights(pgh_ctx* ctx, const float* w, int n);
  * out = ckpt - avg(diffs), over this context's shard.  Host pointers, P_shard floats each. */
 int pgh_fedavg(pgh_ctx* ctx, int mode, const float* ckpt, float* out);
 /* Same with device pointers (16-byte aligned, P_shard floats) on caller stream `stream`
- * (a hipStream_t; NULL = the context's own stream).  Nothing is copied to the host. */
+ * (a hipStream_t; NULL = the HIP default stream, ordered with other blocking streams).  Nothing
+ * is copied to the host. */
 int pgh_fedavg_device(pgh_ctx* ctx, int mode, const float* d_ckpt, float* d_out, void* stream);
 /* Only the shard-relative param range [off, off + len) (off a multiple of 4): lets a caller
  * overlap the collective that ships finished ranges with the fold of the next one.  d_ckpt and

@@ -768,7 +768,7 @@ int pgh_synth_ckpt_device(pgh_ctx* c, uint64_t seed, float* d_ckpt, void* stream
     if (!c->layout) return fail(c, PGH_E_STATE, "pgh_set_layout has not been called");
     if (!d_ckpt || ((uintptr_t)d_ckpt & 15)) return fail(c, PGH_E_ARG, "d_ckpt must be a 16-byte aligned device pointer");
     DeviceGuard g(c->device);
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;
     if (c->pg % 4 == 0) {  // one row of exactly P_shard elements
         hipError_t e = pgh::launch_synth_f32(d_ckpt, 1, c->pg, c->pg, seed, pgh::STREAM_CKPT, 0, c->lo, pgh::CKPT_SCALE, s);
         if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic checkpoint failed: %s", hipGetErrorString(e));
@@ -809,7 +809,7 @@ int pgh_fedavg_device(pgh_ctx* c, int mode, const float* d_ckpt, float* d_out, v
     fa.ckpt = d_ckpt;
     fa.out = d_out;
     RC(fedavg_divisor(c, mode, n, &fa.divisor));
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;
     return fold_run(c, mode, 0, n, true, fa, s);
 }
 
@@ -828,7 +828,7 @@ int pgh_fedavg_device_range(pgh_ctx* c, int mode, int64_t off, int64_t len, cons
     fa.off = off;
     fa.len = len;
     RC(fedavg_divisor(c, mode, n, &fa.divisor));
-    return fold_run(c, mode, 0, n, true, fa, stream ? (hipStream_t)stream : c->stream);
+    return fold_run(c, mode, 0, n, true, fa, (hipStream_t)stream);
 }
 
 int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
@@ -854,7 +854,7 @@ int pgh_secagg_device(pgh_ctx* c, int base, int prec, int64_t* d_sum, float* d_d
     fa.sum = d_sum;
     fa.dec = d_dec;
     RC(fixed_point_divisor(c, base, prec, &fa.divisor));
-    return fold_run(c, KIND_SECAGG, 0, n, true, fa, stream ? (hipStream_t)stream : c->stream);
+    return fold_run(c, KIND_SECAGG, 0, n, true, fa, (hipStream_t)stream);
 }
 
 int pgh_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out) {
@@ -920,7 +920,7 @@ int pgh_stream_finish_device(pgh_ctx* c, const float* d_ckpt, float* d_out, void
     FinalArgs fa;
     fa.ckpt = d_ckpt;
     fa.out = d_out;
-    return stream_finish(c, fa, stream ? (hipStream_t)stream : c->stream, true, c->kind);
+    return stream_finish(c, fa, (hipStream_t)stream, true, c->kind);
 }
 
 int pgh_stream_finish(pgh_ctx* c, const float* ckpt, float* out) {
@@ -944,7 +944,7 @@ int pgh_stream_finish_secagg_device(pgh_ctx* c, int base, int prec, int64_t* d_s
     fa.sum = d_sum;
     fa.dec = d_dec;
     RC(fixed_point_divisor(c, base, prec, &fa.divisor));
-    return stream_finish(c, fa, stream ? (hipStream_t)stream : c->stream, false, base);
+    return stream_finish(c, fa, (hipStream_t)stream, false, base);
 }
 
 int pgh_stream_finish_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out) {
