@@ -89,8 +89,10 @@ def cpu_baseline(P: int, seed: int, budget_s: float, n: int = 32):
             "cycle_close_ms_per_1000_clients": round(el / reps / n * 1000 * 1000, 1)}
 
 
-def load_traffic(workload: str, variant: int):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/), if present."""
+def load_traffic(workload: str, variant: int, alg_bytes: float):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/pmc_traffic.json).
+    When this launch's algorithmic bytes differ from the profiled launch's (e.g. a range-split
+    fold at N > 1), the measured traffic/algorithmic ratio is applied and the source says so."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
         return None, None
@@ -98,7 +100,9 @@ def load_traffic(workload: str, variant: int):
         e = json.loads(f.read_text()).get(workload, {}).get(str(variant))
         if e is None:
             return None, None
-        return float(e["hbm_bytes_per_launch"]), e.get("source")
+        if abs(float(e.get("alg_bytes_per_launch", alg_bytes)) - alg_bytes) <= 1e-6 * alg_bytes:
+            return float(e["hbm_bytes_per_launch"]), e.get("source")
+        return float(e["ratio"]) * alg_bytes, f"{e.get('source')}; ratio {e['ratio']:.6f} applied to this launch"
     except Exception:
         return None, None
 
@@ -186,7 +190,7 @@ def roofline_of(st, workload, variant, kernel):
     ms = st["kernel_ms_total"] / max(st["kernel_launches"], 1)
     alg = st["kernel_bytes_total"] / max(st["kernel_launches"], 1)
     achieved = alg / (ms / 1e3) / 1e9
-    traffic, src = load_traffic(workload, variant)
+    traffic, src = load_traffic(workload, variant, alg)
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
             "kernel_ms_avg": round(ms, 4), "alg_bytes_per_launch": int(alg), "launches": st["kernel_launches"],

@@ -293,3 +293,54 @@ def test_fedavg_device_range_pieces_equal_whole(engine):
     from pygrid_amd import AggregationError
     with pytest.raises(AggregationError):
         engine.fedavg_device_range(1, 2, 10, ck.data_ptr(), lp)  # misaligned range
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 63, 64, 65])
+@pytest.mark.parametrize("N", [1, 2, 9, 17])
+def test_tiny_shapes(engine, P, N):
+    rng = np.random.default_rng(P * 100 + N)
+    d = rng.standard_normal((N, P)).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    w = rng.uniform(0.5, 2, N).astype(F)
+    for mode in (0, 1, 2):
+        assert same(run_f32(engine, d, c, mode, w if mode == 2 else None),
+                    coracle.fedavg(mode, d, c, w if mode == 2 else None)), (P, N, mode)
+
+
+def test_state_ingest_into_shards(engine):
+    """State bytes ingested by param-shard contexts: each takes its slice of the payload spans."""
+    from pygrid_amd import Engine
+    from pygrid_amd.sharding import all_shard_bounds
+    from pygrid_amd.state_schema import build_state_fast
+
+    rng = np.random.default_rng(21)
+    shapes = [(13, 7), (5,), (300,), (64, 3), (1,)]
+    numel = [int(np.prod(s)) for s in shapes]
+    P = sum(numel)
+    diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for _ in range(6)]
+    flat = np.stack([np.concatenate([t.reshape(-1) for t in d]) for d in diffs])
+    c = rng.standard_normal(P).astype(F)
+    want = coracle.fedavg(0, flat, c)
+    parts = []
+    with Engine(engine.device) as e2:
+        e2.set_layout(numel)
+        for lo, hi in all_shard_bounds(P, 3, align=4):
+            e2.set_shard(lo, hi)
+            e2.reserve(len(diffs))
+            for k, d in enumerate(diffs):
+                e2.ingest_state(k, build_state_fast(d))
+            parts.append(e2.fedavg(0, c[lo:hi]))
+    assert same(np.concatenate(parts), want)
+
+
+def test_ingest_shard_sized_buffer(engine):
+    rng = np.random.default_rng(22)
+    P, N = 1000, 4
+    d = rng.standard_normal((N, P)).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    engine.set_layout([P])
+    engine.set_shard(200, 700)
+    engine.reserve(N)
+    for k in range(N):
+        engine.ingest(k, d[k] if k % 2 else d[k, 200:700].copy())  # whole model or shard slice
+    assert same(engine.fedavg(0, c[200:700]), coracle.fedavg(0, d, c)[200:700])
