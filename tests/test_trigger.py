@@ -1,0 +1,111 @@
+"""CPU: cycle-close trigger -- single flight like run_task_once (tasks/cycle.py:9-25), but a
+report that lands during an in-flight close is replayed instead of dropped, and a cycle's end
+time fires the readiness check without waiting for another report (cycle_manager.py:202)."""
+import threading
+import time
+from datetime import datetime, timedelta
+
+from oracle import oracle as O
+from pygrid_amd.trigger import CycleCloseTrigger
+
+
+class FakeNode:
+    """complete_cycle with the reference's readiness predicate (cycle_manager.py:196-210)."""
+
+    def __init__(self, server_config, end=None, work_s=0.05):
+        self.cfg = server_config
+        self.end = end
+        self.received = 0
+        self.closed = False
+        self.concurrent = 0
+        self.max_concurrent = 0
+        self.work_s = work_s
+        self.lock = threading.Lock()
+
+    def complete_cycle(self, cycle_id):
+        with self.lock:
+            self.concurrent += 1
+            self.max_concurrent = max(self.max_concurrent, self.concurrent)
+            n = self.received
+        try:
+            if not self.closed and O.ready_to_average(self.cfg, n, self.end, datetime.now()):
+                time.sleep(self.work_s)  # the average
+                self.closed = True
+        finally:
+            with self.lock:
+                self.concurrent -= 1
+
+
+def test_report_during_inflight_close_is_not_lost():
+    node = FakeNode({"min_diffs": 1}, work_s=0.2)
+    node.received = 1
+    seen = []
+
+    def fn(cid):
+        seen.append(cid)
+        node.complete_cycle(cid)
+
+    trig = CycleCloseTrigger(fn)
+    trig.request(1)
+    time.sleep(0.05)          # the close of cycle 1 is in flight
+    trig.request(2)           # the reference would log "Skipping" and drop this
+    assert trig.wait_idle(5)
+    assert seen == [1, 2]
+    assert node.max_concurrent == 1  # still one close at a time
+
+
+def test_last_report_during_inflight_close_still_closes():
+    node = FakeNode({"min_diffs": 3, "max_diffs": 3}, work_s=0.01)
+    slow_started = threading.Event()
+    release = threading.Event()
+
+    def fn(cid):
+        if node.received == 2 and not slow_started.is_set():
+            slow_started.set()
+            release.wait(5)        # a readiness check (not ready yet) that is still running...
+        node.complete_cycle(cid)
+
+    trig = CycleCloseTrigger(fn)
+    node.received = 2
+    trig.request(7)
+    assert slow_started.wait(5)
+    node.received = 3              # ...when the final report lands
+    trig.request(7)
+    release.set()
+    assert trig.wait_idle(5)
+    assert node.closed             # with run_task_once the cycle would stay open
+
+
+def test_deadline_closes_without_another_report():
+    end = datetime.now() + timedelta(seconds=0.3)
+    node = FakeNode({"min_diffs": 1, "max_diffs": 10}, end=end, work_s=0.0)
+    trig = CycleCloseTrigger(node.complete_cycle)
+    node.received = 2
+    trig.request(3)                # report arrives: min met, max not hit, deadline not reached
+    assert trig.wait_idle(5) and not node.closed
+    trig.schedule_deadline(3, end)
+    time.sleep(0.6)
+    assert trig.wait_idle(5)
+    assert node.closed
+    trig.shutdown()
+
+
+def test_errors_are_logged_and_swallowed():
+    def boom(cid):
+        raise RuntimeError("engine failure")
+
+    trig = CycleCloseTrigger(boom)
+    trig.request(1)
+    assert trig.wait_idle(5)
+    assert trig.errors == 1 and trig.runs == 1
+    trig.request(2)
+    assert trig.wait_idle(5) and trig.runs == 2
+
+
+def test_cancel_deadline():
+    fired = []
+    trig = CycleCloseTrigger(lambda cid: fired.append(cid))
+    trig.schedule_deadline(5, datetime.now() + timedelta(seconds=0.2))
+    trig.cancel_deadline(5)
+    time.sleep(0.4)
+    assert fired == []
