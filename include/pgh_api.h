@@ -122,6 +122,18 @@ int pgh_fedavg_device(pgh_ctx* ctx, int mode, const float* d_ckpt, float* d_out,
  * d_out are the shard base pointers. */
 int pgh_fedavg_device_range(pgh_ctx* ctx, int mode, int64_t off, int64_t len, const float* d_ckpt, float* d_out,
                             void* stream);
+/* ---- resident checkpoint: keep the model in HBM across cycles ---------
+ * Upload the current checkpoint once (flat floats: the whole model or this shard; or straight
+ * from its State bytes), fold with pgh_fedavg_resident -- the result replaces the resident
+ * checkpoint, so the next cycle needs no checkpoint upload -- and read it back as floats or as
+ * State bytes (the template's payload spans overwritten, like pgh_state_patch). */
+int pgh_ckpt_upload(pgh_ctx* ctx, const float* ckpt, size_t nbytes);
+int pgh_ckpt_upload_state(pgh_ctx* ctx, const uint8_t* pb, size_t n);
+int pgh_fedavg_resident(pgh_ctx* ctx, int mode);
+int pgh_ckpt_download(pgh_ctx* ctx, float* out);  /* P_shard floats */
+/* out (n bytes) = tmpl with this shard's slice of every payload taken from the resident checkpoint. */
+int pgh_ckpt_patch_state(pgh_ctx* ctx, const uint8_t* tmpl, size_t n, uint8_t* out);
+
 /* Z_2^64 share sum over all clients x parties, then decode float32(sum) / base**prec.
  * sum_out (int64) and dec_out (float32) are host arrays of P_shard; either may be NULL. */
 int pgh_secagg(pgh_ctx* ctx, int base, int prec, int64_t* sum_out, float* dec_out);

@@ -60,6 +60,11 @@ SIGNATURES = {
     "pgh_fedavg": (_i, [_vp, _i, _vp, _vp]),
     "pgh_fedavg_device": (_i, [_vp, _i, _vp, _vp, _vp]),
     "pgh_fedavg_device_range": (_i, [_vp, _i, _i64, _i64, _vp, _vp, _vp]),
+    "pgh_ckpt_upload": (_i, [_vp, _vp, _sz]),
+    "pgh_ckpt_upload_state": (_i, [_vp, C.c_char_p, _sz]),
+    "pgh_fedavg_resident": (_i, [_vp, _i]),
+    "pgh_ckpt_download": (_i, [_vp, _vp]),
+    "pgh_ckpt_patch_state": (_i, [_vp, C.c_char_p, _sz, _vp]),
     "pgh_secagg": (_i, [_vp, _i, _i, _vp, _vp]),
     "pgh_secagg_device": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pgh_synth_ckpt_device": (_i, [_vp, _u64, _vp, _vp]),

@@ -28,6 +28,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -279,6 +280,76 @@ int stage_h2d(pgh_ctx* c, void* dst, const uint8_t* src, size_t n, bool pinned_s
     CK(c, hipStreamSynchronize(c->copy));
     c->st.h2d_ms_total += now_ms() - t0;
     c->st.h2d_bytes_total += n;
+    return PGH_OK;
+}
+
+struct OutPiece {
+    uint8_t* dst;
+    size_t n;
+};
+
+// Copy bytes [off, off + len) of the concatenation of `pieces` from `src`.
+void scatter_out(const uint8_t* src, size_t off, size_t len, const std::vector<OutPiece>& pieces, int threads) {
+    size_t base = 0;
+    for (auto& p : pieces) {
+        const size_t a = std::max(off, base), b = std::min(off + len, base + p.n);
+        if (a < b) par_memcpy(p.dst + (a - base), src + (a - off), b - a, threads);
+        base += p.n;
+        if (base >= off + len) break;
+    }
+}
+
+// HBM bytes at `src` (after the work already on stream `s`) -> host pieces, through the pinned
+// ring: the DMA of one slot overlaps the host copy-out of the previous one.
+int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>& pieces, hipStream_t s) {
+    size_t total = 0;
+    for (auto& p : pieces) total += p.n;
+    size_t off = 0;
+    int prev_slot = -1;
+    size_t prev_off = 0, prev_len = 0;
+    while (off < total || prev_slot >= 0) {
+        int cur_slot = -1;
+        size_t cur_len = 0;
+        if (off < total) {
+            cur_slot = c->pin_next;
+            c->pin_next ^= 1;
+            if (c->pin_used[cur_slot]) CK(c, hipEventSynchronize(c->pin_ev[cur_slot]));
+            cur_len = std::min(total - off, c->pin_slot);
+            CK(c, hipMemcpyAsync(c->h_pin[cur_slot], src + off, cur_len, hipMemcpyDeviceToHost, s));
+            CK(c, hipEventRecord(c->pin_ev[cur_slot], s));
+            c->pin_used[cur_slot] = true;
+        }
+        if (prev_slot >= 0) {
+            CK(c, hipEventSynchronize(c->pin_ev[prev_slot]));
+            scatter_out(c->h_pin[prev_slot], prev_off, prev_len, pieces, c->copy_threads);
+        }
+        prev_slot = cur_slot;
+        prev_off = off;
+        prev_len = cur_len;
+        off += cur_len;
+    }
+    return PGH_OK;
+}
+
+// The shard's slice of every tensor payload of a State message, as byte ranges of the message.
+int state_shard_spans(pgh_ctx* c, const uint8_t* pb, size_t n, std::vector<std::pair<size_t, size_t>>* out,
+                      const char* what) {
+    std::vector<pgh_state::Span> spans;
+    std::string msg;
+    int rc = pgh_state::scan(pb, n, &spans, &msg);
+    if (rc) return fail(c, rc, "%s State: %s", what, msg.c_str());
+    if (spans.size() != c->numel.size())
+        return fail(c, PGH_E_PARSE, "%s State holds %zu tensors, layout has %zu", what, spans.size(), c->numel.size());
+    out->clear();
+    int64_t off = 0;
+    for (size_t t = 0; t < spans.size(); ++t) {
+        if (spans[t].count != c->numel[t])
+            return fail(c, PGH_E_PARSE, "%s tensor %zu holds %lld floats, layout %lld", what, t,
+                        (long long)spans[t].count, (long long)c->numel[t]);
+        const int64_t a = std::max(off, c->lo), b = std::min(off + spans[t].count, c->hi);
+        if (a < b) out->push_back({spans[t].offset + 4 * (size_t)(a - off), 4 * (size_t)(b - a)});
+        off += spans[t].count;
+    }
     return PGH_OK;
 }
 
@@ -544,7 +615,8 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     c->pin_slot = (pinned_bytes / 2) & ~(size_t)4095;
     if (c->pin_slot < 4096) c->pin_slot = 4096;
     const unsigned hw = std::thread::hardware_concurrency();
-    c->copy_threads = (int)std::max(1u, std::min(8u, hw ? hw : 1u));
+    c->copy_threads = (int)std::max(1u, std::min(16u, hw ? hw : 1u));
+    if (const char* e = std::getenv("PGH_COPY_THREADS")) c->copy_threads = std::max(1, std::atoi(e));
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming) == hipSuccess &&
@@ -689,25 +761,13 @@ int pgh_ingest_raw(pgh_ctx* c, int client, const void* flat, size_t nbytes, int 
 int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
     RC(check_dtype(c, PGH_F32));
     if (!pb && n) return fail(c, PGH_E_ARG, "pb is NULL");
-    std::vector<pgh_state::Span> spans;
-    std::string msg;
-    int rc = pgh_state::scan(pb, n, &spans, &msg);
-    if (rc) return fail(c, rc, "client %d State: %s", client, msg.c_str());
-    if (spans.size() != c->numel.size())
-        return fail(c, PGH_E_PARSE, "client %d State holds %zu tensors, layout has %zu", client, spans.size(),
-                    c->numel.size());
-    // The shard's slice of the concatenated payloads, as pieces of the message itself: the
-    // float32 payload bytes go straight from the protobuf buffer into the pinned ring.
+    // The shard's slice of the payloads goes straight from the protobuf buffer into the pinned ring.
+    std::vector<std::pair<size_t, size_t>> spans;
+    char what[32];
+    snprintf(what, sizeof what, "client %d", client);
+    RC(state_shard_spans(c, pb, n, &spans, what));
     std::vector<Piece> pieces;
-    int64_t off = 0;
-    for (size_t t = 0; t < spans.size(); ++t) {
-        if (spans[t].count != c->numel[t])
-            return fail(c, PGH_E_PARSE, "client %d tensor %zu holds %lld floats, layout %lld", client, t,
-                        (long long)spans[t].count, (long long)c->numel[t]);
-        const int64_t a = std::max(off, c->lo), b = std::min(off + spans[t].count, c->hi);
-        if (a < b) pieces.push_back(Piece{pb + spans[t].offset + 4 * (size_t)(a - off), 4 * (size_t)(b - a)});
-        off += spans[t].count;
-    }
+    for (auto& sp : spans) pieces.push_back(Piece{pb + sp.first, sp.second});
     DeviceGuard g(c->device);
     int slot = 0;
     RC(claim_slot(c, client, &slot));
@@ -837,11 +897,79 @@ int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
     DeviceGuard g(c->device);
     const double t0 = now_ms();
     const size_t bytes = sizeof(float) * (size_t)c->pg;
-    CK(c, hipMemcpyAsync(c->d_ckpt, ckpt, bytes, hipMemcpyHostToDevice, c->stream));
+    RC(stage_h2d(c, c->d_ckpt, (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
     RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
-    CK(c, hipMemcpyAsync(out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
-    CK(c, hipStreamSynchronize(c->stream));
+    if (is_pinned(out)) {
+        CK(c, hipMemcpyAsync(out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
+        CK(c, hipStreamSynchronize(c->stream));
+    } else {
+        RC(stage_d2h_pieces(c, (const uint8_t*)c->d_out, {OutPiece{(uint8_t*)out, bytes}}, c->stream));
+    }
     c->st.close_ms_last = now_ms() - t0;
+    return collect_timings(c);
+}
+
+// ---- resident checkpoint: the new checkpoint stays in HBM as the next cycle's input ------------
+
+int pgh_ckpt_upload(pgh_ctx* c, const float* ckpt, size_t nbytes) {
+    RC(check_dtype(c, PGH_F32));
+    if (!ckpt) return fail(c, PGH_E_ARG, "ckpt is NULL");
+    const size_t whole = 4 * (size_t)c->P, shard = 4 * (size_t)c->pg;
+    if (nbytes != whole && nbytes != shard)
+        return fail(c, PGH_E_ARG, "checkpoint: got %zu bytes, layout needs %zu (model) or %zu (shard)", nbytes, whole,
+                    shard);
+    DeviceGuard g(c->device);
+    const uint8_t* src = (const uint8_t*)ckpt + (nbytes == whole ? 4 * (size_t)c->lo : 0);
+    return stage_h2d(c, c->d_ckpt, src, shard, is_pinned(ckpt));
+}
+
+int pgh_ckpt_upload_state(pgh_ctx* c, const uint8_t* pb, size_t n) {
+    RC(check_dtype(c, PGH_F32));
+    if (!pb && n) return fail(c, PGH_E_ARG, "pb is NULL");
+    std::vector<std::pair<size_t, size_t>> spans;
+    RC(state_shard_spans(c, pb, n, &spans, "checkpoint"));
+    std::vector<Piece> pieces;
+    for (auto& sp : spans) pieces.push_back(Piece{pb + sp.first, sp.second});
+    DeviceGuard g(c->device);
+    return stage_pieces_h2d(c, (uint8_t*)c->d_ckpt, pieces);
+}
+
+int pgh_fedavg_resident(pgh_ctx* c, int mode) {
+    RC(check_dtype(c, PGH_F32));
+    DeviceGuard g(c->device);
+    const double t0 = now_ms();
+    RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
+    std::swap(c->d_ckpt, c->d_out);  // the new checkpoint is the next cycle's input
+    c->st.close_ms_last = now_ms() - t0;
+    return PGH_OK;
+}
+
+int pgh_ckpt_download(pgh_ctx* c, float* out) {
+    RC(check_dtype(c, PGH_F32));
+    if (!out) return fail(c, PGH_E_ARG, "out is NULL");
+    DeviceGuard g(c->device);
+    const size_t bytes = 4 * (size_t)c->pg;
+    RC(order_after_ingest(c, c->stream));
+    if (is_pinned(out)) {
+        CK(c, hipMemcpyAsync(out, c->d_ckpt, bytes, hipMemcpyDeviceToHost, c->stream));
+        CK(c, hipStreamSynchronize(c->stream));
+    } else {
+        RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, {OutPiece{(uint8_t*)out, bytes}}, c->stream));
+    }
+    return collect_timings(c);
+}
+
+int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out) {
+    RC(check_dtype(c, PGH_F32));
+    if (!tmpl || !out) return fail(c, PGH_E_ARG, "tmpl / out is NULL");
+    std::vector<std::pair<size_t, size_t>> spans;
+    RC(state_shard_spans(c, tmpl, n, &spans, "checkpoint template"));
+    DeviceGuard g(c->device);
+    if (out != tmpl) par_memcpy(out, tmpl, n, c->copy_threads);
+    std::vector<OutPiece> pieces;
+    for (auto& sp : spans) pieces.push_back(OutPiece{out + sp.first, sp.second});
+    RC(order_after_ingest(c, c->stream));
+    RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, pieces, c->stream));
     return collect_timings(c);
 }
 

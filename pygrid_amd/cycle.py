@@ -91,6 +91,7 @@ class CycleAggregator:
         self._cap = 0
         self._dtype = None
         self._parties = 0
+        self._resident = None  # the checkpoint bytes object whose params are resident in HBM
 
     def _prepare(self, numel: Sequence[int], n: int, dtype: int = F32, parties: int = 1):
         eng = self.engine
@@ -98,9 +99,11 @@ class CycleAggregator:
         if numel != self._numel:
             eng.set_layout(numel)
             self._numel, self._cap, self._dtype = numel, 0, None
+            self._resident = None
         if n > self._cap or dtype != self._dtype or parties != self._parties:
             eng.reserve(max(n, 1), dtype, parties)
             self._cap, self._dtype, self._parties = max(n, 1), dtype, parties
+            self._resident = None
         else:
             eng.reset()
 
@@ -112,13 +115,16 @@ class CycleAggregator:
         mode = select_mode(server_config, avg_plan, weights)
         numel = state_codec.tensor_numels(checkpoint)  # :240
         self._prepare(numel, len(diffs))
+        if checkpoint is not self._resident:  # the last cycle's output is still in HBM
+            self.engine.ckpt_upload_state(checkpoint)
         for i, d in enumerate(diffs):  # :247-250
             self.engine.ingest_state(i, d)
         if mode == WEIGHTED_MEAN:
             self.engine.set_weights(weights)
-        ckpt = state_codec.flat_params(checkpoint)
-        new = self.engine.fedavg(mode, ckpt)  # :252-296
-        return state_codec.serialize_model_params(checkpoint, new)  # :303
+        self.engine.fedavg_resident(mode)  # :252-296
+        new = self.engine.ckpt_patch_state(checkpoint)  # :303
+        self._resident = new
+        return new
 
     # ---- tensor lists in / out (what the reference holds after unserialize) ---------------------
     def average_params(self, server_config: dict, model_params: Sequence[np.ndarray],

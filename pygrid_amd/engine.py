@@ -168,6 +168,29 @@ class Engine:
                                                       C.c_void_p(d_out), C.c_void_p(stream or None)),
                     "fedavg_device_range")
 
+    # ---- resident checkpoint ---------------------------------------------------------------------
+    def ckpt_upload(self, ckpt: np.ndarray):
+        a = np.ascontiguousarray(ckpt, dtype=np.float32).reshape(-1)
+        self._check(self._lib.pgh_ckpt_upload(self._h, _ptr(a), a.nbytes), "ckpt_upload")
+
+    def ckpt_upload_state(self, pb: bytes):
+        self._check(self._lib.pgh_ckpt_upload_state(self._h, pb, len(pb)), "ckpt_upload_state")
+
+    def fedavg_resident(self, mode: int):
+        """Fold into the resident checkpoint: afterwards it IS the new checkpoint."""
+        self._check(self._lib.pgh_fedavg_resident(self._h, int(mode)), "fedavg_resident")
+
+    def ckpt_download(self) -> np.ndarray:
+        out = np.empty(self.p_shard, dtype=np.float32)
+        self._check(self._lib.pgh_ckpt_download(self._h, _ptr(out)), "ckpt_download")
+        return out
+
+    def ckpt_patch_state(self, template: bytes) -> bytes:
+        """``template`` (State bytes) with this shard's payload slices taken from the resident checkpoint."""
+        out = C.create_string_buffer(len(template))
+        self._check(self._lib.pgh_ckpt_patch_state(self._h, template, len(template), out), "ckpt_patch_state")
+        return out.raw
+
     def secagg(self, base: int = 10, prec: int = 3, want_sum: bool = True,
                want_dec: bool = True) -> Tuple[Optional[np.ndarray], Optional[np.ndarray]]:
         s = np.empty(self.p_shard, dtype=np.int64) if want_sum else None

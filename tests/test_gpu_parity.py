@@ -344,3 +344,38 @@ def test_ingest_shard_sized_buffer(engine):
     for k in range(N):
         engine.ingest(k, d[k] if k % 2 else d[k, 200:700].copy())  # whole model or shard slice
     assert same(engine.fedavg(0, c[200:700]), coracle.fedavg(0, d, c)[200:700])
+
+
+def test_resident_checkpoint_chains_cycles(engine):
+    """Three cycles back to back through State bytes: the new checkpoint stays in HBM and feeds
+    the next cycle (no re-upload when the caller hands the returned bytes back)."""
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(31)
+    shapes = [(64, 33), (33,), (7, 64), (7,)]
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    agg = CycleAggregator(engine)
+    pb = build_state_fast(ckpt)
+    want = ckpt
+    for cyc in range(3):
+        diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for _ in range(4 + cyc)]
+        pb = agg.average_plan_diffs({}, pb, [build_state_fast(d) for d in diffs])
+        want = O.fedavg_mean(want, diffs)
+        for got, w in zip(parse_state(pb), want):
+            assert same(got, w), cyc
+    assert same(engine.ckpt_download(), np.concatenate([w.reshape(-1) for w in want]))
+
+
+def test_resident_api_flat(engine):
+    rng = np.random.default_rng(32)
+    P, N = 5003, 6
+    d = rng.standard_normal((N, P)).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    engine.set_layout([P])
+    engine.reserve(N)
+    engine.ckpt_upload(c)
+    for k in range(N):
+        engine.ingest(k, d[k])
+    engine.fedavg_resident(0)
+    assert same(engine.ckpt_download(), coracle.fedavg(0, d, c))
