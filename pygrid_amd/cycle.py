@@ -143,6 +143,7 @@ class CycleAggregator:
         if mode == WEIGHTED_MEAN:
             self.engine.set_weights(weights)
         flat = np.concatenate([np.asarray(p, np.float32).reshape(-1) for p in model_params])
+        self._resident = None  # the host-buffer fold overwrites the resident checkpoint
         out = self.engine.fedavg(mode, flat)
         res, off = [], 0
         for s, n in zip(shapes, numel):
@@ -158,6 +159,7 @@ class CycleAggregator:
             raise AggregationError("shares must be [clients][parties][P]")
         n, s, p = sh.shape
         self._prepare([p], n, I64, s)
+        self._resident = None
         for c in range(n):
             self.engine.ingest(c, sh[c])
         return self.engine.secagg(base, precision_fractional)
