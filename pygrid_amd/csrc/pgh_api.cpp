@@ -26,6 +26,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -41,6 +44,91 @@
 namespace {
 constexpr int KIND_SECAGG = 3;  // stream kind besides the three fedavg modes
 }
+
+// Host copy engine: a persistent pool that splits one batch of (dst, src, n) segments evenly
+// by bytes across its threads (the caller's thread takes the first share).  Used to fill and
+// drain the pinned staging slots, where payload pieces are many and mostly small.
+class CopyPool {
+  public:
+    struct Seg {
+        uint8_t* dst;
+        const uint8_t* src;
+        size_t n;
+    };
+    explicit CopyPool(int threads) : nthreads_(std::max(1, threads)) {
+        for (int t = 1; t < nthreads_; ++t) workers_.emplace_back([this, t] { loop(t); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& w : workers_) w.join();
+    }
+    int threads() const { return nthreads_; }
+    void run(const std::vector<Seg>& segs) {
+        size_t total = 0;
+        for (auto& sg : segs) total += sg.n;
+        if (total < (4u << 20) || nthreads_ == 1) { copy_range(segs, 0, total); return; }
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            segs_ = &segs;
+            total_ = total;
+            pending_ = nthreads_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        copy_range(segs, 0, share(total, 0));
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [this] { return pending_ == 0; });
+        segs_ = nullptr;
+    }
+
+  private:
+    size_t share(size_t total, int t) const {  // [begin, end) of thread t, 4 KiB granules
+        const size_t per = ((total + nthreads_ - 1) / nthreads_ + 4095) & ~(size_t)4095;
+        return std::min(total, per * (size_t)(t + 1));
+    }
+    static void copy_range(const std::vector<Seg>& segs, size_t a, size_t b) {
+        size_t base = 0;
+        for (auto& sg : segs) {
+            const size_t lo = std::max(a, base), hi = std::min(b, base + sg.n);
+            if (lo < hi) std::memcpy(sg.dst + (lo - base), sg.src + (lo - base), hi - lo);
+            base += sg.n;
+            if (base >= b) break;
+        }
+    }
+    void loop(int t) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::vector<Seg>* segs;
+            size_t total;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                segs = segs_;
+                total = total_;
+            }
+            const size_t a = t == 0 ? 0 : share(total, t - 1);
+            copy_range(*segs, std::min(a, total), share(total, t));
+            std::lock_guard<std::mutex> lk(m_);
+            if (--pending_ == 0) done_cv_.notify_one();
+        }
+    }
+    int nthreads_;
+    std::vector<std::thread> workers_;
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    const std::vector<Seg>* segs_ = nullptr;
+    size_t total_ = 0;
+    int pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
 
 struct pgh_ctx {
     int device = 0;
@@ -73,6 +161,8 @@ struct pgh_ctx {
     bool pin_used[2] = {false, false};
     int pin_next = 0;
     int copy_threads = 8;
+    std::unique_ptr<CopyPool> pool_copy;
+    bool register_ingest = false;  // PGH_REGISTER_INGEST=1: page-lock State messages instead of staging
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
     std::vector<float> weights;
@@ -215,19 +305,6 @@ int timed_launch(pgh_ctx* c, hipStream_t s, uint64_t bytes, F&& launch) {
     return PGH_OK;
 }
 
-void par_memcpy(uint8_t* dst, const uint8_t* src, size_t n, int threads) {
-    if (n < (8u << 20) || threads <= 1) { std::memcpy(dst, src, n); return; }
-    std::vector<std::thread> th;
-    const size_t part = ((n + threads - 1) / threads + 4095) & ~(size_t)4095;
-    for (int t = 0; t < threads; ++t) {
-        const size_t off = (size_t)t * part;
-        if (off >= n) break;
-        const size_t m = std::min(part, n - off);
-        th.emplace_back([=] { std::memcpy(dst + off, src + off, m); });
-    }
-    for (auto& x : th) x.join();
-}
-
 bool is_pinned(const void* p) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) { (void)hipGetLastError(); return false; }
@@ -253,13 +330,15 @@ int stage_pieces_h2d(pgh_ctx* c, uint8_t* dst, const std::vector<Piece>& pieces)
         c->pin_next ^= 1;
         if (c->pin_used[slot]) CK(c, hipEventSynchronize(c->pin_ev[slot]));
         size_t fill = 0;
+        std::vector<CopyPool::Seg> segs;
         while (fill < c->pin_slot && pi < pieces.size()) {
             const size_t m = std::min(pieces[pi].n - poff, c->pin_slot - fill);
-            par_memcpy(c->h_pin[slot] + fill, pieces[pi].src + poff, m, c->copy_threads);
+            segs.push_back({c->h_pin[slot] + fill, pieces[pi].src + poff, m});
             fill += m;
             poff += m;
             if (poff == pieces[pi].n) { ++pi; poff = 0; }
         }
+        c->pool_copy->run(segs);
         CK(c, hipMemcpyAsync(dst + done, c->h_pin[slot], fill, hipMemcpyHostToDevice, c->copy));
         CK(c, hipEventRecord(c->pin_ev[slot], c->copy));
         c->pin_used[slot] = true;
@@ -289,14 +368,16 @@ struct OutPiece {
 };
 
 // Copy bytes [off, off + len) of the concatenation of `pieces` from `src`.
-void scatter_out(const uint8_t* src, size_t off, size_t len, const std::vector<OutPiece>& pieces, int threads) {
+void scatter_out(const uint8_t* src, size_t off, size_t len, const std::vector<OutPiece>& pieces, CopyPool& pool) {
+    std::vector<CopyPool::Seg> segs;
     size_t base = 0;
     for (auto& p : pieces) {
         const size_t a = std::max(off, base), b = std::min(off + len, base + p.n);
-        if (a < b) par_memcpy(p.dst + (a - base), src + (a - off), b - a, threads);
+        if (a < b) segs.push_back({p.dst + (a - base), src + (a - off), b - a});
         base += p.n;
         if (base >= off + len) break;
     }
+    pool.run(segs);
 }
 
 // HBM bytes at `src` (after the work already on stream `s`) -> host pieces, through the pinned
@@ -321,7 +402,7 @@ int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>
         }
         if (prev_slot >= 0) {
             CK(c, hipEventSynchronize(c->pin_ev[prev_slot]));
-            scatter_out(c->h_pin[prev_slot], prev_off, prev_len, pieces, c->copy_threads);
+            scatter_out(c->h_pin[prev_slot], prev_off, prev_len, pieces, *c->pool_copy);
         }
         prev_slot = cur_slot;
         prev_off = off;
@@ -617,6 +698,8 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     const unsigned hw = std::thread::hardware_concurrency();
     c->copy_threads = (int)std::max(1u, std::min(16u, hw ? hw : 1u));
     if (const char* e = std::getenv("PGH_COPY_THREADS")) c->copy_threads = std::max(1, std::atoi(e));
+    c->pool_copy.reset(new CopyPool(c->copy_threads));
+    if (const char* e = std::getenv("PGH_REGISTER_INGEST")) c->register_ingest = std::atoi(e) != 0;
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming) == hipSuccess &&
@@ -771,6 +854,25 @@ int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
     DeviceGuard g(c->device);
     int slot = 0;
     RC(claim_slot(c, client, &slot));
+    if (c->register_ingest && n >= (8u << 20) &&
+        hipHostRegister((void*)pb, n, hipHostRegisterDefault) == hipSuccess) {
+        // page-lock the message for the duration of the call and DMA the spans directly
+        const double t0 = now_ms();
+        size_t off = 0;
+        hipError_t e = hipSuccess;
+        for (auto& p : pieces) {
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(slot_row(c, slot, 0) + off, p.src, p.n, hipMemcpyHostToDevice, c->copy);
+            off += p.n;
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(c->copy);
+        (void)hipHostUnregister((void*)pb);
+        if (e != hipSuccess) return fail(c, PGH_E_HIP, "registered ingest failed: %s", hipGetErrorString(e));
+        c->st.h2d_ms_total += now_ms() - t0;
+        c->st.h2d_bytes_total += off;
+        return mark_ingested(c, client, slot);
+    }
+    (void)hipGetLastError();
     RC(stage_pieces_h2d(c, slot_row(c, slot, 0), pieces));
     return mark_ingested(c, client, slot);
 }
@@ -965,7 +1067,7 @@ int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out
     std::vector<std::pair<size_t, size_t>> spans;
     RC(state_shard_spans(c, tmpl, n, &spans, "checkpoint template"));
     DeviceGuard g(c->device);
-    if (out != tmpl) par_memcpy(out, tmpl, n, c->copy_threads);
+    if (out != tmpl) c->pool_copy->run({CopyPool::Seg{out, tmpl, n}});
     std::vector<OutPiece> pieces;
     for (auto& sp : spans) pieces.push_back(OutPiece{out + sp.first, sp.second});
     RC(order_after_ingest(c, c->stream));
