@@ -162,7 +162,8 @@ struct pgh_ctx {
     int pin_next = 0;
     int copy_threads = 8;
     std::unique_ptr<CopyPool> pool_copy;
-    bool register_ingest = false;  // PGH_REGISTER_INGEST=1: page-lock State messages instead of staging
+    bool register_ingest = false;
+    int ld_mod = 1;  // PGH_REGISTER_INGEST=1: page-lock State messages instead of staging
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
     std::vector<float> weights;
@@ -700,6 +701,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_COPY_THREADS")) c->copy_threads = std::max(1, std::atoi(e));
     c->pool_copy.reset(new CopyPool(c->copy_threads));
     if (const char* e = std::getenv("PGH_REGISTER_INGEST")) c->register_ingest = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PGH_LD_MOD")) c->ld_mod = std::max(1, std::atoi(e));
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming) == hipSuccess &&
@@ -762,6 +764,9 @@ int pgh_set_shard(pgh_ctx* c, int64_t lo, int64_t hi) {
     c->hi = hi;
     c->pg = hi - lo;
     c->ld = (c->pg + 63) & ~(int64_t)63;  // 256-B (fp32) / 512-B (int64) row pitch
+    // Row pitch skew: (ld / 64) % ld_mod == 1 (PGH_LD_MOD, experiment knob; 1 = no skew)
+    if (c->ld_mod > 1)
+        while ((c->ld / 64) % c->ld_mod != 1) c->ld += 64;
     c->st.p_shard = c->pg;
     c->st.ld = c->ld;
     return PGH_OK;
