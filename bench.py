@@ -241,7 +241,7 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
            "parallelism": f"param-shard{ctx.world}" + (
                f" + RCCL all-gather ({args.gather_chunks} ranges overlapped with the fold)" if ctx.world > 1 and dtype == 0
                else " + RCCL all-gather" if ctx.world > 1 else ""),
-           "kernel_variant": args.variant if args.variant is not None else 6}
+           "kernel_variant": eng.effective_variant()}
     rec = record(ctx, args, args.workload, value, el, dt, cfg,
                  roofline_of(st, args.workload, cfg["kernel_variant"], kernel))
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline and dtype == 0 and mode == 0:
@@ -282,7 +282,7 @@ def run_c4(ctx, args, eng, N, pg, P):
                        f"{R}-slot HBM ring, {chunk}-client chunks generated on-device",
            "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R,
            "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
-           "kernel_variant": args.variant if args.variant is not None else 6}
+           "kernel_variant": eng.effective_variant()}
     extra = {"fold_kernel_client_diff_GBps_aggregated": round(kern_gbs, 1),
              "note": "value includes on-device generation of every chunk (writes 4 B/param/client) "
                      "competing for HBM with the fold; the fold kernels alone are fold_kernel_*"}
@@ -328,7 +328,7 @@ def run_c5(ctx, args, eng, N, pg, P):
                        f"config 5 shard), pinned host -> HBM over PCIe, {R}-slot ring, fold batch 2",
            "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R,
            "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
-           "kernel_variant": args.variant if args.variant is not None else 6}
+           "kernel_variant": eng.effective_variant()}
     extra = {"bound_by": "PCIe host->device (Gen5 x16, 63 GB/s spec per GPU)",
              "ingest_GBps_per_gpu": round(ingest_gbs, 2) if ingest_gbs else None,
              "fold_kernel_client_diff_GBps_per_gpu": round(kern_gbs, 1)}
@@ -365,9 +365,9 @@ def run_mnist_state(ctx, args, eng):
     value = 4 * 3 * P * args.steps / el / 1e9
     cfg = {"workload": "mnist-state: MNIST 784-392-10 (P=311,650), 3 clients, State bytes -> checkpoint bytes "
                        "(scan + H2D + fused mean/apply + D2H + patch)", "clients": 3, "params_per_gpu": P,
-           "params_total": P, "parallelism": "single GPU", "kernel_variant": 6}
+           "params_total": P, "parallelism": "single GPU", "kernel_variant": eng.effective_variant()}
     rec = record(ctx, args, "mnist-state", value, el, "f32", cfg,
-                 roofline_of(st, "mnist-state", 6, "k_fedavg"),
+                 roofline_of(st, "mnist-state", eng.effective_variant(), "k_fedavg"),
                  {"new_checkpoint_bytes": len(new),
                   "note": "latency-bound: host protobuf scan, 3 H2D copies and a 0.3M-param kernel"})
     if not args.no_cpu_baseline:
@@ -412,13 +412,13 @@ def run_resnet18_state(ctx, args, eng, N):
     value = 4 * N * P * args.steps / el / 1e9
     cfg = {"workload": f"resnet18-state: ResNet-18 (62 tensors, P={P}) x {N} clients, State protobuf bytes in host "
                        "memory -> new checkpoint bytes (scan + host->HBM + fused mean/apply + HBM->host + patch)",
-           "clients": N, "params_per_gpu": P, "params_total": P, "parallelism": "single GPU", "kernel_variant": 6}
+           "clients": N, "params_per_gpu": P, "params_total": P, "parallelism": "single GPU", "kernel_variant": eng.effective_variant()}
     extra = {"h2d_GBps": round(st["h2d_bytes_total"] / (st["h2d_ms_total"] / 1e3) / 1e9, 2) if st["h2d_ms_total"] else None,
              "h2d_ms_per_close": round(st["h2d_ms_total"] / args.steps, 2),
              "new_checkpoint_bytes": len(new),
              "note": "PCIe-inclusive cycle close from host bytes (never `value` for the resident configs)"}
     return record(ctx, args, "resnet18-state", value, el, "f32", cfg,
-                  roofline_of(st, "resnet18-state", 6, "k_fedavg"), extra)
+                  roofline_of(st, "resnet18-state", eng.effective_variant(), "k_fedavg"), extra)
 
 
 def main():

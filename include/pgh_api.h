@@ -155,9 +155,12 @@ int pgh_stream_finish_secagg(pgh_ctx* ctx, int base, int prec, int64_t* sum_out,
 int pgh_stream_finish_secagg_device(pgh_ctx* ctx, int base, int prec, int64_t* d_sum, float* d_dec, void* stream);
 
 /* ---- tuning and observability -------------------------------------------------------------- */
-/* Kernel variant for A/B measurement (table in csrc/pgh_kernels.hip); -1 = the default. */
-#define PGH_DEFAULT_VARIANT 6
+/* Kernel variant for A/B measurement (table in csrc/pgh_kernels.hip); -1 = the default, which
+ * picks by shard size (auto_variant in csrc/pgh_kernels.hip). */
+#define PGH_DEFAULT_VARIANT (-1)
 int pgh_set_variant(pgh_ctx* ctx, int variant);
+/* The variant the next fp32 fold of this context's shard will run (>= 0), or an error status. */
+int pgh_effective_variant(pgh_ctx* ctx);
 int pgh_stats(pgh_ctx* ctx, pgh_stats_t* out);     /* synchronises pending timing events */
 int pgh_reset_stats(pgh_ctx* ctx);
 /* Device pointer of the slab and its row stride, for callers that drive the kernels. */

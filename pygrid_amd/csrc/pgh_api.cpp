@@ -1199,9 +1199,15 @@ int pgh_stream_finish_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, f
 
 int pgh_set_variant(pgh_ctx* c, int variant) {
     if (!c) return PGH_E_ARG;
-    if (variant < -1 || variant > 10) return fail(c, PGH_E_ARG, "variant %d outside [-1,10]", variant);
-    c->variant = variant < 0 ? PGH_DEFAULT_VARIANT : variant;
+    if (variant < -1 || variant > 14) return fail(c, PGH_E_ARG, "variant %d outside [-1,14]", variant);
+    c->variant = variant;
     return PGH_OK;
+}
+
+int pgh_effective_variant(pgh_ctx* c) {
+    if (!c) return PGH_E_ARG;
+    if (!c->layout) return fail(c, PGH_E_STATE, "pgh_set_layout has not been called");
+    return c->variant >= 0 ? c->variant : pgh::auto_variant(c->pg);
 }
 
 int pgh_stats(pgh_ctx* c, pgh_stats_t* out) {

@@ -24,7 +24,7 @@ struct FedavgArgs {
     float divisor;          // float(N) or sum of weights, FL_FINAL of MEAN / WEIGHTED
     int flags;
     int mode;
-    int variant;            // kernel variant (0 = default), for A/B tuning
+    int variant;            // kernel variant (table in pgh_kernels.hip); < 0 = auto by shard size
 };
 hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s);
 
@@ -41,6 +41,8 @@ struct SecaggArgs {
     int variant;
 };
 hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s);
+// The variant the auto choice (variant < 0) picks for a shard of p params.
+int auto_variant(int64_t p);
 
 // Deterministic synthetic inputs (restated bit for bit by oracle/oracle.py).
 hipError_t launch_synth_f32(float* out, int n_rows, int64_t ld, int64_t p, uint64_t seed,

@@ -74,8 +74,27 @@ __device__ __forceinline__ void st4_tail(float* base, int64_t q, int64_t p, f32x
         if (i + e < p) base[i + e] = v[e];
 }
 
-template <int MODE>
-__device__ __forceinline__ f32x4 fold(f32x4 acc, f32x4 v, int64_t k, const float* w, int r) {
+// Lane element: VEC = 4 (one 16-byte column of 4 params, the default) or VEC = 1 (one param per
+// lane: 4x the lanes, for shards too small to fill 256 CUs with 16-byte columns).
+template <int VEC> struct Lane;
+template <> struct Lane<4> {
+    using T = f32x4;
+    template <bool NT> static __device__ __forceinline__ T load(const float* p) { return ld4<NT>(p); }
+    static __device__ __forceinline__ T load_tail(const float* b, int64_t q, int64_t p) { return ld4_tail(b, q, p); }
+    static __device__ __forceinline__ void store_tail(float* b, int64_t q, int64_t p, T v) { st4_tail(b, q, p, v); }
+};
+template <> struct Lane<1> {
+    using T = float;
+    template <bool NT> static __device__ __forceinline__ T load(const float* p) {
+        if constexpr (NT) return __builtin_nontemporal_load(p);
+        else return *p;
+    }
+    static __device__ __forceinline__ T load_tail(const float* b, int64_t q, int64_t p) { return q < p ? b[q] : 0.f; }
+    static __device__ __forceinline__ void store_tail(float* b, int64_t q, int64_t p, T v) { if (q < p) b[q] = v; }
+};
+
+template <int MODE, class T>
+__device__ __forceinline__ T fold(T acc, T v, int64_t k, const float* w, int r) {
     if constexpr (MODE == MODE_MEAN) {
         return acc + v;                                   // th.add, cycle_manager.py:286
     } else if constexpr (MODE == MODE_WEIGHTED) {
@@ -86,31 +105,34 @@ __device__ __forceinline__ f32x4 fold(f32x4 acc, f32x4 v, int64_t k, const float
     }
 }
 
-// W 16-byte columns per lane (q0, q0 + TB, ...: each load instruction of a wave still reads one
-// contiguous KiB), all rows of the chunk, in order.  4 consecutive params per column.
-template <int MODE, int U, int W, bool NT>
+// W columns per lane (q0, q0 + qstep, ...: each load instruction of a wave still reads one
+// contiguous span), all rows of the chunk, in order.  VEC consecutive params per column.
+template <int MODE, int U, int W, bool NT, int VEC>
 __device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, int64_t qstep) {
+    using L = Lane<VEC>;
+    using T = typename L::T;
     const int n = a.n_rows;
-    f32x4 acc[W];
+    T acc[W];
     int r;
     if (a.flags & FL_FIRST) {
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            acc[w] = ld4<NT>(a.diffs + 4 * (q0 + w * qstep));  // fold starts at d0, not 0
+            acc[w] = L::template load<NT>(a.diffs + VEC * (q0 + w * qstep));  // fold starts at d0, not 0
             if constexpr (MODE == MODE_WEIGHTED) acc[w] = acc[w] * a.weights[0];
         }
         r = 1;
     } else {
 #pragma unroll
-        for (int w = 0; w < W; ++w) acc[w] = ld4_tail(a.acc, q0 + w * qstep, a.p);
+        for (int w = 0; w < W; ++w) acc[w] = L::load_tail(a.acc, q0 + w * qstep, a.p);
         r = 0;
     }
     for (; r + U <= n; r += U) {
-        f32x4 v[U][W];
+        T v[U][W];
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int w = 0; w < W; ++w) v[u][w] = ld4<NT>(a.diffs + (size_t)(r + u) * a.ld + 4 * (q0 + w * qstep));
+            for (int w = 0; w < W; ++w)
+                v[u][w] = L::template load<NT>(a.diffs + (size_t)(r + u) * a.ld + VEC * (q0 + w * qstep));
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -119,30 +141,30 @@ __device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, 
     for (; r < n; ++r)
 #pragma unroll
         for (int w = 0; w < W; ++w)
-            acc[w] = fold<MODE>(acc[w], ld4<NT>(a.diffs + (size_t)r * a.ld + 4 * (q0 + w * qstep)), a.client0 + r,
-                                a.weights, r);
+            acc[w] = fold<MODE>(acc[w], L::template load<NT>(a.diffs + (size_t)r * a.ld + VEC * (q0 + w * qstep)),
+                                a.client0 + r, a.weights, r);
 #pragma unroll
     for (int w = 0; w < W; ++w) {
         const int64_t q = q0 + w * qstep;
         if (a.flags & FL_FINAL) {
-            const f32x4 avg = (MODE == MODE_ITERATIVE) ? acc[w] : acc[w] / a.divisor;  // th.div, :288
-            st4_tail(a.out, q, a.p, ld4_tail(a.ckpt, q, a.p) - avg);                   // :293-296
+            const T avg = (MODE == MODE_ITERATIVE) ? acc[w] : acc[w] / a.divisor;  // th.div, :288
+            L::store_tail(a.out, q, a.p, L::load_tail(a.ckpt, q, a.p) - avg);     // :293-296
         } else {
-            st4_tail(a.acc, q, a.p, acc[w]);
+            L::store_tail(a.acc, q, a.p, acc[w]);
         }
     }
 }
 
 // Grid-stride over tiles of TB x W columns; a partial last tile goes one column per lane.
-template <int MODE, int U, int W, bool NT, int TB>
+template <int MODE, int U, int W, bool NT, int TB, int VEC>
 __global__ __launch_bounds__(TB) void k_fedavg(FedavgArgs a, int64_t ncol) {
     const int64_t tile = (int64_t)TB * W;
     for (int64_t t0 = (int64_t)blockIdx.x * tile; t0 < ncol; t0 += (int64_t)gridDim.x * tile) {
         const int64_t q0 = t0 + threadIdx.x;
         if (t0 + tile <= ncol) {
-            fedavg_columns<MODE, U, W, NT>(a, q0, TB);
+            fedavg_columns<MODE, U, W, NT, VEC>(a, q0, TB);
         } else {
-            for (int64_t q = q0; q < ncol && q < t0 + tile; q += TB) fedavg_columns<MODE, U, 1, NT>(a, q, TB);
+            for (int64_t q = q0; q < ncol && q < t0 + tile; q += TB) fedavg_columns<MODE, U, 1, NT, VEC>(a, q, TB);
         }
     }
 }
@@ -236,22 +258,27 @@ int cu_count() {
     return cached[dev];
 }
 
-// Variants (A/B in one process: tools/ab_variants.py; profiles/r01/README.md).
-//   id  loads  U (rows in flight)  W (columns per lane)  block  grid
-//   0   nt     8                   1                     256    one lane per column
-//   1   nt     8                   1                     256    persistent, 4 blocks/CU
-//   2   plain  8                   1                     256    one lane per column
-//   3   plain  8                   1                     256    persistent
-//   4   plain  16                  1                     256    one lane per column
-//   5   plain  16                  1                     256    persistent
-//   6   nt     16                  1                     256    one lane per column   <- default
-//   7   nt     4                   2                     256    one lane per W columns
-//   8   nt     8                   2                     256    one lane per W columns
-//   9   nt     8                   1                     512    one lane per column
-//   10  nt     4                   1                     256    one lane per column
-// nt loads won 2-3 % on the once-read diff stream (r01: 6393 vs 6270 GB/s, ResNet-18 x 1000);
-// r01c: every nt variant within 1 %, 6 best or tied on K1 (6448), K2 (6415) and K3 (6238 GB/s).
-constexpr int N_VARIANTS = 11;
+// Variants (A/B in one process: tools/ab_variants.py; profiles/r01*/README.md).
+//   id  loads  U (rows in flight)  W (cols/lane)  block  VEC (params/col)  grid
+//   0   nt     8                   1              256    4                 one lane per column
+//   1   nt     8                   1              256    4                 persistent, 4 blocks/CU
+//   2   plain  8                   1              256    4                 one lane per column
+//   3   plain  8                   1              256    4                 persistent
+//   4   plain  16                  1              256    4                 one lane per column
+//   5   plain  16                  1              256    4                 persistent
+//   6   nt     16                  1              256    4                 one lane per column  <- big shards
+//   7   nt     4                   2              256    4                 one lane per W columns
+//   8   nt     8                   2              256    4                 one lane per W columns
+//   9   nt     8                   1              512    4                 one lane per column
+//   10  nt     4                   1              256    4                 one lane per column
+//   11  nt     16                  1              64     4                 one lane per column
+//   12  nt     16                  1              64     1                 one lane per param
+//   13  nt     8                   1              256    1                 one lane per param
+//   14  nt     32                  1              64     1                 one lane per param
+// nt loads won 2-5 % on the once-read diff stream; among nt variants at ResNet-18 size the spread
+// is < 1 % (r01c).  Small shards are bound by lanes / CU balance, not by the loads: the auto
+// choice (PGH_VARIANT_AUTO) picks by shard size (auto_variant below, r01g measurements).
+constexpr int N_VARIANTS = 15;
 
 inline unsigned grid_for(int64_t ncol, int64_t tile, bool persistent) {
     const int64_t full = (ncol + tile - 1) / tile;
@@ -260,31 +287,41 @@ inline unsigned grid_for(int64_t ncol, int64_t tile, bool persistent) {
     return (unsigned)(full < pers ? (full > 0 ? full : 1) : pers);
 }
 
-template <int MODE, int U, int W, bool NT, int TB>
-hipError_t go_fedavg(const FedavgArgs& a, int64_t ncol, bool persistent, hipStream_t s) {
-    k_fedavg<MODE, U, W, NT, TB><<<grid_for(ncol, (int64_t)TB * W, persistent), TB, 0, s>>>(a, ncol);
+template <int MODE, int U, int W, bool NT, int TB, int VEC>
+hipError_t go_fedavg(const FedavgArgs& a, bool persistent, hipStream_t s) {
+    const int64_t ncol = (a.p + VEC - 1) / VEC;
+    k_fedavg<MODE, U, W, NT, TB, VEC><<<grid_for(ncol, (int64_t)TB * W, persistent), TB, 0, s>>>(a, ncol);
     return hipGetLastError();
 }
 
 template <int MODE>
-hipError_t dispatch_fedavg(const FedavgArgs& a, int64_t ncol, hipStream_t s) {
-    switch (a.variant) {
-    case 0: return go_fedavg<MODE, 8, 1, true, 256>(a, ncol, false, s);
-    case 1: return go_fedavg<MODE, 8, 1, true, 256>(a, ncol, true, s);
-    case 2: return go_fedavg<MODE, 8, 1, false, 256>(a, ncol, false, s);
-    case 3: return go_fedavg<MODE, 8, 1, false, 256>(a, ncol, true, s);
-    case 4: return go_fedavg<MODE, 16, 1, false, 256>(a, ncol, false, s);
-    case 5: return go_fedavg<MODE, 16, 1, false, 256>(a, ncol, true, s);
-    case 6: return go_fedavg<MODE, 16, 1, true, 256>(a, ncol, false, s);
-    case 7: return go_fedavg<MODE, 4, 2, true, 256>(a, ncol, false, s);
-    case 8: return go_fedavg<MODE, 8, 2, true, 256>(a, ncol, false, s);
-    case 9: return go_fedavg<MODE, 8, 1, true, 512>(a, ncol, false, s);
-    case 10: return go_fedavg<MODE, 4, 1, true, 256>(a, ncol, false, s);
+hipError_t dispatch_fedavg(const FedavgArgs& a, int variant, hipStream_t s) {
+    switch (variant) {
+    case 0: return go_fedavg<MODE, 8, 1, true, 256, 4>(a, false, s);
+    case 1: return go_fedavg<MODE, 8, 1, true, 256, 4>(a, true, s);
+    case 2: return go_fedavg<MODE, 8, 1, false, 256, 4>(a, false, s);
+    case 3: return go_fedavg<MODE, 8, 1, false, 256, 4>(a, true, s);
+    case 4: return go_fedavg<MODE, 16, 1, false, 256, 4>(a, false, s);
+    case 5: return go_fedavg<MODE, 16, 1, false, 256, 4>(a, true, s);
+    case 6: return go_fedavg<MODE, 16, 1, true, 256, 4>(a, false, s);
+    case 7: return go_fedavg<MODE, 4, 2, true, 256, 4>(a, false, s);
+    case 8: return go_fedavg<MODE, 8, 2, true, 256, 4>(a, false, s);
+    case 9: return go_fedavg<MODE, 8, 1, true, 512, 4>(a, false, s);
+    case 10: return go_fedavg<MODE, 4, 1, true, 256, 4>(a, false, s);
+    case 11: return go_fedavg<MODE, 16, 1, true, 64, 4>(a, false, s);
+    case 12: return go_fedavg<MODE, 16, 1, true, 64, 1>(a, false, s);
+    case 13: return go_fedavg<MODE, 8, 1, true, 256, 1>(a, false, s);
+    case 14: return go_fedavg<MODE, 32, 1, true, 64, 1>(a, false, s);
     default: return hipErrorInvalidValue;
     }
 }
 
 }  // namespace
+
+int auto_variant(int64_t p) {
+    (void)p;
+    return 6;
+}
 
 hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
     if (a.p <= 0 || a.n_rows < 0 || a.ld < a.p || (a.ld & 3)) return hipErrorInvalidValue;
@@ -296,11 +333,11 @@ hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
                                  (reinterpret_cast<uintptr_t>(a.out) & 15)))
         return hipErrorInvalidValue;
     if (a.mode == MODE_WEIGHTED && a.n_rows > 0 && !a.weights) return hipErrorInvalidValue;
-    const int64_t ncol = (a.p + 3) / 4;
+    const int v = a.variant < 0 ? auto_variant(a.p) : a.variant;
     switch (a.mode) {
-    case MODE_MEAN: return dispatch_fedavg<MODE_MEAN>(a, ncol, s);
-    case MODE_ITERATIVE: return dispatch_fedavg<MODE_ITERATIVE>(a, ncol, s);
-    case MODE_WEIGHTED: return dispatch_fedavg<MODE_WEIGHTED>(a, ncol, s);
+    case MODE_MEAN: return dispatch_fedavg<MODE_MEAN>(a, v, s);
+    case MODE_ITERATIVE: return dispatch_fedavg<MODE_ITERATIVE>(a, v, s);
+    case MODE_WEIGHTED: return dispatch_fedavg<MODE_WEIGHTED>(a, v, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -311,13 +348,14 @@ hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s) {
     if (!(a.flags & FL_FINAL) && !a.acc) return hipErrorInvalidValue;
     if (!(a.flags & FL_FIRST) && !a.acc) return hipErrorInvalidValue;
     const int64_t ncol = (a.p + 1) / 2;
-    if (a.variant < 0 || a.variant >= N_VARIANTS) return hipErrorInvalidValue;
-    const unsigned g = grid_for(ncol, BLOCK, a.variant == 1 || a.variant == 3 || a.variant == 5);
-    switch (a.variant) {  // same load policy / depth as the fedavg variant of that id
+    const int v = a.variant < 0 ? auto_variant(a.p) : a.variant;
+    if (v >= N_VARIANTS) return hipErrorInvalidValue;
+    const unsigned g = grid_for(ncol, BLOCK, v == 1 || v == 3 || v == 5);
+    switch (v) {  // same load policy / depth as the fedavg variant of that id
     case 2: case 3: k_secagg<8, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
     case 4: case 5: k_secagg<16, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
-    case 6: k_secagg<16, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
     case 7: case 10: k_secagg<4, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 6: case 11: case 12: case 14: k_secagg<16, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
     default: k_secagg<8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
     }
     return hipGetLastError();

@@ -16,7 +16,7 @@ from .exceptions import AggregationError, EngineUnavailableError, StateParseErro
 
 MEAN, ITERATIVE_MEAN, WEIGHTED_MEAN = 0, 1, 2
 STREAM_SECAGG = 16
-DEFAULT_VARIANT = 6  # PGH_DEFAULT_VARIANT
+DEFAULT_VARIANT = -1  # PGH_DEFAULT_VARIANT: auto by shard size
 F32, I64 = 0, 1
 MODE_NAMES = {MEAN: "mean", ITERATIVE_MEAN: "iterative_mean", WEIGHTED_MEAN: "weighted_mean"}
 
@@ -246,6 +246,11 @@ class Engine:
     def set_variant(self, v: int):
         """Kernel variant (csrc/pgh_kernels.hip table); -1 restores the default."""
         self._check(self._lib.pgh_set_variant(self._h, int(v)), "set_variant")
+
+    def effective_variant(self) -> int:
+        v = self._lib.pgh_effective_variant(self._h)
+        self._check(min(v, 0), "effective_variant")
+        return v
 
     def stats(self) -> dict:
         st = _lib.Stats()

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--params", type=int, default=11_689_512)
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8,9,10")
+    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8,9,10,11,12,13,14")
     a = ap.parse_args()
     import torch
 
