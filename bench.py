@@ -241,7 +241,7 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
            "parallelism": f"param-shard{ctx.world}" + (
                f" + RCCL all-gather ({args.gather_chunks} ranges overlapped with the fold)" if ctx.world > 1 and dtype == 0
                else " + RCCL all-gather" if ctx.world > 1 else ""),
-           "kernel_variant": eng.effective_variant()}
+           "kernel_variant": eng.effective_variant(mode if dtype == 0 else 16)}
     rec = record(ctx, args, args.workload, value, el, dt, cfg,
                  roofline_of(st, args.workload, cfg["kernel_variant"], kernel))
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline and dtype == 0 and mode == 0:
@@ -328,7 +328,7 @@ def run_c5(ctx, args, eng, N, pg, P):
                        f"config 5 shard), pinned host -> HBM over PCIe, {R}-slot ring, fold batch 2",
            "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R,
            "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
-           "kernel_variant": eng.effective_variant()}
+           "kernel_variant": eng.effective_variant(1)}
     extra = {"bound_by": "PCIe host->device (Gen5 x16, 63 GB/s spec per GPU)",
              "ingest_GBps_per_gpu": round(ingest_gbs, 2) if ingest_gbs else None,
              "fold_kernel_client_diff_GBps_per_gpu": round(kern_gbs, 1)}

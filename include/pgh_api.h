@@ -159,8 +159,9 @@ int pgh_stream_finish_secagg_device(pgh_ctx* ctx, int base, int prec, int64_t* d
  * picks by shard size (auto_variant in csrc/pgh_kernels.hip). */
 #define PGH_DEFAULT_VARIANT (-1)
 int pgh_set_variant(pgh_ctx* ctx, int variant);
-/* The variant the next fp32 fold of this context's shard will run (>= 0), or an error status. */
-int pgh_effective_variant(pgh_ctx* ctx);
+/* The variant the next fold of this context's shard runs for `mode` (a pgh_mode, or
+ * PGH_STREAM_SECAGG for the share sum): >= 0, or an error status. */
+int pgh_effective_variant(pgh_ctx* ctx, int mode);
 int pgh_stats(pgh_ctx* ctx, pgh_stats_t* out);     /* synchronises pending timing events */
 int pgh_reset_stats(pgh_ctx* ctx);
 /* Device pointer of the slab and its row stride, for callers that drive the kernels. */

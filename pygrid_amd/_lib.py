@@ -76,7 +76,7 @@ SIGNATURES = {
     "pgh_stream_finish_secagg_device": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pgh_sync": (_i, [_vp]),
     "pgh_set_variant": (_i, [_vp, _i]),
-    "pgh_effective_variant": (_i, [_vp]),
+    "pgh_effective_variant": (_i, [_vp, _i]),
     "pgh_stats": (_i, [_vp, C.POINTER(Stats)]),
     "pgh_reset_stats": (_i, [_vp]),
     "pgh_slab": (_i, [_vp, C.POINTER(_vp), _P64]),

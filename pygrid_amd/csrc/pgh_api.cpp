@@ -1204,10 +1204,13 @@ int pgh_set_variant(pgh_ctx* c, int variant) {
     return PGH_OK;
 }
 
-int pgh_effective_variant(pgh_ctx* c) {
+int pgh_effective_variant(pgh_ctx* c, int mode) {
     if (!c) return PGH_E_ARG;
     if (!c->layout) return fail(c, PGH_E_STATE, "pgh_set_layout has not been called");
-    return c->variant >= 0 ? c->variant : pgh::auto_variant(c->pg);
+    if (c->variant >= 0) return c->variant;
+    if (mode == PGH_STREAM_SECAGG) return 11;
+    if (!valid_mode(mode)) return fail(c, PGH_E_ARG, "unknown averaging mode %d", mode);
+    return pgh::auto_variant(c->pg, mode);
 }
 
 int pgh_stats(pgh_ctx* c, pgh_stats_t* out) {

@@ -41,8 +41,8 @@ struct SecaggArgs {
     int variant;
 };
 hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s);
-// The variant the auto choice (variant < 0) picks for a shard of p params.
-int auto_variant(int64_t p);
+// The fp32 fold variant the auto choice (variant < 0) picks for a shard of p params.
+int auto_variant(int64_t p, int mode);
 
 // Deterministic synthetic inputs (restated bit for bit by oracle/oracle.py).
 hipError_t launch_synth_f32(float* out, int n_rows, int64_t ld, int64_t p, uint64_t seed,

@@ -169,10 +169,10 @@ __global__ __launch_bounds__(TB) void k_fedavg(FedavgArgs a, int64_t ncol) {
     }
 }
 
-template <int U, bool NT>
-__global__ __launch_bounds__(BLOCK) void k_secagg(SecaggArgs a, int64_t ncol) {
-    const int64_t stride = (int64_t)gridDim.x * BLOCK;
-    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < ncol; q += stride) {
+template <int U, bool NT, int TB = BLOCK>
+__global__ __launch_bounds__(TB) void k_secagg(SecaggArgs a, int64_t ncol) {
+    const int64_t stride = (int64_t)gridDim.x * TB;
+    for (int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x; q < ncol; q += stride) {
         const int64_t* col = a.shares + 2 * q;
         const int64_t i = 2 * q;
         const bool full = i + 2 <= a.p;
@@ -318,9 +318,20 @@ hipError_t dispatch_fedavg(const FedavgArgs& a, int variant, hipStream_t s) {
 
 }  // namespace
 
-int auto_variant(int64_t p) {
-    (void)p;
-    return 6;
+// Measured on MI355X (r01g, tools/small_p2.sh / tools/big_p.sh; GB/s of algorithmic bytes):
+//   P = 50K x 60K clients: v14 6088, v12 4013, v11 3984, v6 2644
+//   P = 100K x 30K:        v12 6754, v11 6609, v14 6597, v6 4817
+//   P = 311,650 x 10K:     v11 6963, v14 6616, v12 6564, v6 5604
+//   P = 1M x 3K:           v11 6789, v12 6754, v14 6735, v6 6758
+//   P = 11.69M x 1K:       mean v14 6685 / v12 6679 / v11 6645 / v6 6559;
+//                          iterative v11 6603 / v14 6561 / v6 6516
+// Small shards need more, smaller workgroups (CU balance) and, below ~200K params, one param per
+// lane (lanes); large shards are within 1-2 % of each other, 64-thread blocks ahead.
+int auto_variant(int64_t p, int mode) {
+    if (p < 80000) return 14;
+    if (p < 200000) return 12;
+    if (p < 2000000) return 11;
+    return mode == MODE_ITERATIVE ? 11 : 14;
 }
 
 hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
@@ -333,7 +344,7 @@ hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
                                  (reinterpret_cast<uintptr_t>(a.out) & 15)))
         return hipErrorInvalidValue;
     if (a.mode == MODE_WEIGHTED && a.n_rows > 0 && !a.weights) return hipErrorInvalidValue;
-    const int v = a.variant < 0 ? auto_variant(a.p) : a.variant;
+    const int v = a.variant < 0 ? auto_variant(a.p, a.mode) : a.variant;
     switch (a.mode) {
     case MODE_MEAN: return dispatch_fedavg<MODE_MEAN>(a, v, s);
     case MODE_ITERATIVE: return dispatch_fedavg<MODE_ITERATIVE>(a, v, s);
@@ -348,14 +359,15 @@ hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s) {
     if (!(a.flags & FL_FINAL) && !a.acc) return hipErrorInvalidValue;
     if (!(a.flags & FL_FIRST) && !a.acc) return hipErrorInvalidValue;
     const int64_t ncol = (a.p + 1) / 2;
-    const int v = a.variant < 0 ? auto_variant(a.p) : a.variant;
+    const int v = a.variant < 0 ? 11 : a.variant;  // secagg: 64-thread blocks (r01g)
     if (v >= N_VARIANTS) return hipErrorInvalidValue;
     const unsigned g = grid_for(ncol, BLOCK, v == 1 || v == 3 || v == 5);
     switch (v) {  // same load policy / depth as the fedavg variant of that id
     case 2: case 3: k_secagg<8, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
     case 4: case 5: k_secagg<16, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
     case 7: case 10: k_secagg<4, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
-    case 6: case 11: case 12: case 14: k_secagg<16, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 6: k_secagg<16, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    case 11: case 12: case 13: case 14: k_secagg<16, true, 64><<<grid_for(ncol, 64, false), 64, 0, s>>>(a, ncol); break;
     default: k_secagg<8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
     }
     return hipGetLastError();

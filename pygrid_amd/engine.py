@@ -247,8 +247,10 @@ class Engine:
         """Kernel variant (csrc/pgh_kernels.hip table); -1 restores the default."""
         self._check(self._lib.pgh_set_variant(self._h, int(v)), "set_variant")
 
-    def effective_variant(self) -> int:
-        v = self._lib.pgh_effective_variant(self._h)
+    def effective_variant(self, mode: int = MEAN) -> int:
+        """Kernel variant the next fold runs for ``mode`` (MEAN / ITERATIVE_MEAN / WEIGHTED_MEAN /
+        STREAM_SECAGG)."""
+        v = self._lib.pgh_effective_variant(self._h, int(mode))
         self._check(min(v, 0), "effective_variant")
         return v
 
