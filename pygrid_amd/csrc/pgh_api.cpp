@@ -591,6 +591,7 @@ int claim_slot(pgh_ctx* c, int64_t client, int* slot_out) {
     if (!c->streaming) {
         if (client >= c->slots)
             return fail(c, PGH_E_ARG, "client %lld outside slab capacity %d", (long long)client, c->slots);
+        RC(order_before_overwrite(c));  // a fold issued earlier (any stream) may still read the slab
         *slot_out = (int)client;
         return PGH_OK;
     }
@@ -814,6 +815,7 @@ int pgh_reset(pgh_ctx* c) {
     if (!c) return PGH_E_ARG;
     DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->fold_pending) (void)hipEventSynchronize(c->fold_done);  // folds issued on caller streams
     std::fill(c->slot_client.begin(), c->slot_client.end(), -1);
     c->weights.clear();
     c->weights_on_device = false;
@@ -1004,6 +1006,7 @@ int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
     DeviceGuard g(c->device);
     const double t0 = now_ms();
     const size_t bytes = sizeof(float) * (size_t)c->pg;
+    RC(order_before_overwrite(c));
     RC(stage_h2d(c, c->d_ckpt, (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
     RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
     if (is_pinned(out)) {
@@ -1026,6 +1029,7 @@ int pgh_ckpt_upload(pgh_ctx* c, const float* ckpt, size_t nbytes) {
         return fail(c, PGH_E_ARG, "checkpoint: got %zu bytes, layout needs %zu (model) or %zu (shard)", nbytes, whole,
                     shard);
     DeviceGuard g(c->device);
+    RC(order_before_overwrite(c));
     const uint8_t* src = (const uint8_t*)ckpt + (nbytes == whole ? 4 * (size_t)c->lo : 0);
     return stage_h2d(c, c->d_ckpt, src, shard, is_pinned(ckpt));
 }
@@ -1038,6 +1042,7 @@ int pgh_ckpt_upload_state(pgh_ctx* c, const uint8_t* pb, size_t n) {
     std::vector<Piece> pieces;
     for (auto& sp : spans) pieces.push_back(Piece{pb + sp.first, sp.second});
     DeviceGuard g(c->device);
+    RC(order_before_overwrite(c));
     return stage_pieces_h2d(c, (uint8_t*)c->d_ckpt, pieces);
 }
 
