@@ -379,3 +379,33 @@ def test_resident_api_flat(engine):
         engine.ingest(k, d[k])
     engine.fedavg_resident(0)
     assert same(engine.ckpt_download(), coracle.fedavg(0, d, c))
+
+
+def test_reingest_waits_for_inflight_fold(engine):
+    """RESIDENT: overwriting a slot right after an async fold on the caller's stream must not
+    change what that fold reads."""
+    import torch
+
+    rng = np.random.default_rng(41)
+    P, N = 4_000_000, 40
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    new0 = (rng.standard_normal(P) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    engine.set_layout([P])
+    engine.reserve(N)
+    for k in range(N):
+        engine.ingest(k, d[k])
+    ck = torch.from_numpy(c).cuda()
+    out1 = torch.empty_like(ck)
+    out2 = torch.empty_like(ck)
+    sp = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    engine.fedavg_device(0, ck.data_ptr(), out1.data_ptr(), sp)
+    engine.ingest(0, new0)
+    engine.fedavg_device(0, ck.data_ptr(), out2.data_ptr(), sp)
+    torch.cuda.synchronize()
+    idx = np.random.default_rng(0).integers(0, P, 3000)
+    assert same(out1.cpu().numpy()[idx], coracle.fedavg(0, d[:, idx], c[idx]))
+    d2 = d[:, idx].copy()
+    d2[0] = new0[idx]
+    assert same(out2.cpu().numpy()[idx], coracle.fedavg(0, d2, c[idx]))
