@@ -33,6 +33,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <string>
 #include <thread>
 #include <vector>
@@ -138,6 +139,11 @@ struct pgh_ctx {
     hipEvent_t fold_done = nullptr;
     hipEvent_t xsync = nullptr;    // caller-stream <-> context-stream ordering
     bool fold_pending = false;
+    // STREAM: one event per fold with the fold front after it, so overwriting a slot waits only
+    // for the fold that consumed the slot's previous client (not for the latest fold).
+    struct FoldMark { hipEvent_t ev; int64_t upto; };
+    std::deque<FoldMark> marks;
+    std::vector<hipEvent_t> mark_pool;
 
     std::vector<int64_t> numel;
     int64_t P = 0, lo = 0, hi = 0, pg = 0, ld = 0;
@@ -241,6 +247,8 @@ void free_slab(pgh_ctx* c) {
     (void)hipFree(c->d_w); c->d_w = nullptr; c->w_cap = 0;
     c->slots = 0;
     c->slot_client.clear();
+    for (auto& m : c->marks) c->mark_pool.push_back(m.ev);
+    c->marks.clear();
     c->streaming = false;
     c->folded = 0;
     c->fold_pending = false;
@@ -448,6 +456,37 @@ int order_before_overwrite(pgh_ctx* c) {
     return PGH_OK;
 }
 
+void clear_marks(pgh_ctx* c) {
+    for (auto& m : c->marks) c->mark_pool.push_back(m.ev);
+    c->marks.clear();
+}
+
+// STREAM: the slots of clients up to `last_client` held clients up to last_client - R before;
+// the copy stream waits for the fold that consumed those.
+int order_stream_overwrite(pgh_ctx* c, int64_t last_client) {
+    const int64_t prev = last_client - c->slots;
+    while (!c->marks.empty() && c->marks.front().upto <= c->folded - c->slots) {
+        c->mark_pool.push_back(c->marks.front().ev);  // no future claim needs it
+        c->marks.pop_front();
+    }
+    if (prev < 0) return PGH_OK;  // first pass over the ring (pgh_stream_begin drained older folds)
+    for (auto& m : c->marks)
+        if (m.upto > prev) {
+            CK(c, hipStreamWaitEvent(c->copy, m.ev, 0));
+            return PGH_OK;
+        }
+    return order_before_overwrite(c);
+}
+
+int record_mark(pgh_ctx* c, hipStream_t s, int64_t upto) {
+    hipEvent_t e = nullptr;
+    if (!c->mark_pool.empty()) { e = c->mark_pool.back(); c->mark_pool.pop_back(); }
+    else CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    CK(c, hipEventRecord(e, s));
+    c->marks.push_back({e, upto});
+    return PGH_OK;
+}
+
 int sync_weights(pgh_ctx* c, hipStream_t s) {
     if (c->weights_on_device || c->weights.empty()) return PGH_OK;
     if (c->weights.size() > c->w_cap) {
@@ -582,7 +621,7 @@ int maybe_fold(pgh_ctx* c, bool force) {
     for (int64_t k = 0; k < run; ++k) c->slot_client[(size_t)((c->folded + k) % c->slots)] = -1;
     c->folded += run;
     c->st.n_folded = c->folded;
-    return PGH_OK;
+    return record_mark(c, c->stream, c->folded);
 }
 
 // Claim the slot for `client` (both modes) before bytes are written to it.
@@ -601,7 +640,7 @@ int claim_slot(pgh_ctx* c, int64_t client, int* slot_out) {
     if (held >= 0 && held != client)
         return fail(c, PGH_E_STATE, "ring full: slot %d still holds unfolded client %lld (fold front %lld)", slot,
                     (long long)held, (long long)c->folded);
-    RC(order_before_overwrite(c));
+    RC(order_stream_overwrite(c, client));
     *slot_out = slot;
     return PGH_OK;
 }
@@ -726,6 +765,8 @@ void pgh_destroy(pgh_ctx* c) {
     free_slab(c);
     for (auto& t : c->pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto e : c->pool) (void)hipEventDestroy(e);
+    clear_marks(c);
+    for (auto e : c->mark_pool) (void)hipEventDestroy(e);
     for (int k = 0; k < 2; ++k) {
         if (c->h_pin[k]) (void)hipHostFree(c->h_pin[k]);
         if (c->pin_ev[k]) (void)hipEventDestroy(c->pin_ev[k]);
@@ -816,6 +857,7 @@ int pgh_reset(pgh_ctx* c) {
     DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->fold_pending) (void)hipEventSynchronize(c->fold_done);  // folds issued on caller streams
+    clear_marks(c);
     std::fill(c->slot_client.begin(), c->slot_client.end(), -1);
     c->weights.clear();
     c->weights_on_device = false;
@@ -905,6 +947,7 @@ int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
             }
             ++run;
         }
+        if (c->streaming && run > 1) RC(order_stream_overwrite(c, client + run - 1));
         hipError_t e;
         if (c->dtype == PGH_F32)
             e = pgh::launch_synth_f32((float*)slot_row(c, slot, 0), run, c->ld, c->pg, seed, pgh::STREAM_DIFF, client,
