@@ -169,36 +169,62 @@ __global__ __launch_bounds__(TB) void k_fedavg(FedavgArgs a, int64_t ncol) {
     }
 }
 
-template <int U, bool NT, int TB = BLOCK>
+// Z_2^64 lane element: VEC = 2 (16-byte column of 2 int64) or 1 (one int64 per lane).
+template <int VEC> struct Lane64;
+template <> struct Lane64<2> {
+    using T = u64x2;
+    template <bool NT> static __device__ __forceinline__ T load(const int64_t* p) { return ld2u<NT>(p); }
+};
+template <> struct Lane64<1> {
+    using T = unsigned long long;
+    template <bool NT> static __device__ __forceinline__ T load(const int64_t* p) {
+        const T* q = reinterpret_cast<const T*>(p);
+        if constexpr (NT) return __builtin_nontemporal_load(q);
+        else return *q;
+    }
+};
+
+template <int VEC>
+__device__ __forceinline__ unsigned long long lane_elem(const typename Lane64<VEC>::T& v, int e) {
+    if constexpr (VEC == 1) return v;
+    else return v[e];
+}
+
+template <int VEC>
+__device__ __forceinline__ void lane_set(typename Lane64<VEC>::T& v, int e, unsigned long long x) {
+    if constexpr (VEC == 1) v = x;
+    else v[e] = x;
+}
+
+template <int U, bool NT, int TB, int VEC>
 __global__ __launch_bounds__(TB) void k_secagg(SecaggArgs a, int64_t ncol) {
+    using L = Lane64<VEC>;
+    using T = typename L::T;
     const int64_t stride = (int64_t)gridDim.x * TB;
     for (int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x; q < ncol; q += stride) {
-        const int64_t* col = a.shares + 2 * q;
-        const int64_t i = 2 * q;
-        const bool full = i + 2 <= a.p;
-        u64x2 acc = {0ull, 0ull};
-        if (!(a.flags & FL_FIRST)) {
-            acc[0] = a.acc[i];
-            if (full) acc[1] = a.acc[i + 1];
-        }
+        const int64_t* col = a.shares + VEC * q;
+        const int64_t i = VEC * q;
+        const int ne = (int)(i + VEC <= a.p ? VEC : a.p - i);  // valid elements of this column
+        T acc{};
+        if (!(a.flags & FL_FIRST))
+            for (int e = 0; e < ne; ++e) lane_set<VEC>(acc, e, a.acc[i + e]);
         int r = 0;
         for (; r + U <= a.n_rows; r += U) {
-            u64x2 v[U];
+            T v[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = ld2u<NT>(col + (size_t)(r + u) * a.ld);
+            for (int u = 0; u < U; ++u) v[u] = L::template load<NT>(col + (size_t)(r + u) * a.ld);
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc += v[u];     // wraps mod 2^64
+            for (int u = 0; u < U; ++u) acc += v[u];  // wraps mod 2^64
         }
-        for (; r < a.n_rows; ++r) acc += ld2u<NT>(col + (size_t)r * a.ld);
-        if (a.flags & FL_FINAL) {
-            for (int e = 0; e < 2; ++e) {
-                if (e == 1 && !full) break;
-                if (a.sum_out) a.sum_out[i + e] = (int64_t)acc[e];
-                if (a.dec_out) a.dec_out[i + e] = (float)(int64_t)acc[e] / a.divisor;
+        for (; r < a.n_rows; ++r) acc += L::template load<NT>(col + (size_t)r * a.ld);
+        for (int e = 0; e < ne; ++e) {
+            const unsigned long long x = lane_elem<VEC>(acc, e);
+            if (a.flags & FL_FINAL) {
+                if (a.sum_out) a.sum_out[i + e] = (int64_t)x;
+                if (a.dec_out) a.dec_out[i + e] = (float)(int64_t)x / a.divisor;  // float_prec decode
+            } else {
+                a.acc[i + e] = x;
             }
-        } else {
-            a.acc[i] = acc[0];
-            if (full) a.acc[i + 1] = acc[1];
         }
     }
 }
@@ -275,10 +301,14 @@ int cu_count() {
 //   12  nt     16                  1              64     1                 one lane per param
 //   13  nt     8                   1              256    1                 one lane per param
 //   14  nt     32                  1              64     1                 one lane per param
+//   15  nt     32                  1              64     4                 one lane per column
+//   16  nt     48                  1              64     1                 one lane per param
+//   17  nt     64                  1              64     1                 one lane per param
+//   18  nt     32                  1              128    1                 one lane per param
 // nt loads won 2-5 % on the once-read diff stream; among nt variants at ResNet-18 size the spread
 // is < 1 % (r01c).  Small shards are bound by lanes / CU balance, not by the loads: the auto
 // choice (PGH_VARIANT_AUTO) picks by shard size (auto_variant below, r01g measurements).
-constexpr int N_VARIANTS = 15;
+constexpr int N_VARIANTS = 19;
 
 inline unsigned grid_for(int64_t ncol, int64_t tile, bool persistent) {
     const int64_t full = (ncol + tile - 1) / tile;
@@ -312,6 +342,10 @@ hipError_t dispatch_fedavg(const FedavgArgs& a, int variant, hipStream_t s) {
     case 12: return go_fedavg<MODE, 16, 1, true, 64, 1>(a, false, s);
     case 13: return go_fedavg<MODE, 8, 1, true, 256, 1>(a, false, s);
     case 14: return go_fedavg<MODE, 32, 1, true, 64, 1>(a, false, s);
+    case 15: return go_fedavg<MODE, 32, 1, true, 64, 4>(a, false, s);
+    case 16: return go_fedavg<MODE, 48, 1, true, 64, 1>(a, false, s);
+    case 17: return go_fedavg<MODE, 64, 1, true, 64, 1>(a, false, s);
+    case 18: return go_fedavg<MODE, 32, 1, true, 128, 1>(a, false, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -332,6 +366,13 @@ int auto_variant(int64_t p, int mode) {
     if (p < 200000) return 12;
     if (p < 2000000) return 11;
     return mode == MODE_ITERATIVE ? 11 : 14;
+}
+
+template <int U, bool NT, int TB, int VEC>
+hipError_t go_secagg(const SecaggArgs& a, hipStream_t s) {
+    const int64_t ncol = (a.p + VEC - 1) / VEC;
+    k_secagg<U, NT, TB, VEC><<<grid_for(ncol, TB, false), TB, 0, s>>>(a, ncol);
+    return hipGetLastError();
 }
 
 hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
@@ -358,19 +399,31 @@ hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s) {
     if (a.n_rows > 0 && (!a.shares || (reinterpret_cast<uintptr_t>(a.shares) & 15))) return hipErrorInvalidValue;
     if (!(a.flags & FL_FINAL) && !a.acc) return hipErrorInvalidValue;
     if (!(a.flags & FL_FIRST) && !a.acc) return hipErrorInvalidValue;
-    const int64_t ncol = (a.p + 1) / 2;
     const int v = a.variant < 0 ? 11 : a.variant;  // secagg: 64-thread blocks (r01g)
     if (v >= N_VARIANTS) return hipErrorInvalidValue;
-    const unsigned g = grid_for(ncol, BLOCK, v == 1 || v == 3 || v == 5);
-    switch (v) {  // same load policy / depth as the fedavg variant of that id
-    case 2: case 3: k_secagg<8, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
-    case 4: case 5: k_secagg<16, false><<<g, BLOCK, 0, s>>>(a, ncol); break;
-    case 7: case 10: k_secagg<4, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
-    case 6: k_secagg<16, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
-    case 11: case 12: case 13: case 14: k_secagg<16, true, 64><<<grid_for(ncol, 64, false), 64, 0, s>>>(a, ncol); break;
-    default: k_secagg<8, true><<<g, BLOCK, 0, s>>>(a, ncol); break;
+    switch (v) {  // same load policy / depth / block / lane width as the fedavg variant of that id
+    case 1: case 3: case 5: {  // persistent grids
+        const int64_t ncol = (a.p + 1) / 2;
+        const unsigned g = grid_for(ncol, BLOCK, true);
+        if (v == 1) k_secagg<8, true, BLOCK, 2><<<g, BLOCK, 0, s>>>(a, ncol);
+        else if (v == 3) k_secagg<8, false, BLOCK, 2><<<g, BLOCK, 0, s>>>(a, ncol);
+        else k_secagg<16, false, BLOCK, 2><<<g, BLOCK, 0, s>>>(a, ncol);
+        return hipGetLastError();
     }
-    return hipGetLastError();
+    case 2: return go_secagg<8, false, 256, 2>(a, s);
+    case 4: return go_secagg<16, false, 256, 2>(a, s);
+    case 6: return go_secagg<16, true, 256, 2>(a, s);
+    case 7: case 10: return go_secagg<4, true, 256, 2>(a, s);
+    case 11: return go_secagg<16, true, 64, 2>(a, s);
+    case 12: return go_secagg<16, true, 64, 1>(a, s);
+    case 13: return go_secagg<8, true, 256, 1>(a, s);
+    case 14: return go_secagg<32, true, 64, 1>(a, s);
+    case 15: return go_secagg<32, true, 64, 2>(a, s);
+    case 16: return go_secagg<48, true, 64, 1>(a, s);
+    case 17: return go_secagg<64, true, 64, 1>(a, s);
+    case 18: return go_secagg<32, true, 128, 1>(a, s);
+    default: return go_secagg<8, true, 256, 2>(a, s);
+    }
 }
 
 hipError_t launch_synth_f32(float* out, int n_rows, int64_t ld, int64_t p, uint64_t seed, uint64_t stream_id,

@@ -50,7 +50,7 @@ def test_engine_reports_device(engine):
     assert device_count() >= 1
 
 
-@pytest.mark.parametrize("variant", list(range(-1, 15)))
+@pytest.mark.parametrize("variant", list(range(-1, 19)))
 def test_edge_fixtures_all_modes(engine, gold, variant):
     z = np.load(gold / "edge_f32.npz")
     engine.set_variant(variant)
@@ -64,7 +64,7 @@ def test_edge_fixtures_all_modes(engine, gold, variant):
         engine.set_variant(-1)
 
 
-@pytest.mark.parametrize("variant", list(range(-1, 15)))
+@pytest.mark.parametrize("variant", list(range(-1, 19)))
 def test_variants_mid_size(engine, variant):
     """Full tiles and a partial last tile for every variant (W = 2 tiles are 512 columns)."""
     rng = np.random.default_rng(variant + 1)
@@ -145,7 +145,7 @@ def test_secagg_wrap(engine, gold):
     assert np.array_equal(s2, z["sum"]) and np.array_equal(bits(d2), bits(z["dec_base2_prec16"]))
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 3, 6, 7, 14])
+@pytest.mark.parametrize("variant", [-1, 0, 3, 6, 7, 12, 14, 15, 17, 18])
 def test_secagg_synthetic_sampled(engine, variant):
     """250 clients x 2 parties x 1M params generated on the GPU; bit-exact on a sampled subset."""
     import torch
