@@ -1256,7 +1256,7 @@ int pgh_effective_variant(pgh_ctx* c, int mode) {
     if (!c) return PGH_E_ARG;
     if (!c->layout) return fail(c, PGH_E_STATE, "pgh_set_layout has not been called");
     if (c->variant >= 0) return c->variant;
-    if (mode == PGH_STREAM_SECAGG) return 11;
+    if (mode == PGH_STREAM_SECAGG) return 14;  // SECAGG_AUTO_VARIANT in pgh_kernels.hip
     if (!valid_mode(mode)) return fail(c, PGH_E_ARG, "unknown averaging mode %d", mode);
     return pgh::auto_variant(c->pg, mode);
 }
