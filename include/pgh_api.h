@@ -177,6 +177,12 @@ int pgh_state_scan(const uint8_t* pb, size_t n, int cap, int64_t* offsets, int64
  * has n bytes; out == tmpl patches in place. */
 int pgh_state_patch(const uint8_t* tmpl, size_t n, const float* values, int64_t n_values, uint8_t* out);
 
+/* ---- report path (host only): base64 of the diff (fl_events.py:257) ----------------------- */
+size_t pgh_b64_decoded_cap(size_t n);
+/* Python base64.b64decode semantics (non-validating); threads <= 0 = auto.  PGH_E_PARSE on bad
+ * padding. */
+int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,7 +16,7 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libpygrid_hip.so"
-SOURCES = [CSRC / "pgh_kernels.hip", CSRC / "pgh_api.cpp", CSRC / "pgh_state.cpp"]
+SOURCES = [CSRC / "pgh_kernels.hip", CSRC / "pgh_api.cpp", CSRC / "pgh_state.cpp", CSRC / "pgh_b64.cpp"]
 HEADERS = [CSRC / "pgh_kernels.h", CSRC / "pgh_state.h", ROOT / "include" / "pgh_api.h"]
 ARCH = os.environ.get("PGH_OFFLOAD_ARCH", "gfx950")
 

@@ -1,0 +1,27 @@
+"""Report path helper: the diff's base64 decode (``fl_events.report``,
+``apps/node/src/app/main/events/model_centric/fl_events.py:257``) done natively.
+
+``b64decode(s)`` is a drop-in for ``base64.b64decode(s)`` (same result, same
+``binascii.Error`` on bad padding) that splits the work over host threads; the node's
+``report`` handler can call it instead of the Python codec for multi-MB diffs.
+"""
+from __future__ import annotations
+
+import binascii
+import ctypes as C
+
+from . import _lib
+
+
+def b64decode(s, threads: int = 0) -> bytes:
+    if isinstance(s, str):
+        s = s.encode("ascii")
+    s = bytes(s)
+    lib = _lib.load()
+    cap = lib.pgh_b64_decoded_cap(len(s))
+    out = C.create_string_buffer(max(cap, 1))
+    n = C.c_size_t(0)
+    rc = lib.pgh_b64_decode(s, len(s), out, C.byref(n), int(threads))
+    if rc != 0:
+        raise binascii.Error("Incorrect padding")
+    return out.raw[: n.value]
