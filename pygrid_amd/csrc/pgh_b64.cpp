@@ -50,10 +50,11 @@ extern "C" {
 size_t pgh_b64_decoded_cap(size_t n) { return n / 4 * 3 + 3; }
 
 // Decode `in` (n chars) into `out` (capacity >= pgh_b64_decoded_cap(n)); *written = bytes.
+// out == NULL: validate only and return the exact decoded size in *written.
 // threads <= 0 picks min(16, hardware threads).  Returns PGH_OK or PGH_E_PARSE (Python's
 // "Incorrect padding" / "cannot be 1 more than a multiple of 4").
 int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int threads) {
-    if ((!in && n) || !out || !written) return PGH_E_ARG;
+    if ((!in && n) || !written) return PGH_E_ARG;  // out == NULL: validate and size only
     const unsigned char* s = (const unsigned char*)in;
     int t = threads > 0 ? threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     if (n < (1u << 18)) t = 1;
@@ -94,6 +95,10 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
     if (rem == 1) return PGH_E_PARSE;
     if ((rem == 2 && pads < 2) || (rem == 3 && pads < 1)) return PGH_E_PARSE;
     const size_t n4 = d / 4;
+    if (!out) {
+        *written = n4 * 3 + (rem == 2 ? 1 : rem == 3 ? 2 : 0);
+        return PGH_OK;
+    }
     if (n4 < (1u << 16)) t = 1;
     const size_t per = (n4 + t - 1) / t;
     std::vector<std::thread> th;
