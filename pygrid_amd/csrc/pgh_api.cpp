@@ -937,7 +937,7 @@ int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
         RC(claim_slot(c, client, &slot));
         // contiguous run of slots from `slot`, all claimable
         int run = 1;
-        while (k + run < n && slot + run < c->slots) {
+        while (k + run < n && slot + run < c->slots && run < 65535) {  // 65535: synth grid rows
             const int64_t cl = client + run;
             if (c->streaming) {
                 const int64_t held = c->slot_client[(size_t)(slot + run)];

@@ -60,3 +60,21 @@ def test_null_and_bad_arguments_return_status():
     assert lib.pgh_set_layout(None, 1, None) == -1
     assert lib.pgh_stats(None, None) == -1
     assert lib.pgh_last_error(None) is not None
+
+
+def test_plain_c_consumer_compiles_links_and_runs(tmp_path):
+    """The header is valid C99 and the library links from C (what a cgo / JNI / N-API binding sees)."""
+    import subprocess
+
+    exe = tmp_path / "consumer"
+    lib_dir = ROOT / "pygrid_amd"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", str(ROOT / "include"),
+                    str(ROOT / "tests" / "c_abi_consumer.c"), "-L", str(lib_dir), "-lpygrid_hip",
+                    f"-Wl,-rpath,{lib_dir}", "-o", str(exe)], check=True)
+    import torch
+
+    if torch.cuda.is_available():
+        return  # the run below checks the no-GPU error path
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, (out.returncode, out.stdout, out.stderr)
+    assert out.stdout.startswith("ok")
