@@ -88,7 +88,9 @@ class OverlappedGather:
         self.local = torch.zeros(self.s, dtype=dtype, device=device)
         self.recv = [torch.empty(world * (b - a), dtype=dtype, device=device) for a, b in self.ranges]
 
-    def run(self, fold_range):
+    def run(self, fold_range, force_collective: bool = False):
+        """``force_collective`` issues the all-gathers even at world size 1 (tests the RCCL path
+        on a one-GPU box)."""
         import torch.distributed as dist
 
         works = []
@@ -96,7 +98,7 @@ class OverlappedGather:
             n = min(b, self.pg) - a
             if n > 0:
                 fold_range(a, n)
-            if self.world > 1:
+            if self.world > 1 or force_collective:
                 if r.device.type != "cpu" and dist.get_backend(self.group) == "nccl":
                     works.append(dist.all_gather_into_tensor(r, self.local[a:b], group=self.group, async_op=True))
                 else:

@@ -409,3 +409,42 @@ def test_reingest_waits_for_inflight_fold(engine):
     d2 = d[:, idx].copy()
     d2[0] = new0[idx]
     assert same(out2.cpu().numpy()[idx], coracle.fedavg(0, d2, c[idx]))
+
+
+def test_rccl_overlapped_gather_world1(engine):
+    """The RCCL ("nccl" backend) all-gather path of OverlappedGather, forced at world size 1:
+    async all_gather_into_tensor per fold range on the torch stream, wait, assemble."""
+    import os
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from pygrid_amd.sharding import OverlappedGather
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        rng = np.random.default_rng(51)
+        P, N = 1_000_003, 7
+        d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+        c = rng.standard_normal(P).astype(F)
+        engine.set_layout([P])
+        engine.reserve(N)
+        for k in range(N):
+            engine.ingest(k, d[k])
+        ck = torch.from_numpy(c).cuda()
+        og = OverlappedGather(P, 1, 0, chunks=8)
+        sp = torch.cuda.current_stream().cuda_stream
+        og.run(lambda off, n: engine.fedavg_device_range(0, off, n, ck.data_ptr(), og.local.data_ptr(), sp),
+               force_collective=True)
+        full = og.assemble()
+        torch.cuda.synchronize()
+        idx = rng.integers(0, P, 2000)
+        assert same(full.cpu().numpy()[idx], coracle.fedavg(0, d[:, idx], c[idx]))
+    finally:
+        dist.destroy_process_group()
