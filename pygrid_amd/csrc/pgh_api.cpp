@@ -320,9 +320,6 @@ bool is_pinned(const void* p) {
     return attr.type == hipMemoryTypeHost;
 }
 
-// host bytes -> HBM on the copy stream.  Page-locked sources are DMA'd directly (the call
-// then waits for the copy: the caller's buffer is only borrowed); pageable sources go through
-// the pinned ring, so the host memcpy of one slot overlaps the DMA of the other.
 struct Piece {
     const uint8_t* src;
     size_t n;
@@ -358,6 +355,9 @@ int stage_pieces_h2d(pgh_ctx* c, uint8_t* dst, const std::vector<Piece>& pieces)
     return PGH_OK;
 }
 
+// host bytes -> HBM on the copy stream.  Page-locked sources are DMA'd directly (the call
+// then waits for the copy: the caller's buffer is only borrowed); pageable sources go through
+// the pinned ring, so the host memcpy of one slot overlaps the DMA of the other.
 // host bytes -> HBM on the copy stream.  Page-locked sources are DMA'd directly (the call
 // then waits for the copy: the caller's buffer is only borrowed); pageable sources go through
 // the pinned ring, so the host memcpy of one slot overlaps the DMA of the other.

@@ -1,0 +1,97 @@
+// Host-only fuzz of the untrusted-input parsers (client State bytes, base64 diff text) under
+// AddressSanitizer + UndefinedBehaviorSanitizer.  Built and run by tests/test_native_sanitizers.py
+// with g++ (no HIP): pgh_state.cpp and pgh_b64.cpp need only include/pgh_api.h.
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "pgh_api.h"
+
+static void put_varint(std::vector<uint8_t>& b, uint64_t v) {
+    while (v >= 0x80) { b.push_back((uint8_t)(v | 0x80)); v >>= 7; }
+    b.push_back((uint8_t)v);
+}
+static void put_field(std::vector<uint8_t>& b, uint32_t f, const std::vector<uint8_t>& payload) {
+    put_varint(b, (f << 3) | 2);
+    put_varint(b, payload.size());
+    b.insert(b.end(), payload.begin(), payload.end());
+}
+
+// A valid State (restated schema: tensors=2 -> torch_tensor=1 -> contents_data=4 -> shape=1,
+// dtype=2, contents_float32=12) with `t` tensors of random sizes.
+static std::vector<uint8_t> make_state(std::mt19937_64& rng, int t) {
+    std::vector<uint8_t> st;
+    for (int k = 0; k < t; ++k) {
+        const int n = (int)(rng() % 40);
+        std::vector<uint8_t> dims, size, td, tt, stt, payload(4 * (size_t)n, 0x3f);
+        put_varint(dims, (uint64_t)n);
+        put_field(size, 1, dims);
+        put_field(td, 1, size);
+        put_field(td, 2, std::vector<uint8_t>{'f', 'l', 'o', 'a', 't', '3', '2'});
+        if (n) put_field(td, 12, payload);
+        put_field(tt, 4, td);
+        put_field(stt, 1, tt);
+        put_field(st, 2, stt);
+    }
+    return st;
+}
+
+int main(int argc, char** argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 20000;
+    std::mt19937_64 rng(12345);
+    int parsed = 0, rejected = 0;
+    for (int it = 0; it < iters; ++it) {
+        std::vector<uint8_t> pb = make_state(rng, 1 + (int)(rng() % 5));
+        const int muts = (int)(rng() % 6);
+        for (int m = 0; m < muts && !pb.empty(); ++m) {
+            const size_t i = rng() % pb.size();
+            switch (rng() % 4) {
+            case 0: pb[i] = (uint8_t)rng(); break;
+            case 1: pb.resize(i); break;  // truncate
+            case 2: pb.insert(pb.begin() + (long)i, (uint8_t)rng()); break;
+            default: pb[i] ^= 0x80; break;  // flip varint continuation
+            }
+        }
+        // exact-size heap copy so ASan sees any read past the end
+        uint8_t* buf = new uint8_t[pb.size() ? pb.size() : 1];
+        if (!pb.empty()) std::memcpy(buf, pb.data(), pb.size());
+        int nt = 0;
+        int64_t offs[8], cnts[8];
+        const int rc = pgh_state_scan(buf, pb.size(), 8, offs, cnts, &nt);
+        if (rc == PGH_OK) {
+            ++parsed;
+            int64_t total = 0;
+            for (int k = 0; k < nt && k < 8; ++k) {
+                if (offs[k] < 0 || (size_t)(offs[k] + 4 * cnts[k]) > pb.size()) { std::printf("span out of range\n"); return 2; }
+                total += cnts[k];
+            }
+            if (nt <= 8) {
+                std::vector<float> vals((size_t)total + 1, 1.0f);
+                std::vector<uint8_t> out(pb.size() ? pb.size() : 1);
+                if (pgh_state_patch(buf, pb.size(), vals.data(), total, out.data()) != PGH_OK) { std::printf("patch failed\n"); return 3; }
+            }
+        } else {
+            ++rejected;
+        }
+        delete[] buf;
+        // base64 text with random junk
+        std::string s;
+        const int len = (int)(rng() % 64);
+        const char* alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/= \n*";
+        for (int k = 0; k < len; ++k) s.push_back(alpha[rng() % 67]);
+        char* txt = new char[s.size() ? s.size() : 1];
+        std::memcpy(txt, s.data(), s.size());
+        size_t w = 0;
+        if (pgh_b64_decode(txt, s.size(), nullptr, &w, 1) == PGH_OK) {
+            std::vector<uint8_t> out(w ? w : 1);
+            size_t w2 = 0;
+            if (pgh_b64_decode(txt, s.size(), out.data(), &w2, 1) != PGH_OK || w2 != w) { std::printf("b64 size mismatch\n"); return 4; }
+        }
+        delete[] txt;
+    }
+    std::printf("ok parsed=%d rejected=%d\n", parsed, rejected);
+    return 0;
+}
