@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define PGH_ABI_VERSION 1
+#define PGH_ABI_VERSION 2
 
 typedef struct pgh_ctx pgh_ctx;
 
@@ -61,7 +61,7 @@ typedef struct {
     uint64_t h2d_bytes_total;  /* bytes moved host -> HBM by ingest */
     double close_ms_last;      /* wall time of the last pgh_fedavg / pgh_secagg (host in/out) */
     int64_t p_shard;           /* params in this context's shard */
-    int64_t ld;                /* slab row stride (elements) */
+    int64_t ld;                /* slab block width = row stride inside a block (elements) */
     int64_t n_folded;          /* stream mode: clients folded into the running state */
     int32_t n_clients;         /* clients ingested since the last reset */
     int32_t max_clients;       /* slab capacity (slots) */
@@ -164,8 +164,12 @@ int pgh_set_variant(pgh_ctx* ctx, int variant);
 int pgh_effective_variant(pgh_ctx* ctx, int mode);
 int pgh_stats(pgh_ctx* ctx, pgh_stats_t* out);     /* synchronises pending timing events */
 int pgh_reset_stats(pgh_ctx* ctx);
-/* Device pointer of the slab and its row stride, for callers that drive the kernels. */
-int pgh_slab(pgh_ctx* ctx, void** d_slab, int64_t* ld);
+/* Device pointer and geometry of the slab, for callers that drive the kernels.  The slab is
+ * column-blocked: element (row r, shard param i) is at
+ *   d_slab[(i / ld) * block_pitch + r * ld + i % ld]
+ * (row r = slot * n_parties + party).  A shard of at most one block has block_pitch 0 and is
+ * plain row-major [rows][ld]. */
+int pgh_slab(pgh_ctx* ctx, void** d_slab, int64_t* ld, int64_t* block_pitch);
 int pgh_sync(pgh_ctx* ctx);                       /* wait for the context's streams */
 
 /* ---- State codec (host only; replaces syft serde at model_manager.py:79-103) ------------- */

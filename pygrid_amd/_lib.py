@@ -79,7 +79,7 @@ SIGNATURES = {
     "pgh_effective_variant": (_i, [_vp, _i]),
     "pgh_stats": (_i, [_vp, C.POINTER(Stats)]),
     "pgh_reset_stats": (_i, [_vp]),
-    "pgh_slab": (_i, [_vp, C.POINTER(_vp), _P64]),
+    "pgh_slab": (_i, [_vp, C.POINTER(_vp), _P64, _P64]),
     "pgh_state_scan": (_i, [C.c_char_p, _sz, _i, _P64, _P64, C.POINTER(C.c_int)]),
     "pgh_state_patch": (_i, [C.c_char_p, _sz, _vp, _i64, _vp]),
     "pgh_b64_decoded_cap": (_sz, [_sz]),

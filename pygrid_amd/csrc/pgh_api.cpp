@@ -1,8 +1,10 @@
 // libpygrid_hip: C-ABI context around the gfx950 aggregation kernels.
 //
 // One pgh_ctx = one GPU = one parameter shard.  It owns
-//   * the HBM slab: R slots x rows_per_client rows of ld elements (fp32 diffs, or
-//     n_parties int64 share rows per client), rows padded to 256 B;
+//   * the HBM slab: R slots x rows_per_client rows (fp32 diffs, or n_parties int64 share rows
+//     per client), column-blocked: the shard is cut into blocks of bw columns (256 KiB of one
+//     row by default) and each block stores all rows one after another (SlabMap in
+//     pgh_kernels.h), so a kernel lane walking down the rows of its column stays in one block;
 //   * the [P_shard] device vectors (checkpoint, output, running fold state, weights);
 //   * a 2-slot pinned host ring through which pageable host bytes reach the slab
 //     (multi-threaded host memcpy into a pinned slot overlapping the previous slot's DMA on a
@@ -146,8 +148,14 @@ struct pgh_ctx {
     std::vector<hipEvent_t> mark_pool;
 
     std::vector<int64_t> numel;
-    int64_t P = 0, lo = 0, hi = 0, pg = 0, ld = 0;
+    int64_t P = 0, lo = 0, hi = 0, pg = 0;
+    int64_t pvec = 0;  // length of the [P_shard] device vectors: pg rounded up to 64
     bool layout = false;
+    // slab geometry (pgh_reserve): bw columns per block, nb blocks, bstride elements per block
+    int64_t bw = 0, nb = 0, bstride = 0;
+    int bshift = 62;
+    int64_t bmask = 0;
+    size_t block_bytes = 256u << 10;  // PGH_BLOCK_BYTES; 0 = one block (plain row-major rows)
 
     int slots = 0, dtype = PGH_F32, parties = 1;
     void* d_slab = nullptr;
@@ -168,8 +176,7 @@ struct pgh_ctx {
     int pin_next = 0;
     int copy_threads = 8;
     std::unique_ptr<CopyPool> pool_copy;
-    bool register_ingest = false;
-    int ld_mod = 1;  // PGH_REGISTER_INGEST=1: page-lock State messages instead of staging
+    bool register_ingest = false;  // PGH_REGISTER_INGEST=1: page-lock State messages instead of staging
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
     std::vector<float> weights;
@@ -268,9 +275,67 @@ int check_dtype(pgh_ctx* c, int dtype) {
     return PGH_OK;
 }
 
+// Slab geometry for kernels (off = 0) and the start of a slot's first row inside block 0.
+pgh::SlabMap slab_map(const pgh_ctx* c) { return pgh::SlabMap{c->bw, c->bstride, c->bshift, c->bmask, 0}; }
+
 uint8_t* slot_row(pgh_ctx* c, int slot, int party) {
     const size_t row = (size_t)slot * c->parties + party;
-    return (uint8_t*)c->d_slab + row * (size_t)c->ld * esize(c->dtype);
+    return (uint8_t*)c->d_slab + row * (size_t)c->bw * esize(c->dtype);
+}
+
+// Columns per block for a shard of pg elements of es bytes: one block when the whole row fits
+// in block_bytes (or blocking is off), else the widest power of two <= block_bytes whose
+// padding of the last block stays within 1/16 of the row.
+void slab_geometry(int64_t pg, size_t es, size_t block_bytes, int64_t* bw, int64_t* nb, int* bshift) {
+    const int64_t whole = (pg + 63) & ~(int64_t)63;
+    int64_t maxc = 64;
+    while (maxc * 2 * (int64_t)es <= (int64_t)block_bytes) maxc *= 2;
+    if (block_bytes == 0 || whole <= maxc) { *bw = whole; *nb = 1; *bshift = 62; return; }
+    int64_t b = maxc;
+    while (b > 64 && ((pg + b - 1) / b) * b - pg > pg / 16) b /= 2;
+    *bw = b;
+    *nb = (pg + b - 1) / b;
+    int sh = 0;
+    while ((int64_t(1) << sh) < b) ++sh;
+    *bshift = sh;
+}
+
+// Where host bytes land: a slab row (blocked) or a [p] vector (one block).
+struct Dest {
+    uint8_t* base;       // row start in block 0 / vector start
+    pgh::SlabMap map;
+    size_t es;
+};
+Dest row_dest(pgh_ctx* c, int slot, int party) { return Dest{slot_row(c, slot, party), slab_map(c), esize(c->dtype)}; }
+Dest vec_dest(void* v, int64_t n, size_t es) { return Dest{(uint8_t*)v, pgh::single_block(n), es}; }
+
+// Elements [i0, i0 + n) of one row from contiguous host memory: the partial first block, the
+// whole blocks as ONE 2-D copy (block rows bstride apart), the partial last block.
+int h2d_range(pgh_ctx* c, const Dest& d, int64_t i0, const uint8_t* src, int64_t n, hipStream_t s) {
+    const size_t es = d.es;
+    if (n <= 0) return PGH_OK;
+    if (d.map.bshift == 62) {
+        CK(c, hipMemcpyAsync(d.base + (size_t)i0 * es, src, (size_t)n * es, hipMemcpyHostToDevice, s));
+        return PGH_OK;
+    }
+    const int64_t bw = d.map.ld, i1 = i0 + n;
+    int64_t i = i0;
+    if (i & (bw - 1)) {  // head
+        const int64_t e = std::min(i1, (i | (bw - 1)) + 1);
+        CK(c, hipMemcpyAsync(d.base + (size_t)d.map.at(i) * es, src, (size_t)(e - i) * es, hipMemcpyHostToDevice, s));
+        src += (size_t)(e - i) * es;
+        i = e;
+    }
+    const int64_t full = (i1 - i) / bw;
+    if (full > 0) {
+        CK(c, hipMemcpy2DAsync(d.base + (size_t)d.map.at(i) * es, (size_t)d.map.bstride * es, src, (size_t)bw * es,
+                               (size_t)bw * es, (size_t)full, hipMemcpyHostToDevice, s));
+        src += (size_t)(full * bw) * es;
+        i += full * bw;
+    }
+    if (i < i1)  // tail
+        CK(c, hipMemcpyAsync(d.base + (size_t)d.map.at(i) * es, src, (size_t)(i1 - i) * es, hipMemcpyHostToDevice, s));
+    return PGH_OK;
 }
 
 hipEvent_t take_event(pgh_ctx* c) {
@@ -327,7 +392,7 @@ struct Piece {
 
 // Concatenated host pieces -> HBM at `dst`, through the pinned ring: each slot is filled by
 // (multi-threaded) host copies of as many pieces as fit, then DMA'd while the next slot fills.
-int stage_pieces_h2d(pgh_ctx* c, uint8_t* dst, const std::vector<Piece>& pieces) {
+int stage_pieces_h2d(pgh_ctx* c, const Dest& dst, const std::vector<Piece>& pieces) {
     const double t0 = now_ms();
     size_t total = 0, done = 0, pi = 0, poff = 0;
     for (auto& p : pieces) total += p.n;
@@ -345,7 +410,8 @@ int stage_pieces_h2d(pgh_ctx* c, uint8_t* dst, const std::vector<Piece>& pieces)
             if (poff == pieces[pi].n) { ++pi; poff = 0; }
         }
         c->pool_copy->run(segs);
-        CK(c, hipMemcpyAsync(dst + done, c->h_pin[slot], fill, hipMemcpyHostToDevice, c->copy));
+        // slot fills are whole multiples of 4 KiB but the last, so `done` stays element-aligned
+        RC(h2d_range(c, dst, (int64_t)(done / dst.es), c->h_pin[slot], (int64_t)(fill / dst.es), c->copy));
         CK(c, hipEventRecord(c->pin_ev[slot], c->copy));
         c->pin_used[slot] = true;
         done += fill;
@@ -358,13 +424,10 @@ int stage_pieces_h2d(pgh_ctx* c, uint8_t* dst, const std::vector<Piece>& pieces)
 // host bytes -> HBM on the copy stream.  Page-locked sources are DMA'd directly (the call
 // then waits for the copy: the caller's buffer is only borrowed); pageable sources go through
 // the pinned ring, so the host memcpy of one slot overlaps the DMA of the other.
-// host bytes -> HBM on the copy stream.  Page-locked sources are DMA'd directly (the call
-// then waits for the copy: the caller's buffer is only borrowed); pageable sources go through
-// the pinned ring, so the host memcpy of one slot overlaps the DMA of the other.
-int stage_h2d(pgh_ctx* c, void* dst, const uint8_t* src, size_t n, bool pinned_src) {
-    if (!pinned_src) return stage_pieces_h2d(c, (uint8_t*)dst, {Piece{src, n}});
+int stage_h2d(pgh_ctx* c, const Dest& dst, const uint8_t* src, size_t n, bool pinned_src) {
+    if (!pinned_src) return stage_pieces_h2d(c, dst, {Piece{src, n}});
     const double t0 = now_ms();
-    CK(c, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->copy));
+    RC(h2d_range(c, dst, 0, src, (int64_t)(n / dst.es), c->copy));
     CK(c, hipStreamSynchronize(c->copy));
     c->st.h2d_ms_total += now_ms() - t0;
     c->st.h2d_bytes_total += n;
@@ -556,8 +619,9 @@ int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const Fina
         const uint64_t pg = (uint64_t)len;
         if (kind == KIND_SECAGG) {
             pgh::SecaggArgs a{};
-            a.shares = (const int64_t*)slot_row(c, slot, 0) + off;
-            a.ld = c->ld;
+            a.shares = (const int64_t*)slot_row(c, slot, 0);
+            a.map = slab_map(c);
+            a.map.off = off;
             a.n_rows = (int)(seg * c->parties);
             a.p = len;
             a.acc = c->d_uacc + off;
@@ -571,8 +635,9 @@ int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const Fina
             RC(timed_launch(c, s, bytes, [&] { return pgh::launch_secagg(a, s); }));
         } else {
             pgh::FedavgArgs a{};
-            a.diffs = (const float*)slot_row(c, slot, 0) + off;
-            a.ld = c->ld;
+            a.diffs = (const float*)slot_row(c, slot, 0);
+            a.map = slab_map(c);
+            a.map.off = off;
             a.n_rows = (int)seg;
             a.client0 = c0 + done;
             a.p = len;
@@ -741,7 +806,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_COPY_THREADS")) c->copy_threads = std::max(1, std::atoi(e));
     c->pool_copy.reset(new CopyPool(c->copy_threads));
     if (const char* e = std::getenv("PGH_REGISTER_INGEST")) c->register_ingest = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PGH_LD_MOD")) c->ld_mod = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("PGH_BLOCK_BYTES")) c->block_bytes = (size_t)std::max(0LL, std::atoll(e));
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming) == hipSuccess &&
@@ -805,12 +870,8 @@ int pgh_set_shard(pgh_ctx* c, int64_t lo, int64_t hi) {
     c->lo = lo;
     c->hi = hi;
     c->pg = hi - lo;
-    c->ld = (c->pg + 63) & ~(int64_t)63;  // 256-B (fp32) / 512-B (int64) row pitch
-    // Row pitch skew: (ld / 64) % ld_mod == 1 (PGH_LD_MOD, experiment knob; 1 = no skew)
-    if (c->ld_mod > 1)
-        while ((c->ld / 64) % c->ld_mod != 1) c->ld += 64;
+    c->pvec = (c->pg + 63) & ~(int64_t)63;
     c->st.p_shard = c->pg;
-    c->st.ld = c->ld;
     return PGH_OK;
 }
 
@@ -824,14 +885,19 @@ int pgh_reserve(pgh_ctx* c, int max_clients, int dtype, int n_parties) {
     DeviceGuard g(c->device);
     free_slab(c);
     const size_t rows = (size_t)max_clients * (size_t)n_parties;
-    const size_t bytes = rows * (size_t)c->ld * esize(dtype);
+    slab_geometry(c->pg, esize(dtype), c->block_bytes, &c->bw, &c->nb, &c->bshift);
+    c->bmask = c->bshift == 62 ? (int64_t(1) << 62) - 1 : c->bw - 1;
+    c->bstride = c->nb > 1 ? (int64_t)rows * c->bw : 0;
+    const size_t bytes = rows * (size_t)(c->nb * c->bw) * esize(dtype);
     if (hipMalloc(&c->d_slab, bytes) != hipSuccess) {
         c->d_slab = nullptr;
         (void)hipGetLastError();
-        return fail(c, PGH_E_OOM, "slab allocation of %zu bytes (%zu rows x %lld) failed", bytes, rows, (long long)c->ld);
+        return fail(c, PGH_E_OOM, "slab allocation of %zu bytes (%zu rows x %lld) failed", bytes, rows,
+                    (long long)(c->nb * c->bw));
     }
     c->slab_bytes = bytes;
-    const size_t v4 = (size_t)c->ld * 4, v8 = (size_t)c->ld * 8;
+    c->st.ld = c->bw;
+    const size_t v4 = (size_t)c->pvec * 4, v8 = (size_t)c->pvec * 8;
     bool ok = hipMalloc((void**)&c->d_ckpt, v4) == hipSuccess && hipMalloc((void**)&c->d_out, v4) == hipSuccess &&
               hipMalloc((void**)&c->d_acc, v4) == hipSuccess && hipMalloc((void**)&c->d_uacc, v8) == hipSuccess &&
               hipMalloc((void**)&c->d_sum, v8) == hipSuccess && hipMalloc((void**)&c->d_dec, v4) == hipSuccess;
@@ -886,7 +952,7 @@ int pgh_ingest_raw(pgh_ctx* c, int client, const void* flat, size_t nbytes, int 
     const size_t row_elems = nbytes == whole ? (size_t)c->P : (size_t)c->pg;
     const size_t first = nbytes == whole ? (size_t)c->lo : 0;
     for (int s = 0; s < c->parties; ++s)
-        RC(stage_h2d(c, slot_row(c, slot, s), src + ((size_t)s * row_elems + first) * es, (size_t)c->pg * es, pinned));
+        RC(stage_h2d(c, row_dest(c, slot, s), src + ((size_t)s * row_elems + first) * es, (size_t)c->pg * es, pinned));
     return mark_ingested(c, client, slot);
 }
 
@@ -907,22 +973,23 @@ int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
         hipHostRegister((void*)pb, n, hipHostRegisterDefault) == hipSuccess) {
         // page-lock the message for the duration of the call and DMA the spans directly
         const double t0 = now_ms();
+        const Dest d = row_dest(c, slot, 0);
         size_t off = 0;
-        hipError_t e = hipSuccess;
+        int rc = PGH_OK;
         for (auto& p : pieces) {
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(slot_row(c, slot, 0) + off, p.src, p.n, hipMemcpyHostToDevice, c->copy);
+            if (rc == PGH_OK) rc = h2d_range(c, d, (int64_t)(off / 4), p.src, (int64_t)(p.n / 4), c->copy);
             off += p.n;
         }
-        if (e == hipSuccess) e = hipStreamSynchronize(c->copy);
+        hipError_t e = rc == PGH_OK ? hipStreamSynchronize(c->copy) : hipSuccess;
         (void)hipHostUnregister((void*)pb);
+        if (rc) return rc;
         if (e != hipSuccess) return fail(c, PGH_E_HIP, "registered ingest failed: %s", hipGetErrorString(e));
         c->st.h2d_ms_total += now_ms() - t0;
         c->st.h2d_bytes_total += off;
         return mark_ingested(c, client, slot);
     }
     (void)hipGetLastError();
-    RC(stage_pieces_h2d(c, slot_row(c, slot, 0), pieces));
+    RC(stage_pieces_h2d(c, row_dest(c, slot, 0), pieces));
     return mark_ingested(c, client, slot);
 }
 
@@ -950,11 +1017,11 @@ int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
         if (c->streaming && run > 1) RC(order_stream_overwrite(c, client + run - 1));
         hipError_t e;
         if (c->dtype == PGH_F32)
-            e = pgh::launch_synth_f32((float*)slot_row(c, slot, 0), run, c->ld, c->pg, seed, pgh::STREAM_DIFF, client,
-                                      c->lo, pgh::DIFF_SCALE, c->copy);
+            e = pgh::launch_synth_f32((float*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->pg, seed,
+                                      pgh::STREAM_DIFF, client, c->lo, pgh::DIFF_SCALE, c->copy);
         else
-            e = pgh::launch_synth_shares((int64_t*)slot_row(c, slot, 0), run, c->parties, c->ld, c->pg, seed, client,
-                                         c->lo, 1000.0f, c->copy);
+            e = pgh::launch_synth_shares((int64_t*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->parties,
+                                         c->pg, seed, client, c->lo, 1000.0f, c->copy);
         if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic fill failed: %s", hipGetErrorString(e));
         for (int j = 0; j < run; ++j) {
             if (c->slot_client[(size_t)(slot + j)] != client + j) c->st.n_clients += 1;
@@ -982,12 +1049,14 @@ int pgh_synth_ckpt_device(pgh_ctx* c, uint64_t seed, float* d_ckpt, void* stream
     DeviceGuard g(c->device);
     hipStream_t s = (hipStream_t)stream;
     if (c->pg % 4 == 0) {  // one row of exactly P_shard elements
-        hipError_t e = pgh::launch_synth_f32(d_ckpt, 1, c->pg, c->pg, seed, pgh::STREAM_CKPT, 0, c->lo, pgh::CKPT_SCALE, s);
+        hipError_t e = pgh::launch_synth_f32(d_ckpt, pgh::single_block(c->pg), c->pg, 1, c->pg, seed, pgh::STREAM_CKPT, 0,
+                                             c->lo, pgh::CKPT_SCALE, s);
         if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic checkpoint failed: %s", hipGetErrorString(e));
         return PGH_OK;
     }
     if (!c->d_ckpt) return fail(c, PGH_E_STATE, "pgh_reserve has not been called");
-    hipError_t e = pgh::launch_synth_f32(c->d_ckpt, 1, c->ld, c->pg, seed, pgh::STREAM_CKPT, 0, c->lo, pgh::CKPT_SCALE, s);
+    hipError_t e = pgh::launch_synth_f32(c->d_ckpt, pgh::single_block(c->pvec), c->pvec, 1, c->pg, seed,
+                                         pgh::STREAM_CKPT, 0, c->lo, pgh::CKPT_SCALE, s);
     if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic checkpoint failed: %s", hipGetErrorString(e));
     CK(c, hipMemcpyAsync(d_ckpt, c->d_ckpt, sizeof(float) * c->pg, hipMemcpyDeviceToDevice, s));
     return PGH_OK;
@@ -1050,7 +1119,7 @@ int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
     const double t0 = now_ms();
     const size_t bytes = sizeof(float) * (size_t)c->pg;
     RC(order_before_overwrite(c));
-    RC(stage_h2d(c, c->d_ckpt, (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
+    RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
     RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
     if (is_pinned(out)) {
         CK(c, hipMemcpyAsync(out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
@@ -1074,7 +1143,7 @@ int pgh_ckpt_upload(pgh_ctx* c, const float* ckpt, size_t nbytes) {
     DeviceGuard g(c->device);
     RC(order_before_overwrite(c));
     const uint8_t* src = (const uint8_t*)ckpt + (nbytes == whole ? 4 * (size_t)c->lo : 0);
-    return stage_h2d(c, c->d_ckpt, src, shard, is_pinned(ckpt));
+    return stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), src, shard, is_pinned(ckpt));
 }
 
 int pgh_ckpt_upload_state(pgh_ctx* c, const uint8_t* pb, size_t n) {
@@ -1086,7 +1155,7 @@ int pgh_ckpt_upload_state(pgh_ctx* c, const uint8_t* pb, size_t n) {
     for (auto& sp : spans) pieces.push_back(Piece{pb + sp.first, sp.second});
     DeviceGuard g(c->device);
     RC(order_before_overwrite(c));
-    return stage_pieces_h2d(c, (uint8_t*)c->d_ckpt, pieces);
+    return stage_pieces_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), pieces);
 }
 
 int pgh_fedavg_resident(pgh_ctx* c, int mode) {
@@ -1283,10 +1352,11 @@ int pgh_reset_stats(pgh_ctx* c) {
     return PGH_OK;
 }
 
-int pgh_slab(pgh_ctx* c, void** d_slab, int64_t* ld) {
-    if (!c || !d_slab || !ld) return PGH_E_ARG;
+int pgh_slab(pgh_ctx* c, void** d_slab, int64_t* ld, int64_t* block_pitch) {
+    if (!c || !d_slab || !ld || !block_pitch) return PGH_E_ARG;
     *d_slab = c->d_slab;
-    *ld = c->ld;
+    *ld = c->bw;
+    *block_pitch = c->bstride;
     return PGH_OK;
 }
 

@@ -11,9 +11,29 @@ enum { MODE_MEAN = 0, MODE_ITERATIVE = 1, MODE_WEIGHTED = 2 };
 // flags for a chunked (client-streaming) reduction
 enum { FL_FIRST = 1, FL_FINAL = 2 };
 
+// Column-blocked slab: the shard's params are cut into blocks of `ld`
+// columns; block j holds every row's columns [j*ld, (j+1)*ld) row after row, so element
+// (row r, shard param i) lives at  (i >> bshift) * bstride + r * ld + (i & bmask).
+// A lane walking down the rows of one column then streams through one compact block (rows ld
+// apart) instead of rows a whole shard apart.  One block (bshift = 62) is the plain row-major
+// [rows][ld] layout, used for shards of at most one block and for the [p] vectors.
+struct SlabMap {
+    int64_t ld;        // columns per block = row stride inside a block (multiple of 4; slab: of 64)
+    int64_t bstride;   // elements from block j to block j + 1 (= rows in the slab x ld)
+    int bshift;        // log2(ld) when blocked, 62 for a single block
+    int64_t bmask;     // ld - 1 when blocked, 2^62 - 1 for a single block
+    int64_t off;       // shard param of the launch's local column 0 (range folds)
+    __host__ __device__ int64_t at(int64_t local) const {
+        const int64_t i = off + local;
+        return (i >> bshift) * bstride + (i & bmask);
+    }
+};
+
+inline SlabMap single_block(int64_t ld) { return SlabMap{ld, 0, 62, (int64_t(1) << 62) - 1, 0}; }
+
 struct FedavgArgs {
-    const float* diffs;     // [n_rows][ld] fp32, rows = clients client0 .. client0+n_rows-1
-    int64_t ld;             // row stride in elements, multiple of 4, >= p
+    const float* diffs;     // slab at the first row: clients client0 .. client0+n_rows-1
+    SlabMap map;            // slab geometry; map.off = shard param of local column 0
     int n_rows;
     int64_t client0;        // global index of row 0 (iterative k, weight index)
     int64_t p;              // params in this shard
@@ -29,8 +49,8 @@ struct FedavgArgs {
 hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s);
 
 struct SecaggArgs {
-    const int64_t* shares;  // [n_rows][ld] int64 (rows = clients x parties), ld even, >= p
-    int64_t ld;
+    const int64_t* shares;  // slab at the first row (rows = clients x parties)
+    SlabMap map;
     int n_rows;
     int64_t p;
     uint64_t* acc;          // [p] running wrap-sum; read unless FL_FIRST, written unless FL_FINAL
@@ -44,12 +64,12 @@ hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s);
 // The fp32 fold variant the auto choice (variant < 0) picks for a shard of p params.
 int auto_variant(int64_t p, int mode);
 
-// Deterministic synthetic inputs (restated bit for bit by oracle/oracle.py).
-hipError_t launch_synth_f32(float* out, int n_rows, int64_t ld, int64_t p, uint64_t seed,
-                            uint64_t stream_id, int64_t row0, int64_t idx0, float scale,
-                            hipStream_t s);
-hipError_t launch_synth_shares(int64_t* out, int n_clients, int n_parties, int64_t ld, int64_t p,
-                               uint64_t seed, int64_t client0, int64_t idx0, float enc_scale,
+// Deterministic synthetic inputs (restated bit for bit by oracle/oracle.py).  `out` is the
+// slab (or a [p] vector: single_block) at its first row; params [p, ncols) are zero-filled.
+hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_rows, int64_t p, uint64_t seed,
+                            uint64_t stream_id, int64_t row0, int64_t idx0, float scale, hipStream_t s);
+hipError_t launch_synth_shares(int64_t* out, const SlabMap& m, int64_t ncols, int n_clients, int n_parties,
+                               int64_t p, uint64_t seed, int64_t client0, int64_t idx0, float enc_scale,
                                hipStream_t s);
 
 constexpr uint64_t STREAM_DIFF = 0, STREAM_CKPT = 1, STREAM_SECRET = 2, STREAM_SHARE = 3;

@@ -8,12 +8,13 @@
 // K3  k_secagg                 Z_2^64 wrap-sum over [clients*parties][P] int64 + fixed-point
 //       decode float32(int64)/10^prec (PySyft 0.2.9 semantics)
 //
-// Design (DESIGN.md "Kernels"): every kernel is a single streaming pass over a row-major
-// [rows][ld] slab held in HBM.  Parallelism is over the PARAMETER axis only: one lane owns a
-// 16-byte column (4 fp32 or 2 int64) and walks the client rows in index order, so the fp32
-// fold order is exactly the reference's left fold (bit-exact, no tree/shuffle reordering).
-// A wave reads 1 KiB contiguous per row; U rows are issued before they are consumed to keep
-// U x 1 KiB per wave in flight.  No LDS: there is no reuse to stage, and no MFMA: this is a
+// Design (DESIGN.md "Kernels"): every kernel is a single streaming pass over the slab held in
+// HBM, column-blocked (SlabMap in pgh_kernels.h: blocks of ld columns, each block all rows,
+// so a lane's walk down the client rows stays inside one compact block).  Parallelism is over
+// the PARAMETER axis only: one lane owns a column (1 or 4 fp32, 1 or 2 int64) and walks the
+// client rows in index order, so the fp32 fold order is exactly the reference's left fold
+// (bit-exact, no tree/shuffle reordering).  U rows are issued before they are consumed to keep
+// U loads per lane in flight.  No LDS: there is no reuse to stage, and no MFMA: this is a
 // 0.25 flop/byte reduction, bound by HBM bandwidth.
 //
 // Build flags matter for parity: -ffp-contract=off (no a*k+d -> FMA), no fast-math, f32
@@ -112,12 +113,16 @@ __device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, 
     using L = Lane<VEC>;
     using T = typename L::T;
     const int n = a.n_rows;
+    const int64_t ld = a.map.ld;
+    const float* col[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) col[w] = a.diffs + a.map.at(VEC * (q0 + w * qstep));
     T acc[W];
     int r;
     if (a.flags & FL_FIRST) {
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            acc[w] = L::template load<NT>(a.diffs + VEC * (q0 + w * qstep));  // fold starts at d0, not 0
+            acc[w] = L::template load<NT>(col[w]);  // fold starts at d0, not 0
             if constexpr (MODE == MODE_WEIGHTED) acc[w] = acc[w] * a.weights[0];
         }
         r = 1;
@@ -132,7 +137,7 @@ __device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, 
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int w = 0; w < W; ++w)
-                v[u][w] = L::template load<NT>(a.diffs + (size_t)(r + u) * a.ld + VEC * (q0 + w * qstep));
+                v[u][w] = L::template load<NT>(col[w] + (size_t)(r + u) * ld);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -141,8 +146,7 @@ __device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, 
     for (; r < n; ++r)
 #pragma unroll
         for (int w = 0; w < W; ++w)
-            acc[w] = fold<MODE>(acc[w], L::template load<NT>(a.diffs + (size_t)r * a.ld + VEC * (q0 + w * qstep)),
-                                a.client0 + r, a.weights, r);
+            acc[w] = fold<MODE>(acc[w], L::template load<NT>(col[w] + (size_t)r * ld), a.client0 + r, a.weights, r);
 #pragma unroll
     for (int w = 0; w < W; ++w) {
         const int64_t q = q0 + w * qstep;
@@ -201,9 +205,10 @@ __global__ __launch_bounds__(TB) void k_secagg(SecaggArgs a, int64_t ncol) {
     using L = Lane64<VEC>;
     using T = typename L::T;
     const int64_t stride = (int64_t)gridDim.x * TB;
+    const int64_t ld = a.map.ld;
     for (int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x; q < ncol; q += stride) {
-        const int64_t* col = a.shares + VEC * q;
         const int64_t i = VEC * q;
+        const int64_t* col = a.shares + a.map.at(i);
         const int ne = (int)(i + VEC <= a.p ? VEC : a.p - i);  // valid elements of this column
         T acc{};
         if (!(a.flags & FL_FIRST))
@@ -212,11 +217,11 @@ __global__ __launch_bounds__(TB) void k_secagg(SecaggArgs a, int64_t ncol) {
         for (; r + U <= a.n_rows; r += U) {
             T v[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = L::template load<NT>(col + (size_t)(r + u) * a.ld);
+            for (int u = 0; u < U; ++u) v[u] = L::template load<NT>(col + (size_t)(r + u) * ld);
 #pragma unroll
             for (int u = 0; u < U; ++u) acc += v[u];  // wraps mod 2^64
         }
-        for (; r < a.n_rows; ++r) acc += L::template load<NT>(col + (size_t)r * a.ld);
+        for (; r < a.n_rows; ++r) acc += L::template load<NT>(col + (size_t)r * ld);
         for (int e = 0; e < ne; ++e) {
             const unsigned long long x = lane_elem<VEC>(acc, e);
             if (a.flags & FL_FINAL) {
@@ -229,33 +234,31 @@ __global__ __launch_bounds__(TB) void k_secagg(SecaggArgs a, int64_t ncol) {
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_synth_f32(float* out, int64_t ld, int64_t p, uint64_t seed,
-                                                     uint64_t stream_id, int64_t row0, int64_t idx0,
-                                                     float scale) {
+__global__ __launch_bounds__(BLOCK) void k_synth_f32(float* out, SlabMap m, int64_t ncols, int64_t p, uint64_t seed,
+                                                     uint64_t stream_id, int64_t row0, int64_t idx0, float scale) {
     const int64_t r = blockIdx.y;
     const uint64_t key = row_key(seed, stream_id, (uint64_t)(row0 + r));
-    float* row = out + (size_t)r * ld;
-    const int64_t ncol = ld / 4;
-    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < ncol; q += (int64_t)gridDim.x * BLOCK) {
+    float* row = out + (size_t)r * m.ld;
+    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < ncols / 4; q += (int64_t)gridDim.x * BLOCK) {
         f32x4 v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int64_t i = 4 * q + e;
             v[e] = (i < p) ? bits_to_f32(sm64(key + (uint64_t)(idx0 + i)), scale) : 0.f;
         }
-        *reinterpret_cast<f32x4*>(row + 4 * q) = v;
+        *reinterpret_cast<f32x4*>(row + m.at(4 * q)) = v;  // 4 params never straddle a block
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_synth_shares(int64_t* out, int n_parties, int64_t ld, int64_t p,
-                                                        uint64_t seed, int64_t client0, int64_t idx0,
+__global__ __launch_bounds__(BLOCK) void k_synth_shares(int64_t* out, SlabMap m, int64_t ncols, int n_parties,
+                                                        int64_t p, uint64_t seed, int64_t client0, int64_t idx0,
                                                         float enc_scale) {
     const int64_t c = blockIdx.y;
     const uint64_t kx = row_key(seed, STREAM_SECRET, (uint64_t)(client0 + c));
-    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < ld; i += (int64_t)gridDim.x * BLOCK) {
-        int64_t* dst = out + (size_t)(c * n_parties) * ld + i;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < ncols; i += (int64_t)gridDim.x * BLOCK) {
+        int64_t* dst = out + (size_t)(c * n_parties) * m.ld + m.at(i);
         if (i >= p) {
-            for (int s = 0; s < n_parties; ++s) dst[(size_t)s * ld] = 0;
+            for (int s = 0; s < n_parties; ++s) dst[(size_t)s * m.ld] = 0;
             continue;
         }
         const uint64_t g = (uint64_t)(idx0 + i);
@@ -265,10 +268,10 @@ __global__ __launch_bounds__(BLOCK) void k_synth_shares(int64_t* out, int n_part
         uint64_t acc = 0;
         for (int s = 0; s < n_parties - 1; ++s) {
             const uint64_t sh = sm64(row_key(seed, STREAM_SHARE, (uint64_t)((client0 + c) * n_parties + s)) + g);
-            dst[(size_t)s * ld] = (int64_t)sh;
+            dst[(size_t)s * m.ld] = (int64_t)sh;
             acc += sh;
         }
-        dst[(size_t)(n_parties - 1) * ld] = (int64_t)(enc - acc);
+        dst[(size_t)(n_parties - 1) * m.ld] = (int64_t)(enc - acc);
     }
 }
 
@@ -286,13 +289,13 @@ int cu_count() {
 
 // Variants (A/B in one process: tools/ab_variants.py; profiles/r01*/README.md).
 //   id  loads  U (rows in flight)  W (cols/lane)  block  VEC (params/col)  grid
-//   0   nt     8                   1              256    4                 one lane per column
+//   0   nt     8                   1              256    4                 one lane per column  <- big shards
 //   1   nt     8                   1              256    4                 persistent, 4 blocks/CU
 //   2   plain  8                   1              256    4                 one lane per column
 //   3   plain  8                   1              256    4                 persistent
 //   4   plain  16                  1              256    4                 one lane per column
 //   5   plain  16                  1              256    4                 persistent
-//   6   nt     16                  1              256    4                 one lane per column  <- big shards
+//   6   nt     16                  1              256    4                 one lane per column
 //   7   nt     4                   2              256    4                 one lane per W columns
 //   8   nt     8                   2              256    4                 one lane per W columns
 //   9   nt     8                   1              512    4                 one lane per column
@@ -305,9 +308,9 @@ int cu_count() {
 //   16  nt     48                  1              64     1                 one lane per param
 //   17  nt     64                  1              64     1                 one lane per param
 //   18  nt     32                  1              128    1                 one lane per param
-// nt loads won 2-5 % on the once-read diff stream; among nt variants at ResNet-18 size the spread
-// is < 1 % (r01c).  Small shards are bound by lanes / CU balance, not by the loads: the auto
-// choice (PGH_VARIANT_AUTO) picks by shard size (auto_variant below, r01g measurements).
+// nt loads won 2-5 % on the once-read diff stream (r01c).  Small shards are bound by lanes / CU
+// balance, not by the loads: the auto choice (variant -1) picks by shard size and mode
+// (auto_variant below, r01l measurements on the column-blocked slab).
 constexpr int N_VARIANTS = 19;
 constexpr int SECAGG_AUTO_VARIANT = 14;
 
@@ -353,20 +356,23 @@ hipError_t dispatch_fedavg(const FedavgArgs& a, int variant, hipStream_t s) {
 
 }  // namespace
 
-// Measured on MI355X (r01g, tools/small_p2.sh / tools/big_p.sh; GB/s of algorithmic bytes):
-//   P = 50K x 60K clients: v14 6088, v12 4013, v11 3984, v6 2644
-//   P = 100K x 30K:        v12 6754, v11 6609, v14 6597, v6 4817
-//   P = 311,650 x 10K:     v11 6963, v14 6616, v12 6564, v6 5604
-//   P = 1M x 3K:           v11 6789, v12 6754, v14 6735, v6 6758
-//   P = 11.69M x 1K:       mean v14 6685 / v12 6679 / v11 6645 / v6 6559;
-//                          iterative v11 6603 / v14 6561 / v6 6516
-// Small shards need more, smaller workgroups (CU balance) and, below ~200K params, one param per
-// lane (lanes); large shards are within 1-2 % of each other, 64-thread blocks ahead.
+// Measured on MI355X, column-blocked slab (r01l, tools/sweep_r01l.sh; GB/s of algorithmic bytes):
+//   P = 11.69M x 1K:     mean v0 6930 / v6 6921 / v15 6882 / v11 6861 / v14 6576
+//                        iterative v0 6845 / v6 6828 / v15 6817;  weighted v15 7035 / v0 6921
+//   P = 3M x 1K:         mean v6 6829 / v0 6822 / v15 6773;  iterative v6 6619 / v0 6615
+//   P = 1M x 3K:         mean v0 6921 / v6 6912 / v11 6769;  iterative v0 6753 / v6 6555
+//   P = 311,650 x 10K:   mean v11 6885 / v15 6645 / v0 5753;  iterative v12 5711 / v14 5670 / v11 5351
+//   P = 100K x 30K:      mean v11 6403 / v12 6251;  iterative v14 4742 / v12 4465 / v11 2784
+//   single block (P < 65,536; layout unchanged from r01g): P = 50K x 60K v14 6088 / v12 4013
+// Big shards: 16-byte columns in 256-thread blocks (the blocked slab made them 5 % faster than one
+// param per lane).  Below ~786K params those give < 768 workgroups for 256 CUs, so 64-thread
+// blocks (CU balance) and, for the ALU-heavier iterative fold, one param per lane (lanes).
 int auto_variant(int64_t p, int mode) {
     if (p < 80000) return 14;
-    if (p < 200000) return 12;
-    if (p < 2000000) return 11;
-    return mode == MODE_ITERATIVE ? 11 : 14;
+    if (p < 200000) return mode == MODE_ITERATIVE ? 14 : 11;
+    if (p < 786432) return mode == MODE_ITERATIVE ? 12 : 11;
+    if (p < 2000000) return 0;
+    return mode == MODE_WEIGHTED ? 15 : 0;
 }
 
 template <int U, bool NT, int TB, int VEC>
@@ -376,8 +382,17 @@ hipError_t go_secagg(const SecaggArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Geometry a kernel may rely on: rows 16-byte aligned (ld a multiple of 4), blocks
+// power-of-two wide (or one block holding the launch's columns), the launch's first column
+// 4-aligned so a 16-byte column never straddles a block.
+bool valid_map(const SlabMap& m, int64_t p) {
+    if (m.ld <= 0 || (m.ld & 3) || (m.off & 3) || m.off < 0) return false;
+    if (m.bshift == 62) return m.bmask == (int64_t(1) << 62) - 1 && m.off + p <= m.ld;
+    return m.bshift > 0 && m.bshift < 40 && (int64_t(1) << m.bshift) == m.ld && m.bmask == m.ld - 1 && m.bstride >= m.ld;
+}
+
 hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
-    if (a.p <= 0 || a.n_rows < 0 || a.ld < a.p || (a.ld & 3)) return hipErrorInvalidValue;
+    if (a.p <= 0 || a.n_rows < 0 || !valid_map(a.map, a.p)) return hipErrorInvalidValue;
     if ((a.flags & FL_FIRST) && a.n_rows < 1) return hipErrorInvalidValue;
     if (a.n_rows > 0 && (!a.diffs || (reinterpret_cast<uintptr_t>(a.diffs) & 15))) return hipErrorInvalidValue;
     if (!(a.flags & FL_FIRST) && (!a.acc || (reinterpret_cast<uintptr_t>(a.acc) & 15))) return hipErrorInvalidValue;
@@ -396,12 +411,12 @@ hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s) {
-    if (a.p <= 0 || a.n_rows < 0 || a.ld < a.p || (a.ld & 1)) return hipErrorInvalidValue;
+    if (a.p <= 0 || a.n_rows < 0 || !valid_map(a.map, a.p)) return hipErrorInvalidValue;
     if (a.n_rows > 0 && (!a.shares || (reinterpret_cast<uintptr_t>(a.shares) & 15))) return hipErrorInvalidValue;
     if (!(a.flags & FL_FINAL) && !a.acc) return hipErrorInvalidValue;
     if (!(a.flags & FL_FIRST) && !a.acc) return hipErrorInvalidValue;
-    // auto: one int64 per lane, 32 rows in flight, 64-thread blocks (r01i: 6407 GB/s at
-    // ResNet-18 x 250 x 2, 6862 at 311,650 x 2,500 x 2; 16-byte columns 6377 / 6769)
+    // auto: one int64 per lane, 32 rows in flight, 64-thread blocks (r01l, blocked slab: 6878 GB/s
+    // at ResNet-18 x 1,000 x 2 (v16 6886, 16-byte columns v0 6613), 6747 at 311,650 x 2,500 x 2)
     const int v = a.variant < 0 ? SECAGG_AUTO_VARIANT : a.variant;
     if (v >= N_VARIANTS) return hipErrorInvalidValue;
     switch (v) {  // same load policy / depth / block / lane width as the fedavg variant of that id
@@ -429,26 +444,30 @@ hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s) {
     }
 }
 
-hipError_t launch_synth_f32(float* out, int n_rows, int64_t ld, int64_t p, uint64_t seed, uint64_t stream_id,
-                            int64_t row0, int64_t idx0, float scale, hipStream_t s) {
-    if (!out || n_rows < 0 || n_rows > 65535 || ld < p || (ld & 3) || (reinterpret_cast<uintptr_t>(out) & 15))
+hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_rows, int64_t p, uint64_t seed,
+                            uint64_t stream_id, int64_t row0, int64_t idx0, float scale, hipStream_t s) {
+    if (!out || n_rows < 0 || n_rows > 65535 || ncols < p || (ncols & 3) || m.off != 0 || !valid_map(m, 0) ||
+        (m.bshift == 62 && ncols > m.ld) || (reinterpret_cast<uintptr_t>(out) & 15))
         return hipErrorInvalidValue;
-    if (n_rows == 0 || ld == 0) return hipSuccess;
-    const int64_t ncol = ld / 4;
-    int64_t gx = (ncol + BLOCK - 1) / BLOCK;
+    if (n_rows == 0 || ncols == 0) return hipSuccess;
+    int64_t gx = (ncols / 4 + BLOCK - 1) / BLOCK;
     if (gx > 1024) gx = 1024;
-    k_synth_f32<<<dim3((unsigned)gx, (unsigned)n_rows), BLOCK, 0, s>>>(out, ld, p, seed, stream_id, row0, idx0, scale);
+    k_synth_f32<<<dim3((unsigned)gx, (unsigned)n_rows), BLOCK, 0, s>>>(out, m, ncols, p, seed, stream_id, row0, idx0,
+                                                                      scale);
     return hipGetLastError();
 }
 
-hipError_t launch_synth_shares(int64_t* out, int n_clients, int n_parties, int64_t ld, int64_t p, uint64_t seed,
-                               int64_t client0, int64_t idx0, float enc_scale, hipStream_t s) {
-    if (!out || n_clients < 0 || n_clients > 65535 || n_parties < 1 || ld < p) return hipErrorInvalidValue;
-    if (n_clients == 0 || ld == 0) return hipSuccess;
-    int64_t gx = (ld + BLOCK - 1) / BLOCK;
+hipError_t launch_synth_shares(int64_t* out, const SlabMap& m, int64_t ncols, int n_clients, int n_parties,
+                               int64_t p, uint64_t seed, int64_t client0, int64_t idx0, float enc_scale,
+                               hipStream_t s) {
+    if (!out || n_clients < 0 || n_clients > 65535 || n_parties < 1 || ncols < p || m.off != 0 || !valid_map(m, 0) ||
+        (m.bshift == 62 && ncols > m.ld))
+        return hipErrorInvalidValue;
+    if (n_clients == 0 || ncols == 0) return hipSuccess;
+    int64_t gx = (ncols + BLOCK - 1) / BLOCK;
     if (gx > 1024) gx = 1024;
-    k_synth_shares<<<dim3((unsigned)gx, (unsigned)n_clients), BLOCK, 0, s>>>(out, n_parties, ld, p, seed, client0,
-                                                                            idx0, enc_scale);
+    k_synth_shares<<<dim3((unsigned)gx, (unsigned)n_clients), BLOCK, 0, s>>>(out, m, ncols, n_parties, p, seed,
+                                                                            client0, idx0, enc_scale);
     return hipGetLastError();
 }
 

@@ -262,8 +262,11 @@ class Engine:
     def reset_stats(self):
         self._check(self._lib.pgh_reset_stats(self._h), "reset_stats")
 
-    def slab(self) -> Tuple[int, int]:
+    def slab(self) -> Tuple[int, int, int]:
+        """(device pointer, ld, block_pitch): element (row r, shard param i) is at
+        ``(i // ld) * block_pitch + r * ld + i % ld`` (include/pgh_api.h)."""
         p = C.c_void_p()
         ld = C.c_int64()
-        self._check(self._lib.pgh_slab(self._h, C.byref(p), C.byref(ld)), "slab")
-        return p.value or 0, ld.value
+        bp = C.c_int64()
+        self._check(self._lib.pgh_slab(self._h, C.byref(p), C.byref(ld), C.byref(bp)), "slab")
+        return p.value or 0, ld.value, bp.value

@@ -115,8 +115,85 @@ def test_mnist_golden_device_generator(engine, gold):
     torch.cuda.synchronize()
     assert sha(ck.cpu().numpy()) == g["sha256_ckpt"]
     assert sha(out.cpu().numpy()) == g["sha256_mean"]
-    ptr, ld = engine.slab()
-    assert ptr and ld % 64 == 0
+
+
+def _slab_host(engine, rows, dtype):
+    """The whole slab copied to the host (hipMemcpy through the HIP runtime the library links)."""
+    import ctypes
+
+    ptr, ld, bp = engine.slab()
+    nb = 1 if bp == 0 else -(-engine.stats()["p_shard"] // ld)
+    n = (nb - 1) * bp + rows * ld if bp else rows * ld
+    host = np.empty(n, dtype)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipDeviceSynchronize()
+    rc = hip.hipMemcpy(ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(ptr), ctypes.c_size_t(host.nbytes), 2)
+    assert rc == 0
+    return host, ld, bp
+
+
+@pytest.mark.parametrize("P,N,parties", [(200_003, 3, 1), (311_650, 2, 1), (100_003, 2, 2), (1_000, 4, 1)])
+def test_slab_layout(engine, P, N, parties):
+    """Element (row r, param i) sits at (i // ld) * block_pitch + r * ld + i % ld (pgh_api.h)."""
+    i = np.arange(P)
+    if parties == 1:
+        engine.set_layout([P])
+        engine.reserve(N)
+        for c in range(N):
+            engine.ingest(c, (c * 1_000_000 + i).astype(F))  # exact in fp32 (< 2^24)
+        host, ld, bp = _slab_host(engine, N, np.float32)
+    else:
+        engine.set_layout([P])
+        engine.reserve(N, 1, parties)
+        for c in range(N):
+            engine.ingest(c, np.stack([(c * parties + s) * 10**9 + i for s in range(parties)]).astype(np.int64))
+        host, ld, bp = _slab_host(engine, N * parties, np.int64)
+    assert ld % 64 == 0 and (bp == 0 or (ld & (ld - 1)) == 0)
+    if P > 70_000:
+        assert bp > 0, "shards wider than one 256 KiB block must be column-blocked"
+    for r in range(N * parties):
+        got = host[(i // ld) * bp + r * ld + i % ld]
+        want = (r * 1_000_000 + i) if parties == 1 else (r * 10**9 + i)
+        assert np.array_equal(got, np.asarray(want, got.dtype)), r
+
+
+def test_blocked_equals_row_major(gold):
+    """PGH_BLOCK_BYTES=0 (one block: plain row-major rows) and the blocked default agree bit for
+    bit, for every mode and a range-split fold."""
+    import os
+
+    import torch
+
+    from pygrid_amd import Engine
+
+    rng = np.random.default_rng(5)
+    P, N = 300_001, 7
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    w = rng.uniform(0.5, 2.0, N).astype(F)
+    outs = []
+    for bb in ("0", None):
+        if bb is None:
+            os.environ.pop("PGH_BLOCK_BYTES", None)
+        else:
+            os.environ["PGH_BLOCK_BYTES"] = bb
+        try:
+            with Engine(0) as eng:
+                res = [run_f32(eng, d, c, m, w if m == 2 else None) for m in (0, 1, 2)]
+                ck = torch.from_numpy(c).cuda()
+                out = torch.empty_like(ck)
+                for off in range(0, P, 65_536 + 4):  # ranges straddling block edges
+                    eng.fedavg_device_range(0, off, min(65_540, P - off), ck.data_ptr(), out.data_ptr())
+                torch.cuda.synchronize()
+                res.append(out.cpu().numpy())
+                outs.append((res, eng.slab()[2]))
+        finally:
+            os.environ.pop("PGH_BLOCK_BYTES", None)
+    (rm, bp0), (bl, bp1) = outs
+    assert bp0 == 0 and bp1 > 0
+    for a, b in zip(rm, bl):
+        assert same(a, b)
+    assert same(bl[0], coracle.fedavg(0, d, c)) and same(bl[3], bl[0])
 
 
 def test_smpc_vectors(engine, gold):
