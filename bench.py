@@ -20,6 +20,9 @@ Other BASELINE configs (--workload), each printed as its own JSON line of the sa
   mnist-state            config 1: 3 clients' State protobuf bytes -> new checkpoint bytes
   resnet18-state         ResNet-18 (62 tensors) x 100 clients, State bytes on the host -> new
                          checkpoint bytes: the whole cycle close a node runs (PCIe-inclusive)
+  resnet18-report        the same cycle with report-time aggregation: each
+                         State diff is folded into HBM as it is reported, the checkpoint uploaded
+                         at cycle start; reports the cycle close latency after the last report
 """
 from __future__ import annotations
 
@@ -46,6 +49,7 @@ WORKLOADS = {
     "c5-ingest": (1, 0, 64, 1, 125_000_000),
     "mnist-state": (0, 0, 3, 1, 311_650),
     "resnet18-state": (0, 0, 100, 1, RESNET18_P),
+    "resnet18-report": (0, 0, 100, 1, RESNET18_P),
 }
 
 
@@ -421,6 +425,62 @@ def run_resnet18_state(ctx, args, eng, N):
                   roofline_of(st, "resnet18-state", eng.effective_variant(), "k_fedavg"), extra)
 
 
+def run_resnet18_report(ctx, args, eng, N):
+    """Report-time aggregation (pygrid_amd.incremental.IncrementalCycle): per step one cycle of N
+    reports (State bytes in host memory, in assignment order) folded through a 16-slot HBM ring as
+    they arrive, then close.  `value` is PCIe-inclusive like resnet18-state; `close_ms_after_last_
+    report` is what the node waits for once the last diff is in (cycle_manager.py:180-217)."""
+    import numpy as np
+
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast
+    from pygrid_amd.workloads import RESNET18_SHAPES
+
+    rng = np.random.default_rng(args.seed)
+    numel = [int(np.prod(s)) for s in RESNET18_SHAPES]
+    ck_pb = build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in RESNET18_SHAPES])
+    distinct = [build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2)
+                                  for s in RESNET18_SHAPES]) for _ in range(4)]
+    ring, batch = args.ring or 16, 4
+    closes = []
+
+    def cycle():
+        inc = IncrementalCycle(eng, numel, ring_slots=ring, fold_batch=batch, checkpoint=ck_pb)
+        for w in range(N):
+            inc.assigned(w)
+        for w in range(N):
+            inc.reported(w, distinct[w % 4])
+        t0 = time.perf_counter()
+        new = inc.close(ck_pb)
+        closes.append((time.perf_counter() - t0) * 1e3)
+        return new
+
+    for _ in range(args.warmup):
+        cycle()
+    closes.clear()
+    eng.reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        new = cycle()
+    el = time.perf_counter() - t0
+    st = eng.stats()
+    P = RESNET18_P
+    value = 4 * N * P * args.steps / el / 1e9
+    cfg = {"workload": f"resnet18-report: ResNet-18 (62 tensors, P={P}) x {N} clients, each State diff folded into HBM "
+                       f"as it is reported ({ring}-slot ring, fold batch {batch}), checkpoint uploaded at cycle start, "
+                       "close = last partial fold + new checkpoint bytes patched from HBM",
+           "clients": N, "params_per_gpu": P, "params_total": P, "parallelism": "single GPU",
+           "kernel_variant": eng.effective_variant()}
+    extra = {"close_ms_after_last_report": round(float(np.median(closes)), 3),
+             "close_ms_after_last_report_all": [round(c, 3) for c in closes],
+             "h2d_GBps": round(st["h2d_bytes_total"] / (st["h2d_ms_total"] / 1e3) / 1e9, 2) if st["h2d_ms_total"] else None,
+             "new_checkpoint_bytes": len(new),
+             "note": "PCIe-inclusive whole cycle (reports + close); compare close_ms_after_last_report with "
+                     "resnet18-state's cycle_close_ms (all diffs folded at close)"}
+    return record(ctx, args, "resnet18-report", value, el, "f32", cfg,
+                  roofline_of(st, "resnet18-report", eng.effective_variant(), "k_fedavg"), extra)
+
+
 def main():
     args = parse()
     ctx = Ctx(args)
@@ -445,6 +505,8 @@ def main():
         rec = run_mnist_state(ctx, args, eng)
     elif args.workload == "resnet18-state":
         rec = run_resnet18_state(ctx, args, eng, N)
+    elif args.workload == "resnet18-report":
+        rec = run_resnet18_report(ctx, args, eng, N)
     else:
         rec = run_resident(ctx, args, eng, mode, dtype, N, parties, hi - lo, P, lo, hi)
     if ctx.rank == 0:

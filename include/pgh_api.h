@@ -151,6 +151,10 @@ int pgh_stream_flush(pgh_ctx* ctx);               /* fold the ready run now */
 /* Fold what is left and write out = ckpt - avg (all clients [0, n) must have arrived). */
 int pgh_stream_finish(pgh_ctx* ctx, const float* ckpt, float* out);
 int pgh_stream_finish_device(pgh_ctx* ctx, const float* d_ckpt, float* d_out, void* stream);
+/* Finish into the resident checkpoint (pgh_ckpt_upload / pgh_ckpt_upload_state, possibly uploaded
+ * while clients were still arriving): afterwards it IS the new checkpoint, ready for
+ * pgh_ckpt_patch_state / pgh_ckpt_download and the next cycle. */
+int pgh_stream_finish_resident(pgh_ctx* ctx);
 int pgh_stream_finish_secagg(pgh_ctx* ctx, int base, int prec, int64_t* sum_out, float* dec_out);
 int pgh_stream_finish_secagg_device(pgh_ctx* ctx, int base, int prec, int64_t* d_sum, float* d_dec, void* stream);
 

@@ -1189,7 +1189,19 @@ int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out
     std::vector<std::pair<size_t, size_t>> spans;
     RC(state_shard_spans(c, tmpl, n, &spans, "checkpoint template"));
     DeviceGuard g(c->device);
-    if (out != tmpl) c->pool_copy->run({CopyPool::Seg{out, tmpl, n}});
+    if (out != tmpl) {  // template bytes outside this shard's payload slices (framing, other shards)
+        std::vector<CopyPool::Seg> gaps;
+        size_t pos = 0;
+        bool ordered = true;
+        for (auto& sp : spans) {
+            ordered = ordered && sp.first >= pos;
+            if (sp.first > pos) gaps.push_back({out + pos, tmpl + pos, sp.first - pos});
+            pos = sp.first + sp.second;
+        }
+        if (n > pos) gaps.push_back({out + pos, tmpl + pos, n - pos});
+        if (!ordered) gaps.assign(1, CopyPool::Seg{out, tmpl, n});
+        c->pool_copy->run(gaps);
+    }
     std::vector<OutPiece> pieces;
     for (auto& sp : spans) pieces.push_back(OutPiece{out + sp.first, sp.second});
     RC(order_after_ingest(c, c->stream));
@@ -1273,6 +1285,16 @@ int pgh_stream_finish_device(pgh_ctx* c, const float* d_ckpt, float* d_out, void
     fa.ckpt = d_ckpt;
     fa.out = d_out;
     return stream_finish(c, fa, (hipStream_t)stream, true, c->kind);
+}
+
+int pgh_stream_finish_resident(pgh_ctx* c) {
+    RC(check_dtype(c, PGH_F32));
+    DeviceGuard g(c->device);
+    const double t0 = now_ms();
+    RC(pgh_stream_finish_device(c, c->d_ckpt, c->d_out, c->stream));
+    std::swap(c->d_ckpt, c->d_out);  // the new checkpoint is the next cycle's input
+    c->st.close_ms_last = now_ms() - t0;
+    return PGH_OK;
 }
 
 int pgh_stream_finish(pgh_ctx* c, const float* ckpt, float* out) {

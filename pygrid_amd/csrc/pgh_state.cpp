@@ -254,12 +254,23 @@ int pgh_state_patch(const uint8_t* tmpl, size_t n, const float* values, int64_t 
     int64_t total = 0;
     for (auto& s : spans) total += s.count;
     if (total != n_values) return PGH_E_ARG;
-    if (out != tmpl) std::memcpy(out, tmpl, n);
+    // Spans in message order and disjoint (the walker's output for any well-formed State): copy
+    // the template bytes between them (the framing) and the new payloads into them, every output
+    // byte written once.  Anything else: copy the whole template first.
+    bool ordered = true;
+    for (size_t t = 1; t < spans.size(); ++t)
+        ordered = ordered && spans[t].offset >= spans[t - 1].offset + 4 * (size_t)spans[t - 1].count;
+    if (!ordered && out != tmpl) std::memcpy(out, tmpl, n);
+    if (!ordered) tmpl = out;  // framing already in place
+    size_t pos = 0;
     int64_t off = 0;
     for (auto& s : spans) {
+        if (out != tmpl && s.offset > pos) std::memcpy(out + pos, tmpl + pos, s.offset - pos);
         std::memcpy(out + s.offset, values + off, 4 * (size_t)s.count);
         off += s.count;
+        pos = s.offset + 4 * (size_t)s.count;
     }
+    if (out != tmpl && n > pos) std::memcpy(out + pos, tmpl + pos, n - pos);
     return PGH_OK;
 }
 

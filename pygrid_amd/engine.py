@@ -75,6 +75,7 @@ class Engine:
         self.hi = 0
         self.dtype = F32
         self.parties = 1
+        self.max_clients = 0
 
     # ---- plumbing ----------------------------------------------------------------------------
     def _check(self, rc: int, what: str):
@@ -111,15 +112,18 @@ class Engine:
         self.numel = tuple(int(n) for n in numel)
         self.P = sum(self.numel)
         self.lo, self.hi = 0, self.P
+        self.max_clients = 0  # the slab was freed
 
     def set_shard(self, lo: int, hi: int):
         self._check(self._lib.pgh_set_shard(self._h, int(lo), int(hi)), "set_shard")
         self.lo, self.hi = int(lo), int(hi)
+        self.max_clients = 0
 
     def reserve(self, max_clients: int, dtype: int = F32, n_parties: int = 1):
         self._check(self._lib.pgh_reserve(self._h, int(max_clients), int(dtype), int(n_parties)), "reserve")
         self.dtype = dtype
         self.parties = 1 if dtype == F32 else int(n_parties)
+        self.max_clients = int(max_clients)
 
     def reset(self):
         self._check(self._lib.pgh_reset(self._h), "reset")
@@ -187,9 +191,9 @@ class Engine:
 
     def ckpt_patch_state(self, template: bytes) -> bytes:
         """``template`` (State bytes) with this shard's payload slices taken from the resident checkpoint."""
-        out = C.create_string_buffer(len(template))
-        self._check(self._lib.pgh_ckpt_patch_state(self._h, template, len(template), out), "ckpt_patch_state")
-        return out.raw
+        out, ptr = _lib.fresh_bytes(len(template))  # the library copies the template in, then patches
+        self._check(self._lib.pgh_ckpt_patch_state(self._h, template, len(template), ptr), "ckpt_patch_state")
+        return out
 
     def secagg(self, base: int = 10, prec: int = 3, want_sum: bool = True,
                want_dec: bool = True) -> Tuple[Optional[np.ndarray], Optional[np.ndarray]]:
@@ -226,6 +230,11 @@ class Engine:
     def stream_finish_device(self, d_ckpt: int, d_out: int, stream: int = 0):
         self._check(self._lib.pgh_stream_finish_device(self._h, C.c_void_p(d_ckpt), C.c_void_p(d_out),
                                                        C.c_void_p(stream or None)), "stream_finish_device")
+
+    def stream_finish_resident(self):
+        """Finish the stream into the resident checkpoint (``ckpt_upload*`` earlier, possibly while
+        clients were still arriving): afterwards it IS the new checkpoint."""
+        self._check(self._lib.pgh_stream_finish_resident(self._h), "stream_finish_resident")
 
     def stream_finish_secagg(self, base: int = 10, prec: int = 3):
         s = np.empty(self.p_shard, dtype=np.int64)

@@ -13,11 +13,6 @@ import ctypes as C
 from . import _lib
 
 
-_new_bytes = C.pythonapi.PyBytes_FromStringAndSize
-_new_bytes.restype = C.py_object
-_new_bytes.argtypes = [C.c_void_p, C.c_ssize_t]
-
-
 def b64decode(s, threads: int = 0) -> bytes:
     if isinstance(s, str):
         s = s.encode("ascii")
@@ -27,9 +22,8 @@ def b64decode(s, threads: int = 0) -> bytes:
     n = C.c_size_t(0)
     if lib.pgh_b64_decode(s, len(s), None, C.byref(n), int(threads)) != 0:  # validate + exact size
         raise binascii.Error("Incorrect padding")
-    out = _new_bytes(None, n.value)  # fresh, unshared bytes object: decoded into in place
+    out, dst = _lib.fresh_bytes(n.value)  # fresh, unshared bytes object: decoded into in place
     if n.value:
-        dst = C.cast(C.c_char_p(out), C.c_void_p)
         if lib.pgh_b64_decode(s, len(s), dst, C.byref(n), int(threads)) != 0:
             raise binascii.Error("Incorrect padding")
     return out

@@ -63,9 +63,9 @@ def serialize_model_params(template: bytes, values: np.ndarray) -> bytes:
     """New State bytes: ``template`` with all payloads replaced by ``values`` (P floats)."""
     lib = _lib.load()
     v = np.ascontiguousarray(values, dtype="<f4").reshape(-1)
-    out = C.create_string_buffer(len(template))
-    rc = lib.pgh_state_patch(template, len(template), v.ctypes.data, v.size, out)
+    out, ptr = _lib.fresh_bytes(len(template))  # pgh_state_patch writes all n bytes (copy + patch)
+    rc = lib.pgh_state_patch(template, len(template), v.ctypes.data, v.size, ptr)
     if rc != 0:
         raise StateParseError(f"cannot patch State ({_lib.STATUS_NAMES.get(rc, rc)}): "
                               f"{v.size} values for this checkpoint?", status=rc)
-    return out.raw
+    return out

@@ -28,9 +28,15 @@ class RecordingEngine:
     def ingest_state(self, k, pb):
         self.calls.append(("ingest", k, pb))
 
-    def stream_finish(self, ckpt):
+    def ckpt_upload_state(self, pb):
+        self.calls.append(("upload", pb))
+
+    def stream_finish_resident(self):
         self.calls.append(("finish",))
-        return np.asarray(ckpt, np.float32)
+
+    def ckpt_patch_state(self, pb):
+        self.calls.append(("patch", pb))
+        return pb
 
 
 def ingests(eng):
@@ -73,9 +79,21 @@ def test_close_drops_non_reporters_and_keeps_id_order():
         inc.reported(w, bytes([w]))
     assert ingests(eng) == []            # worker 0 never reports
     ck = build_state_fast([np.array([1.0, 2.0, 3.0], np.float32)])
-    inc.close(ck)
+    assert inc.close(ck) == ck
     assert ingests(eng) == [(0, b"\x01"), (1, b"\x02"), (2, b"\x04"), (3, b"\x05")]
     assert inc.n_folded == 4 and inc.folded_early == 0
+    assert [c[0] for c in eng.calls[-3:]] == ["upload", "finish", "patch"]
+
+
+def test_checkpoint_handed_over_at_start_is_uploaded_once():
+    eng = RecordingEngine()
+    inc = IncrementalCycle(eng, [3], checkpoint=b"ck")
+    assert eng.calls[-1] == ("upload", b"ck")  # before any report: the upload overlaps the cycle
+    inc.assigned("a")
+    inc.reported("a", b"a")
+    assert inc.close(b"ck") == b"ck"
+    assert [c[0] for c in eng.calls].count("upload") == 1
+    assert [c[0] for c in eng.calls[-2:]] == ["finish", "patch"]
 
 
 def test_weights_follow_fold_order():
