@@ -70,8 +70,15 @@ int main(int argc, char** argv) {
             }
             if (nt <= 8) {
                 std::vector<float> vals((size_t)total + 1, 1.0f);
-                std::vector<uint8_t> out(pb.size() ? pb.size() : 1);
+                std::vector<uint8_t> out(pb.size() ? pb.size() : 1, 0xCD);  // poison: every byte must be written
                 if (pgh_state_patch(buf, pb.size(), vals.data(), total, out.data()) != PGH_OK) { std::printf("patch failed\n"); return 3; }
+                std::vector<uint8_t> want(pb.begin(), pb.end());  // template, then payloads in span order
+                int64_t vo = 0;
+                for (int k = 0; k < nt; ++k) {
+                    std::memcpy(want.data() + offs[k], vals.data() + vo, 4 * (size_t)cnts[k]);
+                    vo += cnts[k];
+                }
+                if (!pb.empty() && std::memcmp(want.data(), out.data(), pb.size()) != 0) { std::printf("patch bytes differ\n"); return 5; }
             }
         } else {
             ++rejected;

@@ -251,6 +251,33 @@ def test_secagg_synthetic_sampled(engine, variant):
     assert np.array_equal(bits(got_d), bits(O.fix_prec_decode(want)))
 
 
+def test_secagg_config3_full_size_sampled(engine):
+    """BASELINE config 3: ResNet-18 (P = 11,689,512) x 1,000 clients x 2 parties int64 resident
+    (187.7 GB, 357 column blocks); sums and decodes bit-exact on sampled params incl. block edges."""
+    import torch
+
+    P, N, S, seed = 11_689_512, 1000, 2, 77
+    engine.set_layout([P])
+    engine.reserve(N, 1, S)
+    engine.synth_fill(seed, N)
+    s = torch.empty(P, dtype=torch.int64, device="cuda")
+    d = torch.empty(P, dtype=torch.float32, device="cuda")
+    engine.secagg_device(s.data_ptr(), d.data_ptr())
+    torch.cuda.synchronize()
+    _, ld, bp = engine.slab()
+    assert ld == 32768 and bp == N * S * ld
+    edges = np.array([k * ld + e for k in (1, 2, 178, 356) for e in (-2, -1, 0, 1)])
+    idx = np.unique(np.concatenate([np.arange(4), np.random.default_rng(3).integers(0, P, 1500), edges, [P - 1]]))
+    want = np.zeros(idx.size, np.uint64)
+    with np.errstate(over="ignore"):
+        for c in range(N):
+            want += O.secagg_sum(O.synth_shares(seed, c, S, idx.astype(np.uint64))[None]).view(np.uint64)
+    want = want.view(np.int64)
+    assert np.array_equal(s.cpu().numpy()[idx], want)
+    assert np.array_equal(bits(d.cpu().numpy()[idx]), bits(O.fix_prec_decode(want)))
+    engine.set_layout([1])  # release the 187 GB slab for the next test
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_resnet18_scale_sampled(engine, mode):
     """BASELINE config 2 shape (P = 11,689,512, N = 1,000) fully resident; bit-exact against the
@@ -270,7 +297,8 @@ def test_resnet18_scale_sampled(engine, mode):
     engine.fedavg_device(mode, ck.data_ptr(), out.data_ptr())
     torch.cuda.synchronize()
     rng = np.random.default_rng(mode)
-    idx = np.unique(np.concatenate([np.arange(8), rng.integers(0, P, 4088), [P - 1]])).astype(np.int64)
+    edges = np.array([k * 65536 + e for k in (1, 2, 89, 178) for e in (-4, -1, 0, 3)])  # 256 KiB blocks
+    idx = np.unique(np.concatenate([np.arange(8), rng.integers(0, P, 4072), edges, [P - 1]])).astype(np.int64)
     d = np.stack([O.synth_diff(seed, c, idx.astype(np.uint64)) for c in range(N)])
     c = O.synth_ckpt(seed, idx.astype(np.uint64))
     want = coracle.fedavg(mode, d, c, w if mode == 2 else None)
