@@ -70,27 +70,59 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(P: int, seed: int, budget_s: float, n: int = 32):
-    """The oracle's restatement of cycle_manager.py:276-296 (allocating float32 adds, one thread,
-    like the reference node's th.set_num_threads(1), main/__init__.py:8) on a bounded sample:
-    the same P-param shard, `n` synthetic clients, repeated until `budget_s` of CPU work."""
+def cpu_baseline(P: int, seed: int, budget_s: float, n: int = 32, all_cores: int = 16):
+    """The reference's hard-coded path as the node runs it -- cycle_manager.py:276-296 evaluated in
+    torch on CPU tensors (oracle.fedavg_mean_torch) at th.set_num_threads(1), the node's setting
+    (main/__init__.py:8) -- on a bounded sample: the same P-param shard, `n` synthetic clients,
+    repeated until `budget_s` of CPU work.  Also reported: the same at `all_cores` threads (the
+    GPU box's CPU share) and the numpy restatement (oracle.fedavg_mean) at 1 thread."""
+    import torch
+
     from oracle import coracle
     from oracle import oracle as O
 
     diffs = [[coracle.synth_f32(seed, O.STREAM_DIFF, c, 0, P, float(O.DIFF_SCALE))] for c in range(n)]
     ckpt = [coracle.synth_f32(seed, O.STREAM_CKPT, 0, 0, P, float(O.CKPT_SCALE))]
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        O.fedavg_mean(ckpt, diffs)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    gbs = reps * n * P * 4 / el / 1e9
+    tdiffs = [[torch.from_numpy(t) for t in d] for d in diffs]
+    tckpt = [torch.from_numpy(t) for t in ckpt]
+
+    def rate(fn, budget):
+        fn()  # warm: allocator, thread pool after set_num_threads
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return reps * n * P * 4 / el / 1e9, reps, el
+
+    threads = torch.get_num_threads()
+    try:
+        torch.set_num_threads(1)
+        gbs, reps, el = rate(lambda: O.fedavg_mean_torch(tckpt, tdiffs), budget_s * 0.5)
+        torch.set_num_threads(all_cores)
+        gbs_all, _, _ = rate(lambda: O.fedavg_mean_torch(tckpt, tdiffs), budget_s * 0.25)
+    finally:
+        torch.set_num_threads(threads)
+    gbs_np, _, _ = rate(lambda: O.fedavg_mean(ckpt, diffs), budget_s * 0.25)
     return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"oracle numpy restatement of cycle_manager.py:276-296, P={P}, {n} clients, "
-                      f"{reps} passes in {el:.1f}s, 1 thread",
-            "cycle_close_ms_per_1000_clients": round(el / reps / n * 1000 * 1000, 1)}
+            "sample": f"cycle_manager.py:276-296 in torch {torch.__version__} on CPU tensors "
+                      f"(oracle.fedavg_mean_torch), P={P}, {n} clients, {reps} passes in {el:.1f}s, 1 thread "
+                      f"(the node's th.set_num_threads(1))",
+            "cycle_close_ms_per_1000_clients": round(4 * 1000 * P / (gbs * 1e9) * 1e3, 1),
+            "all_cores": {"value": round(gbs_all, 3), "cores": all_cores,
+                          "cycle_close_ms_per_1000_clients": round(4 * 1000 * P / (gbs_all * 1e9) * 1e3, 1)},
+            "numpy_restatement_1_thread": round(gbs_np, 3), "cpu_model": cpu_model()}
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def load_traffic(workload: str, variant: int, alg_bytes: float):

@@ -63,6 +63,21 @@ def fedavg_mean(model_params, diffs):
     return out
 
 
+def fedavg_mean_torch(model_params, diffs):
+    """The reference's hard-coded branch as it runs on the node: ``cycle_manager.py:276-296``
+    evaluated in torch on CPU tensors (``reduce(th.add, ...)``, ``th.div(sum, len(diffs))``,
+    ``model_param - diff_param``).  Bit-identical to ``fedavg_mean`` (``tests/test_oracle.py``);
+    ``bench.py``'s ``cpu_baseline`` times it at the node's 1 thread and at all host cores."""
+    from functools import reduce
+
+    import torch as th
+
+    raw = [[d[j] for d in diffs] for j in range(len(model_params))]
+    sums = [reduce(th.add, param) for param in raw]
+    avg = [th.div(param, len(diffs)) for param in sums]
+    return [p - a for p, a in zip(model_params, avg)]
+
+
 # ----------------------------------------------------------------------------------------
 # (a6)+(a8) hosted iterative avg plan: cycle_manager.py:266-269 + 01-Create-plan.ipynb:450-454
 # ----------------------------------------------------------------------------------------

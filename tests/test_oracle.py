@@ -71,6 +71,8 @@ def test_oracle_matches_reference_expressions(n):
         assert same(got, want.numpy())
     for got, want in zip(O.fedavg_iterative(ckpt, diffs), ref_iterative(tc, td)):
         assert same(got, want.numpy())
+    for got, want in zip(O.fedavg_mean_torch(tc, td), ref_hardcoded(tc, td)):  # the bench's CPU leg
+        assert same(got.numpy(), want.numpy())
 
 
 def test_oracle_matches_reference_on_edge_values():
