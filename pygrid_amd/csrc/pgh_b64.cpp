@@ -2,14 +2,24 @@
 //
 // Reference: fl_events.report decodes every client diff with
 // `base64.b64decode(data.get(CYCLE.DIFF, None).encode())` (apps/node/src/app/main/events/
-// model_centric/fl_events.py:257) -- O(diff bytes) per request, 47 MB per ResNet-18 diff.  Every
-// 4-character group decodes independently, so the input is split into group-aligned ranges
-// decoded by parallel threads.  Semantics follow Python's default (validate=False): characters
-// outside the alphabet (whitespace, newlines) are discarded before decoding, '=' padding ends
-// the data; a group count that is not a multiple of 4 after that is an error ("Incorrect padding").
+// model_centric/fl_events.py:257) -- O(diff bytes) per request, 47 MB per ResNet-18 diff.
+//
+// Semantics are CPython 3.10's non-validating binascii.a2b_base64 (what b64decode calls with
+// validate=False), which is a state machine over the characters: alphabet characters fill a
+// 4-character quad; any other character except '=' is skipped; '=' is skipped unless at least two
+// characters of the current quad are present, and there it counts as padding -- once quad
+// position + padding reaches 4 the decode stops, ignoring the rest.  A data character resets the
+// padding count.  Input that ends inside a quad is an error (1 character over: "cannot be 1 more
+// than a multiple of 4", 2-3: "Incorrect padding").
+//
+// Parallel form: before the first '=' the machine only decodes alphabet characters and skips the
+// rest, so that prefix is compacted to its alphabet characters (parallel count + prefix sum +
+// copy, only when something needs dropping) and its whole quads are decoded in parallel; the
+// machine itself runs only over the leftover 0-3 characters and the input from the first '='.
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -28,7 +38,7 @@ struct Table {
 };
 const Table kT;
 
-// Decode `n4` complete groups of clean input (no padding) into out; returns bytes written.
+// Decode `n4` complete quads of alphabet characters into out; returns bytes written.
 size_t decode_groups(const unsigned char* in, size_t n4, uint8_t* out) {
     for (size_t g = 0; g < n4; ++g) {
         const uint32_t x = ((uint32_t)kT.v[in[0]] << 18) | ((uint32_t)kT.v[in[1]] << 12) |
@@ -40,6 +50,40 @@ size_t decode_groups(const unsigned char* in, size_t n4, uint8_t* out) {
         out += 3;
     }
     return n4 * 3;
+}
+
+// CPython's a2b_base64 loop (non-strict), resumable: feed() runs characters through it and
+// appends output bytes; `done` once a complete padding sequence has been seen.
+struct Machine {
+    int quad_pos = 0, pads = 0;
+    unsigned leftchar = 0;
+    bool done = false;
+    void feed(const unsigned char* p, size_t n, std::vector<uint8_t>* out) {
+        for (size_t i = 0; i < n && !done; ++i) {
+            const unsigned char ch = p[i];
+            if (ch == '=') {
+                if (quad_pos >= 2 && quad_pos + ++pads >= 4) done = true;
+                continue;
+            }
+            const int v = kT.v[ch];
+            if (v < 0) continue;
+            pads = 0;
+            switch (quad_pos) {
+            case 0: quad_pos = 1; leftchar = (unsigned)v; break;
+            case 1: quad_pos = 2; out->push_back((uint8_t)((leftchar << 2) | ((unsigned)v >> 4))); leftchar = (unsigned)v & 0x0f; break;
+            case 2: quad_pos = 3; out->push_back((uint8_t)((leftchar << 4) | ((unsigned)v >> 2))); leftchar = (unsigned)v & 0x03; break;
+            default: quad_pos = 0; out->push_back((uint8_t)((leftchar << 6) | (unsigned)v)); leftchar = 0; break;
+            }
+        }
+    }
+};
+
+template <class F>
+void parallel(int t, F&& f) {  // f(k) for k in [0, t), k = 0 on the calling thread
+    std::vector<std::thread> th;
+    for (int k = 1; k < t; ++k) th.emplace_back(f, k);
+    f(0);
+    for (auto& x : th) x.join();
 }
 
 }  // namespace
@@ -58,67 +102,51 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
     const unsigned char* s = (const unsigned char*)in;
     int t = threads > 0 ? threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     if (n < (1u << 18)) t = 1;
-    // data ends at the first '='; everything before it must be alphabet for the fast path
     const void* eq = n ? std::memchr(s, '=', n) : nullptr;
-    const size_t fe = eq ? (size_t)((const unsigned char*)eq - s) : n;
-    std::vector<char> bad((size_t)t, 0);
-    {
-        const size_t per = (fe + t - 1) / t;
-        std::vector<std::thread> th;
-        auto scan = [&](int k) {
-            const size_t a = per * k, b = std::min(fe, a + per);
+    const size_t fe = eq ? (size_t)((const unsigned char*)eq - s) : n;  // the machine's fast prefix
+    // count alphabet characters per chunk of [0, fe)
+    const size_t per = (fe + t - 1) / t;
+    std::vector<size_t> good((size_t)t, 0);
+    parallel(t, [&](int k) {
+        const size_t a = std::min(fe, per * k), b = std::min(fe, a + per);
+        size_t g = 0;
+        for (size_t i = a; i < b; ++i) g += kT.v[s[i]] >= 0;
+        good[(size_t)k] = g;
+    });
+    size_t d = 0;
+    for (size_t g : good) d += g;
+    const unsigned char* data = s;
+    std::unique_ptr<unsigned char[]> filtered;  // not zero-filled: every byte is written below
+    if (d != fe) {  // drop what the machine would skip (whitespace, line breaks, junk)
+        filtered.reset(new unsigned char[d ? d : 1]);
+        std::vector<size_t> at((size_t)t, 0);
+        for (int k = 1; k < t; ++k) at[(size_t)k] = at[(size_t)k - 1] + good[(size_t)k - 1];
+        parallel(t, [&](int k) {
+            const size_t a = std::min(fe, per * k), b = std::min(fe, a + per);
+            unsigned char* o = filtered.get() + at[(size_t)k];
             for (size_t i = a; i < b; ++i)
-                if (kT.v[s[i]] < 0) { bad[(size_t)k] = 1; return; }
-        };
-        for (int k = 1; k < t; ++k) th.emplace_back(scan, k);
-        scan(0);
-        for (auto& x : th) x.join();
+                if (kT.v[s[i]] >= 0) *o++ = s[i];
+        });
+        data = filtered.get();
     }
-    bool clean = true;
-    for (char b : bad) clean = clean && !b;
-    std::vector<unsigned char> filtered;
-    size_t d = fe;
-    if (!clean) {  // non-validating decode: drop characters outside the alphabet
-        filtered.reserve(fe);
-        for (size_t k = 0; k < fe; ++k)
-            if (kT.v[s[k]] >= 0) filtered.push_back(s[k]);
-        d = filtered.size();
-    }
-    // padding: '=' characters from the first one on (other non-alphabet characters skipped)
-    size_t pads = 0;
-    for (size_t k = fe; k < n; ++k) {
-        if (s[k] == '=') ++pads;
-        else if (kT.v[s[k]] >= 0) break;
-    }
-    const unsigned char* data = clean ? s : filtered.data();
-    const size_t rem = d % 4;
-    if (rem == 1) return PGH_E_PARSE;
-    if ((rem == 2 && pads < 2) || (rem == 3 && pads < 1)) return PGH_E_PARSE;
     const size_t n4 = d / 4;
+    Machine m;
+    std::vector<uint8_t> tail;
+    m.feed(data + 4 * n4, d - 4 * n4, &tail);  // leftover 0-3 characters of the prefix
+    m.feed(s + fe, n - fe, &tail);              // the first '=' onwards
+    if (!m.done && m.quad_pos != 0) return PGH_E_PARSE;
     if (!out) {
-        *written = n4 * 3 + (rem == 2 ? 1 : rem == 3 ? 2 : 0);
+        *written = n4 * 3 + tail.size();
         return PGH_OK;
     }
-    if (n4 < (1u << 16)) t = 1;
-    const size_t per = (n4 + t - 1) / t;
-    std::vector<std::thread> th;
-    for (int k = 1; k < t; ++k) {
-        const size_t g0 = per * k;
-        if (g0 >= n4) break;
-        const size_t g1 = std::min(n4, g0 + per);
-        th.emplace_back([=] { decode_groups(data + 4 * g0, g1 - g0, out + 3 * g0); });
-    }
-    decode_groups(data, std::min(per, n4), out);
-    for (auto& x : th) x.join();
-    size_t w = n4 * 3;
-    if (rem) {  // 2 or 3 trailing characters -> 1 or 2 bytes
-        const unsigned char* r = data + 4 * n4;
-        uint32_t x = ((uint32_t)kT.v[r[0]] << 18) | ((uint32_t)kT.v[r[1]] << 12);
-        if (rem == 3) x |= (uint32_t)kT.v[r[2]] << 6;
-        out[w++] = (uint8_t)(x >> 16);
-        if (rem == 3) out[w++] = (uint8_t)(x >> 8);
-    }
-    *written = w;
+    const int td = n4 < (1u << 16) ? 1 : t;
+    const size_t pq = (n4 + td - 1) / td;
+    parallel(td, [&](int k) {
+        const size_t g0 = std::min(n4, pq * k), g1 = std::min(n4, g0 + pq);
+        decode_groups(data + 4 * g0, g1 - g0, out + 3 * g0);
+    });
+    if (!tail.empty()) std::memcpy(out + 3 * n4, tail.data(), tail.size());
+    *written = n4 * 3 + tail.size();
     return PGH_OK;
 }
 

@@ -9,7 +9,9 @@ import pytest
 from pygrid_amd.report import b64decode
 
 CASES = ["QQ==", "QQ===", "QUJD", "QUJD=", "QUJD====", "QQ==QUJD", "QUJDRA==", "QU JD\nRA==", "QU*JD",
-         "QUI=", "====", "", "Zm9vYmFy", "Zm9v\r\nYmFy\n"]
+         "QUI=", "====", "", "Zm9vYmFy", "Zm9v\r\nYmFy\n",
+         # '=' the decoder skips (fewer than 2 characters of the quad), padding then more data
+         "9zWv=UyDn", "6=Za3/x/z", "=itfetOos", "yKViQhM9=aJrR", "=*u3sw", "QUI=\n=", "QU=I="]
 BAD = ["QQ", "QQ=", "Q", "QUJDRA", "QUJDRA=", "QUI"]
 
 
@@ -24,6 +26,36 @@ def test_bad_padding_raises_like_python(s):
         base64.b64decode(s)
     with pytest.raises(binascii.Error):
         b64decode(s)
+
+
+def test_fuzz_matches_python():
+    """CPython 3.10 a2b_base64 (non-strict) state machine, on random short strings."""
+    rng = np.random.default_rng(7)
+    alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/"
+    junk = alpha + "===\n *"
+    for _ in range(20000):
+        n = int(rng.integers(0, 17))
+        s = "".join(junk[rng.integers(len(junk))] if rng.random() < 0.4 else alpha[rng.integers(64)]
+                    for _ in range(n))
+        try:
+            want = base64.b64decode(s)
+        except binascii.Error:
+            want = None
+        try:
+            got = b64decode(s)
+        except binascii.Error:
+            got = None
+        assert got == want, s
+
+
+@pytest.mark.parametrize("threads", [1, 5])
+def test_mime_lines_and_junk_large(threads):
+    """76-character lines (base64.encodebytes) and junk: the parallel compaction path."""
+    data = np.random.default_rng(3).integers(0, 256, 3_000_001, dtype=np.uint8).tobytes()
+    enc = base64.encodebytes(data)
+    assert b64decode(enc, threads=threads) == data
+    dirty = enc.replace(b"A", b"A*", 1000) + b"=\n==QUJD"
+    assert b64decode(dirty, threads=threads) == base64.b64decode(dirty)
 
 
 @pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 1000, 1 << 20, (3 << 20) + 1, 12_000_001])
