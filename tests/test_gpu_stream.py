@@ -172,3 +172,38 @@ def test_pinned_buffer_ingest(engine):
     assert same(got, coracle.fedavg(0, d, c))
     for b in bufs:
         b.free()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_blocked_ring_small_staging(mode):
+    """Column-blocked ring (P = 70,001 -> 9 blocks of 8,192, a partial last block) fed through an
+    80 KiB pinned staging slot, so slot fills start and end mid-block: every head / 2-D / tail
+    copy shape of h2d_range, pageable arrays and State spans, out-of-order arrival."""
+    from pygrid_amd import Engine
+    from pygrid_amd.state_schema import build_state_fast
+
+    rng = np.random.default_rng(11 + mode)
+    shapes = [(3, 7001), (12,), (48_985,), (1,)]  # numel sums to 70,001; spans cross blocks
+    numel = [int(np.prod(s)) for s in shapes]
+    P, N, R = sum(numel), 9, 4
+    assert P == 70_001
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    with Engine(0, pinned_bytes=2 * 81_920) as eng:
+        eng.set_layout(numel)
+        eng.reserve(R)
+        _, ld, bp = eng.slab()
+        assert ld == 8192 and bp == R * ld
+        eng.stream_begin(mode, 2)
+        for k in arrival_order(N, R - 2 + 1, rng):
+            if k % 2:
+                eng.ingest(k, d[k])
+            else:
+                parts, o = [], 0
+                for s in shapes:
+                    n = int(np.prod(s))
+                    parts.append(d[k, o:o + n].reshape(s))
+                    o += n
+                eng.ingest_state(k, build_state_fast(parts))
+        got = eng.stream_finish(c)
+    assert same(got, coracle.fedavg(mode, d, c))
