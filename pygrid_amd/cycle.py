@@ -170,8 +170,10 @@ def make_average_plan_diffs(aggregator: CycleAggregator, model_manager, process_
     """Build a drop-in ``CycleManager._average_plan_diffs(self, server_config, cycle)``.
 
     DB I/O mirrors ``cycle_manager.py:234-245`` and ``:304-323``; the arithmetic slice
-    ``:240-303`` goes to the engine.  A plan the engine does not implement, or any engine
-    error, runs the reference's ``original`` method unchanged.
+    ``:240-303`` goes to the engine.  A user-defined (non-iterative) avg plan, which the engine
+    does not implement, runs the reference's ``original`` method unchanged.
+    Engine errors are NOT retried on the CPU: they raise ``PyGridError`` subclasses, which
+    ``tasks.complete_cycle`` logs (``tasks/cycle.py:28-37``), like any failed cycle close.
     """
 
     def _average_plan_diffs(self, server_config: dict, cycle):
