@@ -168,6 +168,11 @@ struct pgh_ctx {
     float* d_dec = nullptr;
     float* d_w = nullptr;
     size_t w_cap = 0;
+    // iterative plan: rec[k] = 1 / (double)(float)(k + 1), grown on demand, kept for the context's
+    // life (a superseded table may still be read by an in-flight fold: freed at destroy)
+    double* d_rec = nullptr;
+    int64_t rec_cap = 0;
+    std::vector<double*> rec_old;
 
     uint8_t* h_pin[2] = {nullptr, nullptr};
     size_t pin_slot = 0;
@@ -568,6 +573,26 @@ int sync_weights(pgh_ctx* c, hipStream_t s) {
     return PGH_OK;
 }
 
+// Reciprocal table covering clients [0, n) for the iterative fold's division (div_by_count in
+// pgh_kernels.hip).  Grows geometrically; the upload is ordered before stream `s`'s next fold.
+int ensure_recips(pgh_ctx* c, int64_t n, hipStream_t s) {
+    if (n <= c->rec_cap) return PGH_OK;
+    const int64_t cap = std::max<int64_t>({n, 2 * c->rec_cap, 4096});
+    std::vector<double> h((size_t)cap);
+    for (int64_t k = 0; k < cap; ++k) h[(size_t)k] = 1.0 / (double)(float)(k + 1);  // y as the plan sees it
+    double* d = nullptr;
+    if (hipMalloc((void**)&d, sizeof(double) * (size_t)cap) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(c, PGH_E_OOM, "reciprocal table allocation failed");
+    }
+    CK(c, hipMemcpyAsync(d, h.data(), sizeof(double) * (size_t)cap, hipMemcpyHostToDevice, s));
+    CK(c, hipStreamSynchronize(s));  // h is freed on return
+    if (c->d_rec) c->rec_old.push_back(c->d_rec);
+    c->d_rec = d;
+    c->rec_cap = cap;
+    return PGH_OK;
+}
+
 int fixed_point_divisor(pgh_ctx* c, int base, int prec, float* div) {
     if (base < 2 || prec < 0 || prec > 18) return fail(c, PGH_E_ARG, "bad fixed-point base %d / precision %d", base, prec);
     long double scale = 1;
@@ -603,6 +628,7 @@ int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const Fina
                         (long long)(c0 + n));
         RC(sync_weights(c, s));
     }
+    if (kind == PGH_ITERATIVE_MEAN && n > 0) RC(ensure_recips(c, c0 + n, s));
     const int R = c->slots;
     const int64_t off = fa.off;
     const int64_t len = fa.len < 0 ? c->pg - off : fa.len;
@@ -642,6 +668,7 @@ int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const Fina
             a.client0 = c0 + done;
             a.p = len;
             a.weights = c->d_w ? c->d_w + (c0 + done) : nullptr;
+            a.recips = c->d_rec ? c->d_rec + (c0 + done) : nullptr;
             a.acc = c->d_acc + off;
             a.ckpt = fa.ckpt ? fa.ckpt + off : nullptr;
             a.out = fa.out ? fa.out + off : nullptr;
@@ -832,6 +859,8 @@ void pgh_destroy(pgh_ctx* c) {
     for (auto e : c->pool) (void)hipEventDestroy(e);
     clear_marks(c);
     for (auto e : c->mark_pool) (void)hipEventDestroy(e);
+    (void)hipFree(c->d_rec);
+    for (double* p : c->rec_old) (void)hipFree(p);
     for (int k = 0; k < 2; ++k) {
         if (c->h_pin[k]) (void)hipHostFree(c->h_pin[k]);
         if (c->pin_ev[k]) (void)hipEventDestroy(c->pin_ev[k]);

@@ -38,6 +38,7 @@ struct FedavgArgs {
     int64_t client0;        // global index of row 0 (iterative k, weight index)
     int64_t p;              // params in this shard
     const float* weights;   // [n_rows] device, MODE_WEIGHTED only
+    const double* recips;   // [n_rows] device, MODE_ITERATIVE: 1 / (double)(float)(client0 + r + 1)
     float* acc;             // [p] running state; read unless FL_FIRST, written unless FL_FINAL
     const float* ckpt;      // [p], FL_FINAL only
     float* out;             // [p], FL_FINAL only

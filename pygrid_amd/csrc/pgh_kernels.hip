@@ -95,14 +95,76 @@ template <> struct Lane<1> {
 };
 
 template <int MODE, class T>
-__device__ __forceinline__ T fold(T acc, T v, int64_t k, const float* w, int r) {
+__device__ __forceinline__ T fold(T acc, T v, const float* w, int r) {
     if constexpr (MODE == MODE_MEAN) {
         return acc + v;                                   // th.add, cycle_manager.py:286
-    } else if constexpr (MODE == MODE_WEIGHTED) {
-        return acc + v * w[r];                            // product rounded, then add
     } else {
-        const float kf = (float)k, kf1 = (float)(k + 1);  // th.tensor([k]) promoted to f32
-        return (acc * kf + v) / kf1;                      // 01-Create-plan.ipynb:453
+        return acc + v * w[r];                            // MODE_WEIGHTED: product rounded, then add
+    }
+}
+
+// Iterative plan step k (01-Create-plan.ipynb:453): t = avg * k + d (two roundings: no FMA under
+// -ffp-contract=off), avg = t / (k + 1) with k and k + 1 promoted to f32 like th.tensor([k]).
+// The IEEE division is replaced by (float)((double)t * rec), rec = RN_f64(1 / y), y = (float)(k+1):
+// the double product is within ~2^-52 of t / y, which for a normal quotient is never an f32
+// rounding midpoint and never within ~2^-49 of one, so the final rounding agrees bit for bit
+// (tests/native/recip_div_check.c: 2e9 operand pairs against IEEE division).  A lane whose
+// quotient could be below 2^-125 (0 < |t| < 2^-125 * y) sets `tiny`; the caller then redoes the
+// batch with real divisions.  rec comes from a per-client table (scalar loads: k is uniform).
+__device__ __forceinline__ float iter_step(float acc, float v, float kf, double rec, uint32_t thr, bool& tiny) {
+    const float t = acc * kf + v;
+    const uint32_t ut = __float_as_uint(t) & 0x7fffffffu;
+    tiny |= (ut - 1u) < thr;  // thr = bits(2^-125 * y) - 1
+    return (float)((double)t * rec);
+}
+__device__ __forceinline__ f32x4 iter_step(f32x4 acc, f32x4 v, float kf, double rec, uint32_t thr, bool& tiny) {
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = iter_step(acc[e], v[e], kf, rec, thr, tiny);
+    return o;
+}
+
+// Fold rows r .. r + U - 1 (already loaded in v) into acc, in order.
+template <int MODE, int U, int W, class T>
+__device__ __forceinline__ void fold_rows(T (&acc)[W], const T (&v)[U][W], const FedavgArgs& a, int r) {
+    if constexpr (MODE != MODE_ITERATIVE) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int w = 0; w < W; ++w) acc[w] = fold<MODE>(acc[w], v[u][w], a.weights, r + u);
+    } else {
+        T acc0[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) acc0[w] = acc[w];
+        bool tiny = false;
+        const uint32_t k0 = (uint32_t)(a.client0 + r);  // client indices < 2^31
+#pragma unroll
+        for (int u0 = 0; u0 < U; u0 += 8) {
+            double rec[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (u0 + j < U) rec[j] = a.recips[r + u0 + j];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (u0 + j >= U) break;
+                const uint32_t k = k0 + (uint32_t)(u0 + j);
+                const float kf = (float)k, y = (float)(k + 1u);
+                const uint32_t thr = __float_as_uint(0x1p-125f * y) - 1u;
+#pragma unroll
+                for (int w = 0; w < W; ++w) acc[w] = iter_step(acc[w], v[u0 + j][w], kf, rec[j], thr, tiny);
+            }
+        }
+        if (tiny) {  // rare: a quotient near f32's subnormal range -- redo these rows dividing for real
+#pragma unroll
+            for (int w = 0; w < W; ++w) acc[w] = acc0[w];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t k = k0 + (uint32_t)u;
+                const float kf = (float)k, y = (float)(k + 1u);
+#pragma unroll
+                for (int w = 0; w < W; ++w) acc[w] = (acc[w] * kf + v[u][w]) / y;
+            }
+        }
     }
 }
 
@@ -138,15 +200,14 @@ __device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, 
 #pragma unroll
             for (int w = 0; w < W; ++w)
                 v[u][w] = L::template load<NT>(col[w] + (size_t)(r + u) * ld);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int w = 0; w < W; ++w) acc[w] = fold<MODE>(acc[w], v[u][w], a.client0 + r + u, a.weights, r + u);
+        fold_rows<MODE, U, W>(acc, v, a, r);
     }
-    for (; r < n; ++r)
+    for (; r < n; ++r) {
+        T v[1][W];
 #pragma unroll
-        for (int w = 0; w < W; ++w)
-            acc[w] = fold<MODE>(acc[w], L::template load<NT>(col[w] + (size_t)r * ld), a.client0 + r, a.weights, r);
+        for (int w = 0; w < W; ++w) v[0][w] = L::template load<NT>(col[w] + (size_t)r * ld);
+        fold_rows<MODE, 1, W>(acc, v, a, r);
+    }
 #pragma unroll
     for (int w = 0; w < W; ++w) {
         const int64_t q = q0 + w * qstep;
@@ -364,13 +425,17 @@ hipError_t dispatch_fedavg(const FedavgArgs& a, int variant, hipStream_t s) {
 //   P = 311,650 x 10K:   mean v11 6885 / v15 6645 / v0 5753;  iterative v12 5711 / v14 5670 / v11 5351
 //   P = 100K x 30K:      mean v11 6403 / v12 6251;  iterative v14 4742 / v12 4465 / v11 2784
 //   single block (P < 65,536; layout unchanged from r01g): P = 50K x 60K v14 6088 / v12 4013
+// Iterative fold with the reciprocal-multiply division (r01o, tools/ab_iterative.sh):
+//   P = 50K x 60K v17 3665 / v14 3496;  100K x 30K v14 5970 / v17 5616;  311,650 x 10K v11 6359 /
+//   v14 5894;  1M x 3K v0 6755;  11.69M x 1K v0 6846  (IEEE division: 3209 / 4757 / 5784 / 6753 / 6845)
 // Big shards: 16-byte columns in 256-thread blocks (the blocked slab made them 5 % faster than one
 // param per lane).  Below ~786K params those give < 768 workgroups for 256 CUs, so 64-thread
-// blocks (CU balance) and, for the ALU-heavier iterative fold, one param per lane (lanes).
+// blocks (CU balance); below ~200K params one param per lane (lanes), with deeper row pipelines
+// for the iterative fold of the smallest shards (few waves: latency).
 int auto_variant(int64_t p, int mode) {
-    if (p < 80000) return 14;
+    if (p < 80000) return mode == MODE_ITERATIVE ? 17 : 14;
     if (p < 200000) return mode == MODE_ITERATIVE ? 14 : 11;
-    if (p < 786432) return mode == MODE_ITERATIVE ? 12 : 11;
+    if (p < 786432) return 11;
     if (p < 2000000) return 0;
     return mode == MODE_WEIGHTED ? 15 : 0;
 }
@@ -401,6 +466,7 @@ hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
                                  (reinterpret_cast<uintptr_t>(a.out) & 15)))
         return hipErrorInvalidValue;
     if (a.mode == MODE_WEIGHTED && a.n_rows > 0 && !a.weights) return hipErrorInvalidValue;
+    if (a.mode == MODE_ITERATIVE && a.n_rows > 0 && !a.recips) return hipErrorInvalidValue;
     const int v = a.variant < 0 ? auto_variant(a.p, a.mode) : a.variant;
     switch (a.mode) {
     case MODE_MEAN: return dispatch_fedavg<MODE_MEAN>(a, v, s);

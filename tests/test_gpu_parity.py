@@ -553,3 +553,52 @@ def test_rccl_overlapped_gather_world1(engine):
         assert same(full.cpu().numpy()[idx], coracle.fedavg(0, d[:, idx], c[idx]))
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("variant", [-1, 0, 6, 11, 12, 14, 15, 17])
+def test_iterative_division_shortcut_edges(engine, variant):
+    """The iterative fold's reciprocal-multiply division (div shortcut in pgh_kernels.hip) around
+    its fallback threshold |t| ~ 2^-125 * (k + 1), subnormals, zeros of both signs, overflow to
+    inf and NaN -- lanes that need the real division sharing row batches with lanes that do not."""
+    rng = np.random.default_rng(variant + 50)
+    N, P = 70, 4103
+    d = np.empty((N, P), F)
+    kinds = rng.integers(0, 7, P)
+    for c in range(N):
+        y = F(c + 1)
+        thr = F(2.0 ** -125) * y
+        col = np.where(kinds == 0, thr * F(rng.uniform(0.5, 2.0)),                   # around the threshold
+              np.where(kinds == 1, F(1e-41) * F(rng.uniform(-3, 3)),                  # subnormal
+              np.where(kinds == 2, F(rng.choice([0.0, -0.0])),                        # signed zeros
+              np.where(kinds == 3, F(3e38) * F(rng.choice([-1, 1])),                  # overflow: acc * k -> inf
+              np.where(kinds == 4, F(2.0 ** -120) * F(rng.uniform(-1, 1)),            # small normal
+                       rng.standard_normal(P).astype(F))))))
+        d[c] = col.astype(F)
+    d[5, ::97] = np.nan
+    c = rng.standard_normal(P).astype(F)
+    engine.set_variant(variant)
+    try:
+        got = run_f32(engine, d, c, 1)
+    finally:
+        engine.set_variant(-1)
+    assert same(got, coracle.fedavg(1, d, c))
+
+
+def test_iterative_division_exact_subnormal_midpoints(engine):
+    """Quotients that are exact ties between two f32 subnormals, where the reciprocal multiply
+    alone rounds the wrong way (e.g. 147 * 2^-149 / 98 = 1.5 * 2^-149 -> 2^-148 by ties-to-even;
+    t * RN(1/98) lands just below the tie): the kernel's fallback to the real division keeps them
+    bit-exact.  Clients 0..96 send zeros so the plan's running average is 0 when client 97's
+    diff T * 2^-149 arrives (k = 97, y = 98)."""
+    P, N = 2048, 98
+    T = 49 * (2 * np.arange(P, dtype=np.uint32) + 1)  # odd multiples of y / 2: exact midpoints
+    d = np.zeros((N, P), F)
+    d[97] = T.view(F)
+    c = np.zeros(P, F)
+    for variant in (-1, 0, 14, 17):
+        engine.set_variant(variant)
+        try:
+            got = run_f32(engine, d, c, 1)
+        finally:
+            engine.set_variant(-1)
+        assert same(got, coracle.fedavg(1, d, c)), variant
