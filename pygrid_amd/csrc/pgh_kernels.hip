@@ -289,7 +289,16 @@ __global__ __launch_bounds__(TB) void k_secagg(SecaggArgs a, int64_t ncol) {
 #pragma unroll
             for (int u = 0; u < U; ++u) acc += v[u];  // wraps mod 2^64
         }
-        for (; r < a.n_rows; ++r) acc += L::template load<NT>(col + (size_t)r * ld);
+        if (r < a.n_rows) {  // last partial batch, its loads in flight together
+            const int nv = a.n_rows - r;
+            T v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (u < nv) v[u] = L::template load<NT>(col + (size_t)(r + u) * ld);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (u < nv) acc += v[u];
+        }
         for (int e = 0; e < ne; ++e) {
             const unsigned long long x = lane_elem<VEC>(acc, e);
             if (a.flags & FL_FINAL) {
