@@ -1367,7 +1367,7 @@ int pgh_stream_finish_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, f
 
 int pgh_set_variant(pgh_ctx* c, int variant) {
     if (!c) return PGH_E_ARG;
-    if (variant < -1 || variant > 18) return fail(c, PGH_E_ARG, "variant %d outside [-1,18]", variant);
+    if (variant < -1 || variant > 20) return fail(c, PGH_E_ARG, "variant %d outside [-1,20]", variant);
     c->variant = variant;
     return PGH_OK;
 }

@@ -385,10 +385,12 @@ int cu_count() {
 //   16  nt     48                  1              64     1                 one lane per param
 //   17  nt     64                  1              64     1                 one lane per param
 //   18  nt     32                  1              128    1                 one lane per param
+//   19  nt     16                  1              512    4                 one lane per column
+//   20  nt     8                   1              1024   4                 one lane per column
 // nt loads won 2-5 % on the once-read diff stream (r01c).  Small shards are bound by lanes / CU
 // balance, not by the loads: the auto choice (variant -1) picks by shard size and mode
 // (auto_variant below, r01l measurements on the column-blocked slab).
-constexpr int N_VARIANTS = 19;
+constexpr int N_VARIANTS = 21;
 constexpr int SECAGG_AUTO_VARIANT = 14;
 
 inline unsigned grid_for(int64_t ncol, int64_t tile, bool persistent) {
@@ -427,6 +429,8 @@ hipError_t dispatch_fedavg(const FedavgArgs& a, int variant, hipStream_t s) {
     case 16: return go_fedavg<MODE, 48, 1, true, 64, 1>(a, false, s);
     case 17: return go_fedavg<MODE, 64, 1, true, 64, 1>(a, false, s);
     case 18: return go_fedavg<MODE, 32, 1, true, 128, 1>(a, false, s);
+    case 19: return go_fedavg<MODE, 16, 1, true, 512, 4>(a, false, s);
+    case 20: return go_fedavg<MODE, 8, 1, true, 1024, 4>(a, false, s);
     default: return hipErrorInvalidValue;
     }
 }
