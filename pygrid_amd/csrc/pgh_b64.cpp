@@ -13,13 +13,15 @@
 // than a multiple of 4", 2-3: "Incorrect padding").
 //
 // Parallel form: before the first '=' the machine only decodes alphabet characters and skips the
-// rest, so that prefix is compacted to its alphabet characters (parallel count + prefix sum +
-// copy, only when something needs dropping) and its whole quads are decoded in parallel; the
-// machine itself runs only over the leftover 0-3 characters and the input from the first '='.
+// rest.  A parallel count of the prefix's alphabet characters per chunk gives every chunk its
+// position in that character stream; each thread then decodes the whole quads whose first
+// character lies in its chunk, skipping non-alphabet characters in place (no compacted copy).  The
+// machine itself runs only over the prefix's last 0-3 alphabet characters and the input from the
+// first '=' on.
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
-#include <memory>
+
 #include <string>
 #include <thread>
 #include <vector>
@@ -113,38 +115,50 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
         for (size_t i = a; i < b; ++i) g += kT.v[s[i]] >= 0;
         good[(size_t)k] = g;
     });
-    size_t d = 0;
-    for (size_t g : good) d += g;
-    const unsigned char* data = s;
-    std::unique_ptr<unsigned char[]> filtered;  // not zero-filled: every byte is written below
-    if (d != fe) {  // drop what the machine would skip (whitespace, line breaks, junk)
-        filtered.reset(new unsigned char[d ? d : 1]);
-        std::vector<size_t> at((size_t)t, 0);
-        for (int k = 1; k < t; ++k) at[(size_t)k] = at[(size_t)k - 1] + good[(size_t)k - 1];
-        parallel(t, [&](int k) {
-            const size_t a = std::min(fe, per * k), b = std::min(fe, a + per);
-            unsigned char* o = filtered.get() + at[(size_t)k];
-            for (size_t i = a; i < b; ++i)
-                if (kT.v[s[i]] >= 0) *o++ = s[i];
-        });
-        data = filtered.get();
-    }
-    const size_t n4 = d / 4;
+    // at[k]: index, among the prefix's alphabet characters, of chunk k's first one
+    std::vector<size_t> at((size_t)t + 1, 0);
+    for (int k = 0; k < t; ++k) at[(size_t)k + 1] = at[(size_t)k] + good[(size_t)k];
+    const size_t d = at[(size_t)t], n4 = d / 4;
+    // the machine runs over the prefix's last d % 4 alphabet characters, then from the first '='
+    unsigned char lead[3];
+    size_t nl = 0;
+    for (size_t i = fe; i > 0 && nl < d % 4; --i)
+        if (kT.v[s[i - 1]] >= 0) lead[nl++] = s[i - 1];
+    std::reverse(lead, lead + nl);
     Machine m;
     std::vector<uint8_t> tail;
-    m.feed(data + 4 * n4, d - 4 * n4, &tail);  // leftover 0-3 characters of the prefix
-    m.feed(s + fe, n - fe, &tail);              // the first '=' onwards
+    m.feed(lead, nl, &tail);
+    m.feed(s + fe, n - fe, &tail);
     if (!m.done && m.quad_pos != 0) return PGH_E_PARSE;
     if (!out) {
         *written = n4 * 3 + tail.size();
         return PGH_OK;
     }
-    const int td = n4 < (1u << 16) ? 1 : t;
-    const size_t pq = (n4 + td - 1) / td;
-    parallel(td, [&](int k) {
-        const size_t g0 = std::min(n4, pq * k), g1 = std::min(n4, g0 + pq);
-        decode_groups(data + 4 * g0, g1 - g0, out + 3 * g0);
-    });
+    if (d == fe) {  // clean prefix: whole quads straight from the input
+        const int td = n4 < (1u << 16) ? 1 : t;
+        const size_t pq = (n4 + td - 1) / td;
+        parallel(td, [&](int k) {
+            const size_t g0 = std::min(n4, pq * k), g1 = std::min(n4, g0 + pq);
+            decode_groups(s + 4 * g0, g1 - g0, out + 3 * g0);
+        });
+    } else {  // skip what the machine skips: thread k decodes the quads whose FIRST character is in its chunk
+        parallel(t, [&](int k) {
+            size_t i = std::min(fe, per * k), c = at[(size_t)k];
+            const size_t c_end = std::min(at[(size_t)k + 1], 4 * n4);
+            while (c % 4 && c < c_end) c += kT.v[s[i++]] >= 0;  // finishes a quad begun in an earlier chunk
+            for (; c < c_end; c += 4) {                           // may read past the chunk: never past fe
+                uint32_t x = 0;
+                for (int got = 0; got < 4; ++i) {
+                    const int v = kT.v[s[i]];
+                    if (v >= 0) { x = (x << 6) | (uint32_t)v; ++got; }
+                }
+                uint8_t* o = out + 3 * (c / 4);
+                o[0] = (uint8_t)(x >> 16);
+                o[1] = (uint8_t)(x >> 8);
+                o[2] = (uint8_t)x;
+            }
+        });
+    }
     if (!tail.empty()) std::memcpy(out + 3 * n4, tail.data(), tail.size());
     *written = n4 * 3 + tail.size();
     return PGH_OK;

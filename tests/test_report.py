@@ -58,6 +58,28 @@ def test_mime_lines_and_junk_large(threads):
     assert b64decode(dirty, threads=threads) == base64.b64decode(dirty)
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_junk_multithreaded_matches_python(seed):
+    """Large inputs (threaded path) with junk bursts, quads split across chunk edges, and '='
+    tricks near the end, for several thread counts."""
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 256, int(rng.integers(200_000, 400_000)), dtype=np.uint8).tobytes()
+    enc = bytearray(base64.b64encode(data).rstrip(b"="))
+    for pos in sorted(rng.integers(0, len(enc), 300), reverse=True):
+        enc[pos:pos] = bytes(rng.choice(list(b" \n\r*~\t"), int(rng.integers(1, 40))))
+    enc = bytes(enc) + [b"", b"=", b"==", b"=\n=QUJD", b"Q=", b"QUJD=="][seed]
+    try:
+        want = base64.b64decode(enc)
+    except binascii.Error:
+        want = None
+    for th in (2, 3, 7, 16):
+        try:
+            got = b64decode(enc, threads=th)
+        except binascii.Error:
+            got = None
+        assert got == want, th
+
+
 @pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 1000, 1 << 20, (3 << 20) + 1, 12_000_001])
 def test_random_payloads(n):
     data = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
