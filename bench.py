@@ -253,7 +253,7 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
             lp = og.local.data_ptr()
 
             def step():
-                og.run(lambda off, n: eng.fedavg_device_range(mode, off, n, ckpt.data_ptr(), lp, sp))
+                og.run(lambda off, n, st: eng.fedavg_device_range(mode, off, n, ckpt.data_ptr(), lp, st))
                 og.assemble()
         else:
             def step():

@@ -138,9 +138,12 @@ struct pgh_ctx {
     hipStream_t stream = nullptr;  // reductions
     hipStream_t copy = nullptr;    // ingest H2D and on-device synthetic fill
     hipEvent_t copy_done = nullptr;
-    hipEvent_t fold_done = nullptr;
     hipEvent_t xsync = nullptr;    // caller-stream <-> context-stream ordering
-    bool fold_pending = false;
+    // The last fold issued on each stream (folds may run on several caller streams at once, e.g.
+    // the param ranges of the multi-GPU overlap): the copy stream waits on all before it
+    // overwrites slots, and then forgets them (later copies are ordered after those waits).
+    std::vector<std::pair<hipStream_t, hipEvent_t>> fold_evs;
+    std::vector<hipEvent_t> fold_ev_pool;
     // STREAM: one event per fold with the fold front after it, so overwriting a slot waits only
     // for the fold that consumed the slot's previous client (not for the latest fold).
     struct FoldMark { hipEvent_t ev; int64_t upto; };
@@ -249,6 +252,7 @@ size_t esize(int dtype) { return dtype == PGH_F32 ? 4 : 8; }
 void free_slab(pgh_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
+    for (auto& fe : c->fold_evs) (void)hipEventSynchronize(fe.second);  // folds on caller streams
     (void)hipFree(c->d_slab); c->d_slab = nullptr; c->slab_bytes = 0;
     (void)hipFree(c->d_ckpt); c->d_ckpt = nullptr;
     (void)hipFree(c->d_out); c->d_out = nullptr;
@@ -263,7 +267,8 @@ void free_slab(pgh_ctx* c) {
     c->marks.clear();
     c->streaming = false;
     c->folded = 0;
-    c->fold_pending = false;
+    for (auto& fe : c->fold_evs) c->fold_ev_pool.push_back(fe.second);
+    c->fold_evs.clear();
     c->weights_on_device = false;
 }
 
@@ -518,9 +523,26 @@ int order_after_ingest(pgh_ctx* c, hipStream_t s) {
     return PGH_OK;
 }
 
-// Before the copy stream overwrites a slot, it waits for the last fold that read slots.
+// Before the copy stream overwrites a slot, it waits for every fold issued so far (the last one
+// on each stream that ran folds).
 int order_before_overwrite(pgh_ctx* c) {
-    if (c->fold_pending) CK(c, hipStreamWaitEvent(c->copy, c->fold_done, 0));
+    for (auto& fe : c->fold_evs) CK(c, hipStreamWaitEvent(c->copy, fe.second, 0));
+    for (auto& fe : c->fold_evs) c->fold_ev_pool.push_back(fe.second);
+    c->fold_evs.clear();
+    return PGH_OK;
+}
+
+// Remember the fold just issued on stream s.
+int record_fold(pgh_ctx* c, hipStream_t s) {
+    hipEvent_t ev = nullptr;
+    for (auto& fe : c->fold_evs)
+        if (fe.first == s) ev = fe.second;
+    if (!ev) {
+        if (!c->fold_ev_pool.empty()) { ev = c->fold_ev_pool.back(); c->fold_ev_pool.pop_back(); }
+        else CK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        c->fold_evs.push_back({s, ev});
+    }
+    CK(c, hipEventRecord(ev, s));
     return PGH_OK;
 }
 
@@ -682,9 +704,7 @@ int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const Fina
         }
         done += seg;
     } while (done < n);
-    CK(c, hipEventRecord(c->fold_done, s));
-    c->fold_pending = true;
-    return PGH_OK;
+    return record_fold(c, s);
 }
 
 // Length of the run of ingested clients starting at `from` (slot ring order).
@@ -837,7 +857,6 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&c->fold_done, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->xsync, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->pin_ev[0], hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->pin_ev[1], hipEventDisableTiming) == hipSuccess;
@@ -865,8 +884,9 @@ void pgh_destroy(pgh_ctx* c) {
         if (c->h_pin[k]) (void)hipHostFree(c->h_pin[k]);
         if (c->pin_ev[k]) (void)hipEventDestroy(c->pin_ev[k]);
     }
-    for (hipEvent_t e : {c->copy_done, c->fold_done, c->xsync})
+    for (hipEvent_t e : {c->copy_done, c->xsync})
         if (e) (void)hipEventDestroy(e);
+    for (auto e : c->fold_ev_pool) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
     delete c;
@@ -951,14 +971,15 @@ int pgh_reset(pgh_ctx* c) {
     if (!c) return PGH_E_ARG;
     DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->fold_pending) (void)hipEventSynchronize(c->fold_done);  // folds issued on caller streams
+    for (auto& fe : c->fold_evs) (void)hipEventSynchronize(fe.second);  // folds issued on caller streams
+    for (auto& fe : c->fold_evs) c->fold_ev_pool.push_back(fe.second);
+    c->fold_evs.clear();
     clear_marks(c);
     std::fill(c->slot_client.begin(), c->slot_client.end(), -1);
     c->weights.clear();
     c->weights_on_device = false;
     c->streaming = false;
     c->folded = 0;
-    c->fold_pending = false;
     c->st.n_clients = 0;
     c->st.n_folded = 0;
     return PGH_OK;

@@ -44,7 +44,7 @@ def _worker(rank, world, port, P, N, mode, q):
         # chunked fold + overlapped all-gather (what bench.py runs at N > 1)
         og = OverlappedGather(P, world, rank, chunks=3, device="cpu")
 
-        def fold_range(off, n):
+        def fold_range(off, n, stream):
             w = np.linspace(0.5, 2.0, N).astype(np.float32)
             og.local[off:off + n] = torch.from_numpy(coracle.fedavg(
                 mode, np.ascontiguousarray(d[:, lo + off:lo + off + n]), c[lo + off:lo + off + n],

@@ -393,7 +393,7 @@ def test_fedavg_device_range_pieces_equal_whole(engine):
     ck = torch.from_numpy(c).cuda()
     og = OverlappedGather(P, 1, 0, chunks=5)
     lp = og.local.data_ptr()
-    og.run(lambda off, n: engine.fedavg_device_range(1, off, n, ck.data_ptr(), lp))
+    og.run(lambda off, n, st: engine.fedavg_device_range(1, off, n, ck.data_ptr(), lp, st))
     assert same(og.assemble().cpu().numpy(), whole)
     from pygrid_amd import AggregationError
     with pytest.raises(AggregationError):
@@ -544,8 +544,7 @@ def test_rccl_overlapped_gather_world1(engine):
             engine.ingest(k, d[k])
         ck = torch.from_numpy(c).cuda()
         og = OverlappedGather(P, 1, 0, chunks=8)
-        sp = torch.cuda.current_stream().cuda_stream
-        og.run(lambda off, n: engine.fedavg_device_range(0, off, n, ck.data_ptr(), og.local.data_ptr(), sp),
+        og.run(lambda off, n, st: engine.fedavg_device_range(0, off, n, ck.data_ptr(), og.local.data_ptr(), st),
                force_collective=True)
         full = og.assemble()
         torch.cuda.synchronize()

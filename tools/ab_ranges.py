@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--params", type=int, default=11_689_512)
     ap.add_argument("--chunks", default="1,2,4,8,16")
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--variant", type=int, default=-1)
+    ap.add_argument("--streams", type=int, default=1, help="alternate range folds over this many streams")
     a = ap.parse_args()
     import torch
 
@@ -31,6 +33,7 @@ def main():
     eng.set_layout([P])
     eng.reserve(N)
     eng.synth_fill(1, N)
+    eng.set_variant(a.variant)
     sp = torch.cuda.current_stream().cuda_stream
     ck = torch.empty(P, dtype=torch.float32, device="cuda")
     out = torch.empty_like(ck)
@@ -43,12 +46,19 @@ def main():
         plans[k] = [(o, min(c, P - o)) for o in range(0, P, c)]
         res[k] = []
 
+    main = torch.cuda.current_stream()
+    side = [main] + [torch.cuda.Stream() for _ in range(a.streams - 1)]
+
     def step(k):
         if k == 1:
             eng.fedavg_device(0, ck.data_ptr(), out.data_ptr(), sp)
         else:
-            for o, n in plans[k]:
-                eng.fedavg_device_range(0, o, n, ck.data_ptr(), out.data_ptr(), sp)
+            for s in side[1:]:
+                s.wait_stream(main)  # step boundary: every range after the previous step
+            for i, (o, n) in enumerate(plans[k]):
+                eng.fedavg_device_range(0, o, n, ck.data_ptr(), out.data_ptr(), side[i % len(side)].cuda_stream)
+            for s in side[1:]:
+                main.wait_stream(s)
 
     for k in plans:
         step(k)
@@ -62,7 +72,7 @@ def main():
             torch.cuda.synchronize()
             res[k].append((time.perf_counter() - t0) / 3 * 1e3)
     alg = 4 * N * P + 8 * P
-    print(json.dumps({"P": P, "N": N, "variant": eng.effective_variant(),
+    print(json.dumps({"P": P, "N": N, "variant": a.variant, "streams": a.streams,
                       "chunks": {k: {"ms_median": round(statistics.median(v), 4),
                                      "GBps": round(alg / statistics.median(v) / 1e6, 1)} for k, v in res.items()}}))
 
