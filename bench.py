@@ -235,7 +235,6 @@ def roofline_of(st, workload, variant, kernel):
 
 def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
     torch = ctx.torch
-    from pygrid_amd.sharding import gather_flat
 
     eng.reserve(N, dtype, parties)
     eng.synth_fill(args.seed, N)
@@ -262,11 +261,18 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
     else:
         s_out = torch.empty(pg, dtype=torch.int64, device="cuda")
         d_out = torch.empty(pg, dtype=torch.float32, device="cuda")
+        if ctx.world > 1:
+            # decoded shard gathered range by range beside the share sum of the next range
+            from pygrid_amd.sharding import OverlappedGather
+            og = OverlappedGather(P, ctx.world, ctx.rank, chunks=args.gather_chunks)
+            lp = og.local.data_ptr()
 
-        def step():
-            eng.secagg_device(s_out.data_ptr(), d_out.data_ptr(), 10, 3, sp)
-            if ctx.world > 1:
-                gather_flat(d_out, P, ctx.world, ctx.rank)
+            def step():
+                og.run(lambda off, n, st: eng.secagg_device_range(off, n, s_out.data_ptr(), lp, 10, 3, st))
+                og.assemble()
+        else:
+            def step():
+                eng.secagg_device(s_out.data_ptr(), d_out.data_ptr(), 10, 3, sp)
         diff_bytes, dt, kernel = 8 * parties * N * pg, "int64", "k_secagg"
     torch.cuda.synchronize()
     el, st = timed(ctx, step, args.steps, args.warmup, eng)
@@ -275,8 +281,7 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
                        + (f" x {parties} parties int64" if dtype == 1 else " fp32") + ", resident in HBM",
            "clients": N, "params_per_gpu": pg, "params_total": P,
            "parallelism": f"param-shard{ctx.world}" + (
-               f" + RCCL all-gather ({args.gather_chunks} ranges overlapped with the fold)" if ctx.world > 1 and dtype == 0
-               else " + RCCL all-gather" if ctx.world > 1 else ""),
+               f" + RCCL all-gather ({args.gather_chunks} ranges overlapped with the fold)" if ctx.world > 1 else ""),
            "kernel_variant": eng.effective_variant(mode if dtype == 0 else 16)}
     rec = record(ctx, args, args.workload, value, el, dt, cfg,
                  roofline_of(st, args.workload, cfg["kernel_variant"], kernel))

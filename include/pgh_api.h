@@ -138,6 +138,10 @@ int pgh_ckpt_patch_state(pgh_ctx* ctx, const uint8_t* tmpl, size_t n, uint8_t* o
  * sum_out (int64) and dec_out (float32) are host arrays of P_shard; either may be NULL. */
 int pgh_secagg(pgh_ctx* ctx, int base, int prec, int64_t* sum_out, float* dec_out);
 int pgh_secagg_device(pgh_ctx* ctx, int base, int prec, int64_t* d_sum, float* d_dec, void* stream);
+/* Only the shard-relative param range [off, off + len) (off % 4 == 0); d_sum / d_dec are the
+ * shard-sized outputs, of which only that range is written (multi-GPU gather overlap). */
+int pgh_secagg_device_range(pgh_ctx* ctx, int base, int prec, int64_t off, int64_t len, int64_t* d_sum,
+                            float* d_dec, void* stream);
 /* Fill a device buffer with the synthetic checkpoint of this shard (P_shard floats). */
 int pgh_synth_ckpt_device(pgh_ctx* ctx, uint64_t seed, float* d_ckpt, void* stream);
 

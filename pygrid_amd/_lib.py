@@ -80,6 +80,7 @@ SIGNATURES = {
     "pgh_ckpt_patch_state": (_i, [_vp, C.c_char_p, _sz, _vp]),
     "pgh_secagg": (_i, [_vp, _i, _i, _vp, _vp]),
     "pgh_secagg_device": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
+    "pgh_secagg_device_range": (_i, [_vp, _i, _i, _i64, _i64, _vp, _vp, _vp]),
     "pgh_synth_ckpt_device": (_i, [_vp, _u64, _vp, _vp]),
     "pgh_stream_begin": (_i, [_vp, _i, _i]),
     "pgh_stream_flush": (_i, [_vp]),

@@ -1271,6 +1271,21 @@ int pgh_secagg_device(pgh_ctx* c, int base, int prec, int64_t* d_sum, float* d_d
     return fold_run(c, KIND_SECAGG, 0, n, true, fa, (hipStream_t)stream);
 }
 
+int pgh_secagg_device_range(pgh_ctx* c, int base, int prec, int64_t off, int64_t len, int64_t* d_sum, float* d_dec,
+                            void* stream) {
+    RC(check_dtype(c, PGH_I64));
+    DeviceGuard g(c->device);
+    int64_t n = 0;
+    RC(resident_count(c, &n));
+    FinalArgs fa;
+    fa.sum = d_sum;
+    fa.dec = d_dec;
+    fa.off = off;
+    fa.len = len;
+    RC(fixed_point_divisor(c, base, prec, &fa.divisor));
+    return fold_run(c, KIND_SECAGG, 0, n, true, fa, (hipStream_t)stream);
+}
+
 int pgh_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out) {
     RC(check_dtype(c, PGH_I64));
     DeviceGuard g(c->device);

@@ -208,6 +208,13 @@ class Engine:
                                                 C.c_void_p(d_dec or None), C.c_void_p(stream or None)),
                     "secagg_device")
 
+    def secagg_device_range(self, off: int, length: int, d_sum: int, d_dec: int, base: int = 10, prec: int = 3,
+                            stream: int = 0):
+        """Share sum + decode of the shard-relative param range [off, off + length) (off % 4 == 0)."""
+        self._check(self._lib.pgh_secagg_device_range(self._h, int(base), int(prec), int(off), int(length),
+                                                      C.c_void_p(d_sum or None), C.c_void_p(d_dec or None),
+                                                      C.c_void_p(stream or None)), "secagg_device_range")
+
     def synth_ckpt_device(self, seed: int, d_ckpt: int, stream: int = 0):
         self._check(self._lib.pgh_synth_ckpt_device(self._h, C.c_uint64(seed), C.c_void_p(d_ckpt),
                                                     C.c_void_p(stream or None)), "synth_ckpt_device")

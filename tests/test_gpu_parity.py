@@ -516,6 +516,32 @@ def test_reingest_waits_for_inflight_fold(engine):
     assert same(out2.cpu().numpy()[idx], coracle.fedavg(0, d2, c[idx]))
 
 
+def test_secagg_device_range_pieces_equal_whole(engine):
+    """Share sums + decodes of param ranges (the multi-GPU secagg overlap) equal one launch."""
+    import torch
+
+    from pygrid_amd.sharding import OverlappedGather
+
+    P, N, S = 300_007, 40, 2
+    engine.set_layout([P])
+    engine.reserve(N, 1, S)
+    engine.synth_fill(5, N)
+    s_whole = torch.empty(P, dtype=torch.int64, device="cuda")
+    d_whole = torch.empty(P, dtype=torch.float32, device="cuda")
+    engine.secagg_device(s_whole.data_ptr(), d_whole.data_ptr())
+    s_part = torch.full((P,), -1, dtype=torch.int64, device="cuda")
+    og = OverlappedGather(P, 1, 0, chunks=7)
+    lp = og.local.data_ptr()
+    og.run(lambda off, n, st: engine.secagg_device_range(off, n, s_part.data_ptr(), lp, 10, 3, st))
+    d_part = og.assemble()
+    torch.cuda.synchronize()
+    assert torch.equal(s_part, s_whole)
+    assert torch.equal(d_part.view(torch.int32), d_whole.view(torch.int32))
+    from pygrid_amd import AggregationError
+    with pytest.raises(AggregationError):
+        engine.secagg_device_range(6, 10, s_part.data_ptr(), lp)  # misaligned range
+
+
 def test_rccl_overlapped_gather_world1(engine):
     """The RCCL ("nccl" backend) all-gather path of OverlappedGather, forced at world size 1:
     async all_gather_into_tensor per fold range on the torch stream, wait, assemble."""
