@@ -70,21 +70,51 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(P: int, seed: int, budget_s: float, n: int = 32, all_cores: int = 16):
-    """The reference's hard-coded path as the node runs it -- cycle_manager.py:276-296 evaluated in
-    torch on CPU tensors (oracle.fedavg_mean_torch) at th.set_num_threads(1), the node's setting
-    (main/__init__.py:8) -- on a bounded sample: the same P-param shard, `n` synthetic clients,
-    repeated until `budget_s` of CPU work.  Also reported: the same at `all_cores` threads (the
-    GPU box's CPU share) and the numpy restatement (oracle.fedavg_mean) at 1 thread."""
+def cpu_baseline(kind: str, P: int, seed: int, budget_s: float, n: int = 32, all_cores: int = 16):
+    """The reference's path as the node runs it, in torch on CPU tensors at th.set_num_threads(1)
+    (the node's setting, main/__init__.py:8), on a bounded sample: the same P-param shard, `n`
+    synthetic clients, repeated until `budget_s` of CPU work.
+      mean       cycle_manager.py:276-296                (oracle.fedavg_mean_torch)
+      iterative  cycle_manager.py:266-269 + the plan     (oracle.fedavg_iterative_torch)
+      secagg     syft share adds + fix-prec decode       (oracle.secagg_sum_torch), 2 parties
+      weighted   no reference counterpart: the numpy oracle (oracle.fedavg_weighted)
+    Also reported: the same at `all_cores` threads (the GPU box's CPU share) and the numpy
+    restatement at 1 thread."""
+    import numpy as np
     import torch
 
     from oracle import coracle
     from oracle import oracle as O
 
-    diffs = [[coracle.synth_f32(seed, O.STREAM_DIFF, c, 0, P, float(O.DIFF_SCALE))] for c in range(n)]
-    ckpt = [coracle.synth_f32(seed, O.STREAM_CKPT, 0, 0, P, float(O.CKPT_SCALE))]
-    tdiffs = [[torch.from_numpy(t) for t in d] for d in diffs]
-    tckpt = [torch.from_numpy(t) for t in ckpt]
+    if kind == "secagg":
+        n = max(1, n // 4)
+        rng = np.random.default_rng(seed)
+        sh = [[rng.integers(-2**63, 2**63 - 1, P, dtype=np.int64, endpoint=True) for _ in range(2)] for _ in range(n)]
+        tsh = [[torch.from_numpy(x) for x in c] for c in sh]
+        sh_np = np.stack([np.stack(c) for c in sh])
+        unit_bytes = 8 * 2 * P
+        ref = lambda: O.secagg_sum_torch(tsh)  # noqa: E731
+        port = lambda: O.fix_prec_decode(O.secagg_sum(sh_np))  # noqa: E731
+        what = "syft share adds (torch int64 add, wrapping) + .float() / 10**3 decode (oracle.secagg_sum_torch)"
+    else:
+        diffs = [[coracle.synth_f32(seed, O.STREAM_DIFF, c, 0, P, float(O.DIFF_SCALE))] for c in range(n)]
+        ckpt = [coracle.synth_f32(seed, O.STREAM_CKPT, 0, 0, P, float(O.CKPT_SCALE))]
+        tdiffs = [[torch.from_numpy(t) for t in d] for d in diffs]
+        tckpt = [torch.from_numpy(t) for t in ckpt]
+        unit_bytes = 4 * P
+        w = np.linspace(0.5, 2.0, n).astype(np.float32)
+        if kind == "iterative":
+            ref = lambda: O.fedavg_iterative_torch(tckpt, tdiffs)  # noqa: E731
+            port = lambda: O.fedavg_iterative(ckpt, diffs)  # noqa: E731
+            what = "cycle_manager.py:266-269 + 01-Create-plan.ipynb:450-454 (oracle.fedavg_iterative_torch)"
+        elif kind == "weighted":
+            ref = None
+            port = lambda: O.fedavg_weighted(ckpt, diffs, w)  # noqa: E731
+            what = "no reference counterpart: numpy oracle (oracle.fedavg_weighted)"
+        else:
+            ref = lambda: O.fedavg_mean_torch(tckpt, tdiffs)  # noqa: E731
+            port = lambda: O.fedavg_mean(ckpt, diffs)  # noqa: E731
+            what = "cycle_manager.py:276-296 (oracle.fedavg_mean_torch)"
 
     def rate(fn, budget):
         fn()  # warm: allocator, thread pool after set_num_threads
@@ -94,24 +124,24 @@ def cpu_baseline(P: int, seed: int, budget_s: float, n: int = 32, all_cores: int
             reps += 1
             el = time.perf_counter() - t0
             if el >= budget:
-                return reps * n * P * 4 / el / 1e9, reps, el
+                return reps * n * unit_bytes / el / 1e9, reps, el
 
     threads = torch.get_num_threads()
     try:
         torch.set_num_threads(1)
-        gbs, reps, el = rate(lambda: O.fedavg_mean_torch(tckpt, tdiffs), budget_s * 0.5)
+        gbs, reps, el = rate(ref or port, budget_s * 0.5)
         torch.set_num_threads(all_cores)
-        gbs_all, _, _ = rate(lambda: O.fedavg_mean_torch(tckpt, tdiffs), budget_s * 0.25)
+        gbs_all, _, _ = rate(ref, budget_s * 0.25) if ref else (None, 0, 0)
     finally:
         torch.set_num_threads(threads)
-    gbs_np, _, _ = rate(lambda: O.fedavg_mean(ckpt, diffs), budget_s * 0.25)
+    gbs_np, _, _ = rate(port, budget_s * 0.25) if ref else (gbs, 0, 0)
+    close_1000 = lambda g: round(unit_bytes * 1000 / (g * 1e9) * 1e3, 1)  # noqa: E731
     return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"cycle_manager.py:276-296 in torch {torch.__version__} on CPU tensors "
-                      f"(oracle.fedavg_mean_torch), P={P}, {n} clients, {reps} passes in {el:.1f}s, 1 thread "
-                      f"(the node's th.set_num_threads(1))",
-            "cycle_close_ms_per_1000_clients": round(4 * 1000 * P / (gbs * 1e9) * 1e3, 1),
-            "all_cores": {"value": round(gbs_all, 3), "cores": all_cores,
-                          "cycle_close_ms_per_1000_clients": round(4 * 1000 * P / (gbs_all * 1e9) * 1e3, 1)},
+            "sample": f"{what}, {f'torch {torch.__version__} CPU tensors' if ref else 'numpy'}, P={P}, {n} clients, "
+                      f"{reps} passes in {el:.1f}s, 1 thread (the node's th.set_num_threads(1))",
+            "cycle_close_ms_per_1000_clients": close_1000(gbs),
+            "all_cores": ({"value": round(gbs_all, 3), "cores": all_cores,
+                           "cycle_close_ms_per_1000_clients": close_1000(gbs_all)} if gbs_all else None),
             "numpy_restatement_1_thread": round(gbs_np, 3), "cpu_model": cpu_model()}
 
 
@@ -285,9 +315,10 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
            "kernel_variant": eng.effective_variant(mode if dtype == 0 else 16)}
     rec = record(ctx, args, args.workload, value, el, dt, cfg,
                  roofline_of(st, args.workload, cfg["kernel_variant"], kernel))
-    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline and dtype == 0 and mode == 0:
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
+        kind = "secagg" if dtype == 1 else {0: "mean", 1: "iterative", 2: "weighted"}[mode]
         try:
-            rec["cpu_baseline"] = cpu_baseline(pg, args.seed, args.cpu_seconds)
+            rec["cpu_baseline"] = cpu_baseline(kind, pg, args.seed, args.cpu_seconds)
         except Exception as e:  # noqa: BLE001
             rec["cpu_baseline"] = {"error": str(e)}
     return rec

@@ -107,6 +107,23 @@ def fedavg_iterative(model_params, diffs):
     return out
 
 
+def fedavg_iterative_torch(model_params, diffs):
+    """The iterative branch as the node runs it, in torch on CPU tensors:
+    ``cycle_manager.py:266-269`` calling the plan of ``01-Create-plan.ipynb:450-454`` with
+    ``th.tensor([i + 1])`` (the plan's ops executed directly instead of through syft's Plan
+    interpreter, so this is a lower bound on the reference's time).  Bit-identical to
+    ``fedavg_iterative`` (``tests/test_oracle.py``)."""
+    import torch as th
+
+    def avg_plan(avg, item, num):
+        return [(a * num + i) / (num + 1) for a, i in zip(avg, item)]
+
+    diff_avg = diffs[0]
+    for i, diff in enumerate(diffs[1:]):
+        diff_avg = avg_plan(list(diff_avg), diff, th.tensor([i + 1]))
+    return [p - a for p, a in zip(model_params, diff_avg)]
+
+
 # ----------------------------------------------------------------------------------------
 # weighted FedAvg (north_star; no reference counterpart -- build-owned definition)
 # ----------------------------------------------------------------------------------------
@@ -163,6 +180,19 @@ def ready_to_average(server_config, received_diffs, cycle_end=None, now=None):
 # (a10) secure aggregation: PySyft 0.2.9 FixedPrecisionTensor + AdditiveSharingTensor
 # exercised at tests/data_centric/test_basic_syft_operations.py:388-454
 # ----------------------------------------------------------------------------------------
+
+
+def secagg_sum_torch(shares):
+    """The server-side share aggregation as torch runs it (syft's AdditiveSharingTensor ``add``
+    is a torch int64 add per share, wrapping): ``shares`` a list over clients of lists over
+    parties of int64 tensors; returns the int64 sum and its fixed-point decode
+    (``.float() / 10**3``).  Equal to ``secagg_sum`` / ``fix_prec_decode``."""
+    from functools import reduce
+
+    import torch as th
+
+    s = reduce(th.add, [sh for client in shares for sh in client])
+    return s, s.float() / 1000
 
 
 def fix_prec_encode(x, base=10, precision_fractional=3):

@@ -71,8 +71,19 @@ def test_oracle_matches_reference_expressions(n):
         assert same(got, want.numpy())
     for got, want in zip(O.fedavg_iterative(ckpt, diffs), ref_iterative(tc, td)):
         assert same(got, want.numpy())
-    for got, want in zip(O.fedavg_mean_torch(tc, td), ref_hardcoded(tc, td)):  # the bench's CPU leg
+    for got, want in zip(O.fedavg_mean_torch(tc, td), ref_hardcoded(tc, td)):  # the bench's CPU legs
         assert same(got.numpy(), want.numpy())
+    for got, want in zip(O.fedavg_iterative_torch(tc, td), ref_iterative(tc, td)):
+        assert same(got.numpy(), want.numpy())
+
+
+def test_secagg_torch_restatement_matches_oracle():
+    rng = np.random.default_rng(9)
+    sh = rng.integers(-2**63, 2**63 - 1, size=(5, 2, 300), dtype=np.int64, endpoint=True)
+    s, dec = O.secagg_sum_torch([[th.from_numpy(sh[c, p]) for p in range(2)] for c in range(5)])
+    want = O.secagg_sum(sh)
+    assert np.array_equal(s.numpy(), want)
+    assert np.array_equal(dec.numpy().view(np.uint32), O.fix_prec_decode(want).view(np.uint32))
 
 
 def test_oracle_matches_reference_on_edge_values():
