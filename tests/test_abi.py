@@ -3,7 +3,6 @@ the host-only State codec works without a GPU; the engine refuses to run without
 import re
 from pathlib import Path
 
-import numpy as np
 import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
