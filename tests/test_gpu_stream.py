@@ -207,3 +207,64 @@ def test_blocked_ring_small_staging(mode):
                 eng.ingest_state(k, build_state_fast(parts))
         got = eng.stream_finish(c)
     assert same(got, coracle.fedavg(mode, d, c))
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_config4_shard_full_size_sampled(engine, mode):
+    """BASELINE config 4, one GPU's shard at full size: 12.5 M params x 10,000 clients (500 GB of
+    diffs) through a 1,000-slot ring, generated on the GPU in 500-client chunks exactly like
+    `bench.py --workload c4-stream`; bit-exact on sampled params (block edges included) against
+    the oracle folding all 10,000 clients."""
+    import torch
+
+    P, N, R, chunk, seed = 12_500_000, 10_000, 1000, 500, 4242
+    engine.set_layout([P])
+    engine.reserve(R)
+    engine.stream_begin(mode, chunk)
+    for c0 in range(0, N, chunk):
+        engine.synth_ingest(seed, c0, min(chunk, N - c0))
+    ck = torch.empty(P, dtype=torch.float32, device="cuda")
+    out = torch.empty_like(ck)
+    engine.synth_ckpt_device(seed, ck.data_ptr())
+    engine.stream_finish_device(ck.data_ptr(), out.data_ptr())
+    torch.cuda.synchronize()
+    edges = np.array([k * 65536 + e for k in (1, 95, 190) for e in (-1, 0)])
+    idx = np.unique(np.concatenate([[0, 1], np.random.default_rng(mode).integers(0, P, 300), edges, [P - 1]]))
+    u = idx.astype(np.uint64)
+    d = np.stack([O.synth_diff(seed, k, u) for k in range(N)])
+    want = coracle.fedavg(mode, d, O.synth_ckpt(seed, u))
+    assert same(out.cpu().numpy()[idx], want)
+    engine.set_layout([1])  # release the ring
+
+
+def test_config5_shard_full_size_pinned_sampled(engine):
+    """BASELINE config 5, one GPU's shard at full size: 125 M params x 64 clients, iterative plan,
+    diffs DMA'd from page-locked host memory into an 8-slot ring, folded in pairs while the next
+    copies run (`bench.py --workload c5-ingest`); bit-exact on sampled params."""
+    import torch
+
+    from pygrid_amd import PinnedBuffer
+
+    P, N, R = 125_000_000, 64, 8
+    rng = np.random.default_rng(5)
+    bufs = [PinnedBuffer((P,)) for _ in range(4)]
+    try:
+        for b in bufs:
+            b.array[:] = rng.standard_normal(P, dtype=np.float32) * np.float32(1e-2)
+        engine.set_layout([P])
+        engine.reserve(R)
+        engine.stream_begin(1, 2)
+        for k in range(N):
+            engine.ingest(k, bufs[k % 4].array)
+        c = rng.standard_normal(P, dtype=np.float32)
+        ck = torch.from_numpy(c).cuda()
+        out = torch.empty_like(ck)
+        engine.stream_finish_device(ck.data_ptr(), out.data_ptr())
+        torch.cuda.synchronize()
+        idx = np.unique(np.concatenate([[0], rng.integers(0, P, 2000), [P - 1]]))
+        d = np.stack([bufs[k % 4].array[idx] for k in range(N)])
+        assert same(out.cpu().numpy()[idx], coracle.fedavg(1, d, c[idx]))
+    finally:
+        for b in bufs:
+            b.free()
+        engine.set_layout([1])
