@@ -10,7 +10,7 @@ timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
 rc=$?; echo "pytest rc=$rc"; tail -2 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
 for w in resnet18-iterative resnet18-weighted resnet18-secagg mnist-state; do
-  timeout -k 10 200 python bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_$w.json 2> $OUT/bench_$w.err || exit $?
+  timeout -k 10 200 python bench.py --workload $w --steps 10 --warmup 2 > $OUT/bench_$w.json 2> $OUT/bench_$w.err || exit $?
 done
 timeout -k 10 300 python bench.py --workload resnet18-state --steps 3 --warmup 1 > $OUT/bench_resnet18-state.json 2> $OUT/bench_resnet18-state.err || exit $?
 timeout -k 10 300 python bench.py --workload resnet18-report --steps 3 --warmup 1 > $OUT/bench_resnet18-report.json 2> $OUT/bench_resnet18-report.err || exit $?
