@@ -17,6 +17,9 @@ timeout -k 10 300 python bench.py --workload resnet18-report --steps 3 --warmup 
 timeout -k 10 300 python bench.py --workload c4-stream --steps 4 --warmup 1 > $OUT/bench_c4-stream.json 2> $OUT/bench_c4-stream.err || exit $?
 timeout -k 10 300 python bench.py --workload c5-ingest --steps 3 --warmup 1 > $OUT/bench_c5-ingest.json 2> $OUT/bench_c5-ingest.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 > $OUT/bench_resnet18-fedavg.json 2> $OUT/bench_trace.err || exit $?
+for w in resnet18-iterative resnet18-secagg; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_$w -o run --output-format csv -- python3 bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_trace_$w.json 2> $OUT/bench_trace_$w.err || exit $?
+done
 for w in resnet18-fedavg resnet18-iterative resnet18-weighted resnet18-secagg; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 200 rocprofv3 --pmc $c -d $OUT/pmc_${w}_$c -o run --output-format csv -- python3 bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmc_${w}_$c.log 2>&1 || exit $?
