@@ -94,18 +94,18 @@ class CycleAggregator:
         self._resident = None  # the checkpoint bytes object whose params are resident in HBM
 
     def _prepare(self, numel: Sequence[int], n: int, dtype: int = F32, parties: int = 1):
+        # the engine's own state is the truth: another user of the same engine may have changed it
         eng = self.engine
         numel = tuple(int(x) for x in numel)
-        if numel != self._numel:
+        if numel != tuple(eng.numel) or numel != self._numel:  # (a new aggregator always lays out)
             eng.set_layout(numel)
-            self._numel, self._cap, self._dtype = numel, 0, None
             self._resident = None
-        if n > self._cap or dtype != self._dtype or parties != self._parties:
+        if n > eng.max_clients or dtype != eng.dtype or (dtype != F32 and parties != eng.parties):
             eng.reserve(max(n, 1), dtype, parties)
-            self._cap, self._dtype, self._parties = max(n, 1), dtype, parties
             self._resident = None
         else:
             eng.reset()
+        self._numel, self._cap, self._dtype, self._parties = numel, eng.max_clients, dtype, parties
 
     # ---- bytes in / bytes out: the replaceable slice cycle_manager.py:240-303 -------------------
     def average_plan_diffs(self, server_config: dict, checkpoint: bytes, diffs: Sequence[bytes],
@@ -115,13 +115,14 @@ class CycleAggregator:
         mode = select_mode(server_config, avg_plan, weights)
         numel = state_codec.tensor_numels(checkpoint)  # :240
         self._prepare(numel, len(diffs))
-        if checkpoint is not self._resident:  # the last cycle's output is still in HBM
-            self.engine.ckpt_upload_state(checkpoint)
+        if checkpoint is not self._resident or self.engine.ckpt_owner is not self:
+            self.engine.ckpt_upload_state(checkpoint)  # else: the last cycle's output is still in HBM
         for i, d in enumerate(diffs):  # :247-250
             self.engine.ingest_state(i, d)
         if mode == WEIGHTED_MEAN:
             self.engine.set_weights(weights)
         self.engine.fedavg_resident(mode)  # :252-296
+        self.engine.ckpt_owner = self
         new = self.engine.ckpt_patch_state(checkpoint)  # :303
         self._resident = new
         return new

@@ -76,6 +76,9 @@ class Engine:
         self.dtype = F32
         self.parties = 1
         self.max_clients = 0
+        # Who put the current resident checkpoint in HBM (CycleAggregator / IncrementalCycle): any
+        # call that overwrites it resets this, so a holder re-uploads instead of trusting stale bytes.
+        self.ckpt_owner = None
 
     # ---- plumbing ----------------------------------------------------------------------------
     def _check(self, rc: int, what: str):
@@ -113,17 +116,20 @@ class Engine:
         self.P = sum(self.numel)
         self.lo, self.hi = 0, self.P
         self.max_clients = 0  # the slab was freed
+        self.ckpt_owner = None
 
     def set_shard(self, lo: int, hi: int):
         self._check(self._lib.pgh_set_shard(self._h, int(lo), int(hi)), "set_shard")
         self.lo, self.hi = int(lo), int(hi)
         self.max_clients = 0
+        self.ckpt_owner = None
 
     def reserve(self, max_clients: int, dtype: int = F32, n_parties: int = 1):
         self._check(self._lib.pgh_reserve(self._h, int(max_clients), int(dtype), int(n_parties)), "reserve")
         self.dtype = dtype
         self.parties = 1 if dtype == F32 else int(n_parties)
         self.max_clients = int(max_clients)
+        self.ckpt_owner = None
 
     def reset(self):
         self._check(self._lib.pgh_reset(self._h), "reset")
@@ -159,6 +165,7 @@ class Engine:
         if c.size != self.p_shard:
             raise AggregationError(f"checkpoint has {c.size} params, shard has {self.p_shard}")
         out = np.empty_like(c)
+        self.ckpt_owner = None  # the host checkpoint is staged through the resident one
         self._check(self._lib.pgh_fedavg(self._h, int(mode), _ptr(c), _ptr(out)), "fedavg")
         return out
 
@@ -175,9 +182,11 @@ class Engine:
     # ---- resident checkpoint ---------------------------------------------------------------------
     def ckpt_upload(self, ckpt: np.ndarray):
         a = np.ascontiguousarray(ckpt, dtype=np.float32).reshape(-1)
+        self.ckpt_owner = None
         self._check(self._lib.pgh_ckpt_upload(self._h, _ptr(a), a.nbytes), "ckpt_upload")
 
     def ckpt_upload_state(self, pb: bytes):
+        self.ckpt_owner = None
         self._check(self._lib.pgh_ckpt_upload_state(self._h, pb, len(pb)), "ckpt_upload_state")
 
     def fedavg_resident(self, mode: int):
@@ -216,6 +225,7 @@ class Engine:
                                                       C.c_void_p(stream or None)), "secagg_device_range")
 
     def synth_ckpt_device(self, seed: int, d_ckpt: int, stream: int = 0):
+        self.ckpt_owner = None  # may stage through the resident checkpoint
         self._check(self._lib.pgh_synth_ckpt_device(self._h, C.c_uint64(seed), C.c_void_p(d_ckpt),
                                                     C.c_void_p(stream or None)), "synth_ckpt_device")
 
@@ -231,6 +241,7 @@ class Engine:
         if c.size != self.p_shard:
             raise AggregationError(f"checkpoint has {c.size} params, shard has {self.p_shard}")
         out = np.empty_like(c)
+        self.ckpt_owner = None
         self._check(self._lib.pgh_stream_finish(self._h, _ptr(c), _ptr(out)), "stream_finish")
         return out
 

@@ -51,6 +51,7 @@ class IncrementalCycle:
         self._ckpt: Optional[bytes] = None  # checkpoint bytes whose payloads are resident in HBM
         if checkpoint is not None:
             engine.ckpt_upload_state(checkpoint)
+            engine.ckpt_owner = self
             self._ckpt = checkpoint
 
     def assigned(self, worker):
@@ -91,9 +92,10 @@ class IncrementalCycle:
         self._advance(final=True)
         if self._next_client == 0:
             raise AggregationError("no diffs to average")
-        if checkpoint is not self._ckpt:
+        if checkpoint is not self._ckpt or getattr(self.engine, "ckpt_owner", None) is not self:
             self.engine.ckpt_upload_state(checkpoint)  # scan + staged H2D of the payload spans
         self.engine.stream_finish_resident()
+        self.engine.ckpt_owner = self
         self._ckpt = None  # HBM now holds the NEW checkpoint
         return self.engine.ckpt_patch_state(checkpoint)
 

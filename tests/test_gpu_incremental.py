@@ -47,3 +47,34 @@ def test_incremental_cycle_matches_reference_order(engine, mode, ckpt_at_start):
     for got, w in zip(parse_state(new), want):
         assert np.array_equal(bits(got), bits(w))
     assert inc.n_folded == len(reporters)
+
+
+def test_shared_engine_resident_checkpoint_is_not_trusted_after_another_user(engine):
+    """CycleAggregator keeps its last output checkpoint in HBM for the next cycle; if another
+    user of the same engine (here an IncrementalCycle) replaced it meanwhile, the aggregator must
+    upload the checkpoint again instead of folding into someone else's."""
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(90)
+    shapes = [(40, 9), (9,)]
+    numel = [int(np.prod(s)) for s in shapes]
+    mk = lambda scale: [(rng.standard_normal(s) * scale).astype(F) for s in shapes]  # noqa: E731
+    agg = CycleAggregator(engine)
+    ck0 = mk(1.0)
+    d1 = [mk(1e-2) for _ in range(3)]
+    new1 = agg.average_plan_diffs({}, build_state_fast(ck0), [build_state_fast(d) for d in d1])
+    want1 = O.fedavg_mean(ck0, d1)
+    # someone else uses the engine in between
+    other_ck = mk(1.0)
+    inc = IncrementalCycle(engine, numel, ring_slots=4, fold_batch=2, checkpoint=build_state_fast(other_ck))
+    inc.assigned(0)
+    inc.reported(0, build_state_fast(mk(1e-2)))
+    inc.close(build_state_fast(other_ck))
+    # the aggregator's next cycle starts from ITS checkpoint (new1), not the incremental result
+    d2 = [mk(1e-2) for _ in range(2)]
+    new2 = agg.average_plan_diffs({}, new1, [build_state_fast(d) for d in d2])
+    want2 = O.fedavg_mean(want1, d2)
+    for got, w in zip(parse_state(new2), want2):
+        assert np.array_equal(bits(got), bits(w))
