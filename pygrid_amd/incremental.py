@@ -15,6 +15,11 @@ has already reported.  ``IncrementalCycle`` keeps that rule:
   incomplete rows), folds the parked diffs in id order, and returns the new checkpoint bytes --
   bit-identical to folding everything at close time.
 
+Thread safety: the node calls ``reported`` from request handlers and ``close`` from its executor
+thread (``tasks/cycle.py``), so every method holds the cycle's lock (the engine context itself is
+single-owner).  A report that arrives after ``close`` started raises ``AggregationError`` -- the
+reference likewise averages only the diffs its query saw (``cycle_manager.py:243-245``).
+
 The checkpoint can be handed over when the cycle starts (``checkpoint=``): its payloads are then
 uploaded into HBM while clients report, and ``close`` only folds the last partial batch into it
 and patches the new State bytes from HBM -- O(P) work after the last report instead of the
@@ -22,6 +27,7 @@ reference's N + 1 unserializations and N-way fold.
 """
 from __future__ import annotations
 
+import threading
 from typing import Dict, List, Optional
 
 from .engine import F32, MEAN, Engine
@@ -42,6 +48,8 @@ class IncrementalCycle:
         self._weights_by_worker = weights_by_worker
         self._weights: List[float] = []
         self.folded_early = 0
+        self._lock = threading.Lock()
+        self._closed = False
         # keep the engine's ring when a cycle of the same model follows (no re-allocation)
         if tuple(getattr(engine, "numel", ())) != tuple(int(n) for n in numel) or \
                 getattr(engine, "max_clients", 0) != ring_slots or getattr(engine, "dtype", None) != F32:
@@ -55,19 +63,23 @@ class IncrementalCycle:
             self._ckpt = checkpoint
 
     def assigned(self, worker):
-        if worker in self._pos:
-            return
-        self._pos[worker] = len(self._order)
-        self._order.append(worker)
+        with self._lock:
+            if worker in self._pos:
+                return
+            self._pos[worker] = len(self._order)
+            self._order.append(worker)
 
     def reported(self, worker, diff: bytes):
-        if worker not in self._pos:
-            raise AggregationError(f"worker {worker!r} reported without being assigned to the cycle")
-        if worker in self._reported:
-            raise AggregationError(f"worker {worker!r} reported twice")
-        self._reported.add(worker)
-        self._parked[worker] = diff
-        self._advance(final=False)
+        with self._lock:
+            if self._closed:
+                raise AggregationError(f"worker {worker!r} reported after the cycle closed")
+            if worker not in self._pos:
+                raise AggregationError(f"worker {worker!r} reported without being assigned to the cycle")
+            if worker in self._reported:
+                raise AggregationError(f"worker {worker!r} reported twice")
+            self._reported.add(worker)
+            self._parked[worker] = diff
+            self._advance(final=False)
 
     def _ingest(self, worker):
         if self._weights_by_worker is not None:
@@ -89,15 +101,19 @@ class IncrementalCycle:
 
     def close(self, checkpoint: bytes) -> bytes:
         """New checkpoint bytes (``cycle_manager.py:293-303``)."""
-        self._advance(final=True)
-        if self._next_client == 0:
-            raise AggregationError("no diffs to average")
-        if checkpoint is not self._ckpt or getattr(self.engine, "ckpt_owner", None) is not self:
-            self.engine.ckpt_upload_state(checkpoint)  # scan + staged H2D of the payload spans
-        self.engine.stream_finish_resident()
-        self.engine.ckpt_owner = self
-        self._ckpt = None  # HBM now holds the NEW checkpoint
-        return self.engine.ckpt_patch_state(checkpoint)
+        with self._lock:
+            if self._closed:
+                raise AggregationError("cycle already closed")
+            self._closed = True
+            self._advance(final=True)
+            if self._next_client == 0:
+                raise AggregationError("no diffs to average")
+            if checkpoint is not self._ckpt or getattr(self.engine, "ckpt_owner", None) is not self:
+                self.engine.ckpt_upload_state(checkpoint)  # scan + staged H2D of the payload spans
+            self.engine.stream_finish_resident()
+            self.engine.ckpt_owner = self
+            self._ckpt = None  # HBM now holds the NEW checkpoint
+            return self.engine.ckpt_patch_state(checkpoint)
 
     @property
     def n_folded(self) -> int:

@@ -120,3 +120,28 @@ def test_errors():
     inc2.assigned("b")
     with pytest.raises(AggregationError):
         inc2.close(b"")
+
+
+def test_reports_from_many_threads_and_a_late_one():
+    """Request threads report concurrently (the node's handlers); folds still follow assignment
+    order exactly once each, and a report after close is refused."""
+    import threading
+
+    eng = RecordingEngine()
+    inc = IncrementalCycle(eng, [3], checkpoint=b"ck")
+    workers = list(range(64))
+    for w in workers:
+        inc.assigned(w)
+    rng = np.random.default_rng(4)
+    order = [int(w) for w in rng.permutation(workers)]
+    threads = [threading.Thread(target=inc.reported, args=(w, bytes([w]))) for w in order]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert ingests(eng) == [(k, bytes([k])) for k in range(64)]
+    inc.close(b"ck")
+    with pytest.raises(AggregationError):
+        inc.reported(0, b"late")
+    with pytest.raises(AggregationError):
+        inc.close(b"ck")
