@@ -7,6 +7,7 @@ constructed without the library and a visible GPU (``EngineUnavailableError``).
 from __future__ import annotations
 
 import ctypes as C
+import threading
 from typing import Optional, Sequence, Tuple
 
 import numpy as np
@@ -59,9 +60,25 @@ class PinnedBuffer:
             pass
 
 
+class _Serialized:
+    """The library with every call made under one lock: a context is single-owner, and ctypes
+    releases the GIL, so two Python threads sharing an Engine would otherwise enter it together."""
+
+    def __init__(self, lib, lock):
+        self._l, self._m = lib, lock
+
+    def __getattr__(self, name):
+        fn = getattr(self._l, name)
+
+        def call(*args):
+            with self._m:
+                return fn(*args)
+        return call
+
+
 class Engine:
     def __init__(self, device: int = 0, pinned_bytes: int = 0):
-        self._lib = _lib.load()
+        self._lib = _Serialized(_lib.load(), threading.RLock())
         h = C.c_void_p()
         rc = self._lib.pgh_create(int(device), int(pinned_bytes), C.byref(h))
         if rc != 0:
