@@ -159,6 +159,7 @@ struct pgh_ctx {
     int bshift = 62;
     int64_t bmask = 0;
     size_t block_bytes = 256u << 10;  // PGH_BLOCK_BYTES; 0 = one block (plain row-major rows)
+    int64_t synth_wgs = 8192;  // PGH_SYNTH_WGS: STREAM synthetic fill grid cap (0 = a grid row per row; r01t)
 
     int slots = 0, dtype = PGH_F32, parties = 1;
     void* d_slab = nullptr;
@@ -853,6 +854,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_COPY_THREADS")) c->copy_threads = std::max(1, std::atoi(e));
     c->pool_copy.reset(new CopyPool(c->copy_threads));
     if (const char* e = std::getenv("PGH_REGISTER_INGEST")) c->register_ingest = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PGH_SYNTH_WGS")) c->synth_wgs = std::max(0LL, std::atoll(e));
     if (const char* e = std::getenv("PGH_BLOCK_BYTES")) c->block_bytes = (size_t)std::max(0LL, std::atoll(e));
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
@@ -1068,7 +1070,8 @@ int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
         hipError_t e;
         if (c->dtype == PGH_F32)
             e = pgh::launch_synth_f32((float*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->pg, seed,
-                                      pgh::STREAM_DIFF, client, c->lo, pgh::DIFF_SCALE, c->copy);
+                                      pgh::STREAM_DIFF, client, c->lo, pgh::DIFF_SCALE, c->copy,
+                                      c->streaming ? c->synth_wgs : 0);
         else
             e = pgh::launch_synth_shares((int64_t*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->parties,
                                          c->pg, seed, client, c->lo, 1000.0f, c->copy);

@@ -68,7 +68,8 @@ int auto_variant(int64_t p, int mode);
 // Deterministic synthetic inputs (restated bit for bit by oracle/oracle.py).  `out` is the
 // slab (or a [p] vector: single_block) at its first row; params [p, ncols) are zero-filled.
 hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_rows, int64_t p, uint64_t seed,
-                            uint64_t stream_id, int64_t row0, int64_t idx0, float scale, hipStream_t s);
+                            uint64_t stream_id, int64_t row0, int64_t idx0, float scale, hipStream_t s,
+                            int64_t max_wgs = 0);  // > 0: cap the grid at max_wgs workgroups
 hipError_t launch_synth_shares(int64_t* out, const SlabMap& m, int64_t ncols, int n_clients, int n_parties,
                                int64_t p, uint64_t seed, int64_t client0, int64_t idx0, float enc_scale,
                                hipStream_t s);

@@ -21,6 +21,8 @@
 // denormals kept, IEEE (correctly rounded) f32 division.
 #include "pgh_kernels.h"
 
+#include <algorithm>
+
 namespace pgh {
 namespace {
 
@@ -311,19 +313,24 @@ __global__ __launch_bounds__(TB) void k_secagg(SecaggArgs a, int64_t ncol) {
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_synth_f32(float* out, SlabMap m, int64_t ncols, int64_t p, uint64_t seed,
-                                                     uint64_t stream_id, int64_t row0, int64_t idx0, float scale) {
-    const int64_t r = blockIdx.y;
-    const uint64_t key = row_key(seed, stream_id, (uint64_t)(row0 + r));
-    float* row = out + (size_t)r * m.ld;
-    for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < ncols / 4; q += (int64_t)gridDim.x * BLOCK) {
-        f32x4 v;
+__global__ __launch_bounds__(BLOCK) void k_synth_f32(float* out, SlabMap m, int64_t ncols, int n_rows, int64_t p,
+                                                     uint64_t seed, uint64_t stream_id, int64_t row0, int64_t idx0,
+                                                     float scale) {
+    for (int64_t r = blockIdx.y; r < n_rows; r += gridDim.y) {
+        const uint64_t key = row_key(seed, stream_id, (uint64_t)(row0 + r));
+        float* row = out + (size_t)r * m.ld;
+        for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < ncols / 4; q += (int64_t)gridDim.x * BLOCK) {
+            f32x4 v;
+            const uint64_t k0 = key + (uint64_t)(idx0 + 4 * q);
+            if (4 * q + 4 <= p) {  // branch-free: four independent hash chains interleave
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int64_t i = 4 * q + e;
-            v[e] = (i < p) ? bits_to_f32(sm64(key + (uint64_t)(idx0 + i)), scale) : 0.f;
+                for (int e = 0; e < 4; ++e) v[e] = bits_to_f32(sm64(k0 + (uint64_t)e), scale);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = (4 * q + e < p) ? bits_to_f32(sm64(k0 + (uint64_t)e), scale) : 0.f;
+            }
+            *reinterpret_cast<f32x4*>(row + m.at(4 * q)) = v;  // 4 params never straddle a block
         }
-        *reinterpret_cast<f32x4*>(row + m.at(4 * q)) = v;  // 4 params never straddle a block
     }
 }
 
@@ -530,15 +537,21 @@ hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_rows, int64_t p, uint64_t seed,
-                            uint64_t stream_id, int64_t row0, int64_t idx0, float scale, hipStream_t s) {
+                            uint64_t stream_id, int64_t row0, int64_t idx0, float scale, hipStream_t s,
+                            int64_t max_wgs) {
     if (!out || n_rows < 0 || n_rows > 65535 || ncols < p || (ncols & 3) || m.off != 0 || !valid_map(m, 0) ||
         (m.bshift == 62 && ncols > m.ld) || (reinterpret_cast<uintptr_t>(out) & 15))
         return hipErrorInvalidValue;
     if (n_rows == 0 || ncols == 0) return hipSuccess;
     int64_t gx = (ncols / 4 + BLOCK - 1) / BLOCK;
     if (gx > 1024) gx = 1024;
-    k_synth_f32<<<dim3((unsigned)gx, (unsigned)n_rows), BLOCK, 0, s>>>(out, m, ncols, p, seed, stream_id, row0, idx0,
-                                                                      scale);
+    int64_t gy = n_rows;
+    if (max_wgs > 0) {  // bounded grid: rows strided, leaves CU slots to a fold running beside it
+        if (gx > max_wgs) gx = max_wgs;
+        gy = std::max<int64_t>(1, std::min<int64_t>(n_rows, max_wgs / gx));
+    }
+    k_synth_f32<<<dim3((unsigned)gx, (unsigned)gy), BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id, row0,
+                                                                  idx0, scale);
     return hipGetLastError();
 }
 
