@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define PGH_ABI_VERSION 2
+#define PGH_ABI_VERSION 3
 
 typedef struct pgh_ctx pgh_ctx;
 
@@ -65,6 +65,8 @@ typedef struct {
     int64_t n_folded;          /* stream mode: clients folded into the running state */
     int32_t n_clients;         /* clients ingested since the last reset */
     int32_t max_clients;       /* slab capacity (slots) */
+    double kernel_busy_ms_total;/* union of the timed launches' [start, end] intervals: launches
+                                 * running concurrently on several streams count once */
 } pgh_stats_t;
 
 /* ---- context lifecycle ------------------------------------------------------------------ */
@@ -142,6 +144,14 @@ int pgh_secagg_device(pgh_ctx* ctx, int base, int prec, int64_t* d_sum, float* d
  * shard-sized outputs, of which only that range is written (multi-GPU gather overlap). */
 int pgh_secagg_device_range(pgh_ctx* ctx, int base, int prec, int64_t off, int64_t len, int64_t* d_sum,
                             float* d_dec, void* stream);
+/* Decode only: d_dec[i] = float32(int64 d_sum[i]) / base**prec for i < n, on `stream` (device
+ * pointers; needs no slab).  Client-sharded secure aggregation: every rank sums the shares of its
+ * own clients (pgh_secagg_device with d_dec = NULL), the [P] sums are reduce-scattered with an
+ * int64 SUM (wrap-add is associative: exact), and each rank decodes its param shard here -- the
+ * same expression as pgh_secagg's decode.  Replaces the decode half of PySyft 0.2.9's
+ * FixedPrecisionTensor.float_precision (test_basic_syft_operations.py:417-424). */
+int pgh_secagg_decode_device(pgh_ctx* ctx, int base, int prec, const int64_t* d_sum, int64_t n, float* d_dec,
+                             void* stream);
 /* Fill a device buffer with the synthetic checkpoint of this shard (P_shard floats). */
 int pgh_synth_ckpt_device(pgh_ctx* ctx, uint64_t seed, float* d_ckpt, void* stream);
 

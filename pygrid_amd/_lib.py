@@ -33,6 +33,7 @@ class Stats(C.Structure):
         ("n_folded", C.c_int64),
         ("n_clients", C.c_int32),
         ("max_clients", C.c_int32),
+        ("kernel_busy_ms_total", C.c_double),
     ]
 
 
@@ -81,6 +82,7 @@ SIGNATURES = {
     "pgh_secagg": (_i, [_vp, _i, _i, _vp, _vp]),
     "pgh_secagg_device": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "pgh_secagg_device_range": (_i, [_vp, _i, _i, _i64, _i64, _vp, _vp, _vp]),
+    "pgh_secagg_decode_device": (_i, [_vp, _i, _i, _vp, _i64, _vp, _vp]),
     "pgh_synth_ckpt_device": (_i, [_vp, _u64, _vp, _vp]),
     "pgh_stream_begin": (_i, [_vp, _i, _i]),
     "pgh_stream_flush": (_i, [_vp]),
@@ -101,6 +103,7 @@ SIGNATURES = {
     "pgh_b64_decode": (_i, [C.c_char_p, _sz, _vp, C.POINTER(_sz), _i]),
 }
 
+ABI_VERSION = 3  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
 _LIB = None
 
 
@@ -122,5 +125,8 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.pgh_abi_version() != ABI_VERSION:
+        raise EngineUnavailableError(f"{LIB_PATH.name} has ABI {lib.pgh_abi_version()}, this package needs "
+                                     f"{ABI_VERSION}: rebuild it (python -m pygrid_amd.build)")
     _LIB = lib
     return lib

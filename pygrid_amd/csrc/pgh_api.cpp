@@ -357,10 +357,15 @@ hipEvent_t take_event(pgh_ctx* c) {
 }
 
 int collect_timings(pgh_ctx* c) {
+    // busy time: union of the launches' intervals, placed on one clock relative to the first start
+    std::vector<std::pair<double, double>> iv;
+    iv.reserve(c->pending.size());
     for (auto& t : c->pending) {
         CK(c, hipEventSynchronize(t.b));
-        float ms = 0.f;
+        float ms = 0.f, t0 = 0.f;
         CK(c, hipEventElapsedTime(&ms, t.a, t.b));
+        CK(c, hipEventElapsedTime(&t0, c->pending.front().a, t.a));
+        iv.push_back({(double)t0, (double)t0 + ms});
         c->st.kernel_ms_last = ms;
         c->st.kernel_ms_total += ms;
         c->st.kernel_launches += 1;
@@ -370,6 +375,16 @@ int collect_timings(pgh_ctx* c) {
         c->pool.push_back(t.b);
     }
     c->pending.clear();
+    std::sort(iv.begin(), iv.end());
+    double busy = 0, lo = 0, hi = 0;
+    bool open = false;
+    for (auto& x : iv) {
+        if (open && x.first <= hi) { hi = std::max(hi, x.second); continue; }
+        if (open) busy += hi - lo;
+        lo = x.first; hi = x.second; open = true;
+    }
+    if (open) busy += hi - lo;
+    c->st.kernel_busy_ms_total += busy;
     return PGH_OK;
 }
 
@@ -1287,6 +1302,20 @@ int pgh_secagg_device_range(pgh_ctx* c, int base, int prec, int64_t off, int64_t
     fa.len = len;
     RC(fixed_point_divisor(c, base, prec, &fa.divisor));
     return fold_run(c, KIND_SECAGG, 0, n, true, fa, (hipStream_t)stream);
+}
+
+int pgh_secagg_decode_device(pgh_ctx* c, int base, int prec, const int64_t* d_sum, int64_t n, float* d_dec,
+                             void* stream) {
+    if (!c) return fail(nullptr, PGH_E_ARG, "null context");
+    if (n < 0 || (n > 0 && (!d_sum || !d_dec))) return fail(c, PGH_E_ARG, "bad decode arguments (n=%lld)", (long long)n);
+    DeviceGuard g(c->device);
+    float div = 1.f;
+    RC(fixed_point_divisor(c, base, prec, &div));
+    const hipStream_t s = (hipStream_t)stream;
+    // not in pgh_stats' kernel timings: those stay the share-sum / fold kernels' (12 B per param here)
+    const hipError_t e = pgh::launch_secagg_decode(d_sum, d_dec, n, div, s);
+    if (e != hipSuccess) return fail(c, PGH_E_HIP, "decode launch failed: %s", hipGetErrorString(e));
+    return PGH_OK;
 }
 
 int pgh_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out) {

@@ -313,6 +313,14 @@ __global__ __launch_bounds__(TB) void k_secagg(SecaggArgs a, int64_t ncol) {
     }
 }
 
+// Decode of an already-summed Z_2^64 vector (client-sharded secagg: the per-rank share sums are
+// reduce-scattered, then each rank decodes its param shard).  Same expression as k_secagg's
+// FINAL epilogue, compiled with the same flags: bit-identical to the single-GPU decode.
+__global__ __launch_bounds__(BLOCK) void k_secagg_decode(const int64_t* sum, float* dec, int64_t n, float divisor) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK)
+        dec[i] = (float)sum[i] / divisor;
+}
+
 __global__ __launch_bounds__(BLOCK) void k_synth_f32(float* out, SlabMap m, int64_t ncols, int n_rows, int64_t p,
                                                      uint64_t seed, uint64_t stream_id, int64_t row0, int64_t idx0,
                                                      float scale) {
@@ -552,6 +560,15 @@ hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_r
     }
     k_synth_f32<<<dim3((unsigned)gx, (unsigned)gy), BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id, row0,
                                                                   idx0, scale);
+    return hipGetLastError();
+}
+
+hipError_t launch_secagg_decode(const int64_t* sum, float* dec, int64_t n, float divisor, hipStream_t s) {
+    if (n < 0 || (n > 0 && (!sum || !dec))) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    int64_t g = (n + BLOCK - 1) / BLOCK;
+    if (g > 8192) g = 8192;
+    k_secagg_decode<<<(unsigned)g, BLOCK, 0, s>>>(sum, dec, n, divisor);
     return hipGetLastError();
 }
 

@@ -241,6 +241,13 @@ class Engine:
                                                       C.c_void_p(d_sum or None), C.c_void_p(d_dec or None),
                                                       C.c_void_p(stream or None)), "secagg_device_range")
 
+    def secagg_decode_device(self, d_sum: int, n: int, d_dec: int, base: int = 10, prec: int = 3, stream: int = 0):
+        """d_dec[:n] = float32(int64 d_sum[:n]) / base**prec (client-sharded secagg, after the
+        cross-rank reduce-scatter of the share sums)."""
+        self._check(self._lib.pgh_secagg_decode_device(self._h, int(base), int(prec), C.c_void_p(d_sum or None),
+                                                       int(n), C.c_void_p(d_dec or None),
+                                                       C.c_void_p(stream or None)), "secagg_decode_device")
+
     def synth_ckpt_device(self, seed: int, d_ckpt: int, stream: int = 0):
         self.ckpt_owner = None  # may stage through the resident checkpoint
         self._check(self._lib.pgh_synth_ckpt_device(self._h, C.c_uint64(seed), C.c_void_p(d_ckpt),

@@ -8,6 +8,12 @@ split across ranks on the fp32 path (that would reorder the sum).
 The only collective is the all-gather of the new checkpoint's shards (the node serializes one
 checkpoint; ``cycle_manager.py:303-304``): one ``all_gather`` of equal padded shards over
 RCCL/xGMI (``torch.distributed`` backend "nccl"), or gloo on CPU in tests.
+
+Secure aggregation may instead shard the CLIENTS (``client_bounds``): each rank sums the shares
+of its own clients over the whole parameter vector, the int64 sums are reduce-scattered (SUM,
+wrap-around: addition mod 2^64 is associative and commutative, so any client split is exact),
+each rank decodes its part and the decoded vector is all-gathered (``OverlappedReduceScatter``).
+That is the layout when each GPU ingests a different subset of clients over its own PCIe link.
 """
 from __future__ import annotations
 
@@ -126,6 +132,100 @@ class OverlappedGather:
                     grid[:, a:b].copy_(r.view(self.world, b - a))
                 else:
                     grid[:, a:b].copy_(self.local[a:b].view(1, b - a))
+        for st in self.side:
+            main.wait_stream(st)
+
+    def assemble(self):
+        return self.out[: self.P]
+
+
+def client_bounds(N: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous client range of ``rank`` when clients are sharded (secure aggregation only)."""
+    if not (0 <= rank < world) or N < 0:
+        raise ValueError(f"bad client shard request N={N} world={world} rank={rank}")
+    q, r = divmod(N, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+class OverlappedReduceScatter:
+    """Client-sharded secure aggregation across ranks, pipelined over param ranges.
+
+    Every rank holds the shares of its own clients for the whole parameter vector (length P).
+    The vector is cut into ranges whose length is a multiple of ``world * align``; for range
+    ``[a, b)``, on alternating streams:
+
+    1. ``sum_range(a, n, stream)`` writes the rank's Z_2^64 share sum of ``[a, a + n)`` into
+       ``self.sums[a:a + n]`` (the engine's ``secagg_device_range`` with no decode; ``stream`` is
+       a HIP stream handle, or None on CPU);
+    2. ``reduce_scatter_tensor`` (int64 SUM, wraps mod 2^64) leaves rank r the total of the
+       r-th ``(b - a) / world`` slice of the range;
+    3. ``decode(total, dec, stream)`` decodes that slice (int64 tensor -> float32 tensor of the
+       same length; ``secagg_decode_device``);
+    4. ``all_gather_into_tensor`` puts the decoded slices of every rank back in range order,
+       straight into ``self.out[a:b]``.
+
+    Range i's collectives run beside the share sum of range i + 1.  ``self.out[:P]`` is the
+    decoded vector (bit-identical to one GPU summing every client), ``self.total`` holds this
+    rank's reduced int64 slices (range by range).  ``sums`` tail past P stays zero.
+    """
+
+    def __init__(self, P: int, world: int, rank: int, chunks: int = 8, device="cuda", group=None,
+                 align: int = ALIGN, streams: int = 2):
+        import torch
+
+        self.P, self.world, self.rank, self.group = P, world, rank, group
+        unit = world * align
+        c = -(-P // max(1, chunks))
+        c = -(-c // unit) * unit
+        self.L = -(-P // c) * c
+        self.ranges = [(a, a + c) for a in range(0, self.L, c)]
+        self.sums = torch.zeros(self.L, dtype=torch.int64, device=device)
+        self.total = torch.empty(self.L // world, dtype=torch.int64, device=device)
+        self.dec = torch.empty(self.L // world, dtype=torch.float32, device=device)
+        self.out = torch.empty(self.L, dtype=torch.float32, device=device)
+        self.cuda = self.sums.device.type == "cuda"
+        self.side = [torch.cuda.Stream(device=self.sums.device) for _ in range(max(0, streams - 1))] \
+            if self.cuda else []
+
+    def run(self, sum_range, decode, force_collective: bool = False):
+        import contextlib
+
+        import torch
+        import torch.distributed as dist
+
+        collective = self.world > 1 or force_collective
+        main = torch.cuda.current_stream(self.sums.device) if self.cuda else None
+        streams = [main] + self.side
+        for st in self.side:
+            st.wait_stream(main)
+        nccl = collective and self.cuda and dist.get_backend(self.group) == "nccl"
+        for i, (a, b) in enumerate(self.ranges):
+            st = streams[i % len(streams)]
+            h = st.cuda_stream if st is not None else None
+            m = (b - a) // self.world
+            t, d = self.total[a // self.world: a // self.world + m], self.dec[a // self.world: a // self.world + m]
+            with torch.cuda.stream(st) if st is not None else contextlib.nullcontext():
+                n = min(b, self.P) - a
+                if n > 0:
+                    sum_range(a, n, h)
+                if collective:
+                    if nccl:
+                        dist.reduce_scatter_tensor(t, self.sums[a:b], group=self.group, async_op=True).wait()
+                    else:
+                        dist.reduce_scatter(t, list(self.sums[a:b].chunk(self.world)), group=self.group,
+                                            async_op=True).wait()
+                else:
+                    t.copy_(self.sums[a:b])
+                decode(t, d, h)
+                if collective:
+                    if nccl:
+                        dist.all_gather_into_tensor(self.out[a:b], d, group=self.group, async_op=True).wait()
+                    else:
+                        dist.all_gather(list(self.out[a:b].chunk(self.world)), d, group=self.group,
+                                        async_op=True).wait()
+                else:
+                    self.out[a:b].copy_(d)
         for st in self.side:
             main.wait_stream(st)
 

@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.SIGNATURES), "ctypes signatures out of sync with the header"
-    assert lib.pgh_abi_version() == 2
+    assert lib.pgh_abi_version() == 3
 
 
 def test_library_has_gfx950_code_object():

@@ -14,7 +14,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pygrid_amd.sharding import OverlappedGather, all_shard_bounds, gather_flat, shard_bounds
+from pygrid_amd.sharding import (OverlappedGather, OverlappedReduceScatter, all_shard_bounds, client_bounds,
+                                 gather_flat, shard_bounds)
 
 
 def _free_port():
@@ -105,3 +106,76 @@ def test_weak_scaling_shards_equal():
     for world in (1, 2, 4, 8):
         for lo, hi in all_shard_bounds(world * Pg, world):
             assert abs((hi - lo) - Pg) < 64 * world
+
+
+def _shares(P, N, S):
+    rng = np.random.default_rng(99)
+    sh = rng.integers(-2**63, 2**63 - 1, size=(N, S, P), dtype=np.int64, endpoint=True)
+    sh[:, :, :3] = np.iinfo(np.int64).max  # wrap many times over
+    return sh
+
+
+def _cs_worker(rank, world, port, P, N, S, chunks, q):
+    from oracle import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sh = _shares(P, N, S)
+        c0, c1 = client_bounds(N, world, rank)  # this rank ingests only its own clients
+        og = OverlappedReduceScatter(P, world, rank, chunks=chunks, device="cpu")
+
+        def sum_range(a, n, stream):
+            if c1 > c0:
+                og.sums[a:a + n] = torch.from_numpy(O.secagg_sum(sh[c0:c1, :, a:a + n]))
+            else:
+                og.sums[a:a + n] = 0
+
+        def decode(total, dec, stream):
+            dec.copy_(torch.from_numpy(O.fix_prec_decode(total.numpy())))
+        og.run(sum_range, decode)
+        q.put((rank, og.assemble().numpy().tobytes(), og.total.numpy().tobytes(), og.L))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("P,N,S,chunks", [(10_007, 5, 2, 3), (130, 3, 3, 8), (1, 1, 2, 1), (300, 7, 2, 2)])
+def test_client_sharded_secagg_reduce_scatter_is_bit_identical(P, N, S, chunks):
+    """Secure aggregation with the CLIENTS sharded (north_star: reduce-scatter when clients are
+    sharded): per-rank Z_2^64 sums reduce-scattered, decoded per slice, all-gathered -- equal bit
+    for bit to one rank summing every client, and the reduced slices are the full sum's."""
+    from oracle import oracle as O
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cs_worker, args=(r, world, port, P, N, S, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sh = _shares(P, N, S)
+    want_sum = O.secagg_sum(sh)
+    want = O.fix_prec_decode(want_sum)
+    for rank, blob, tot, L in res:
+        got = np.frombuffer(blob, dtype=np.float32)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), rank
+        full = np.zeros(L, np.int64)
+        full[:P] = want_sum
+        m = L // world
+        og_ranges = OverlappedReduceScatter(P, world, rank, chunks=chunks, device="cpu").ranges
+        mine = np.concatenate([full[a + rank * (b - a) // world: a + (rank + 1) * (b - a) // world]
+                               for a, b in og_ranges])
+        assert mine.size == m and np.array_equal(np.frombuffer(tot, dtype=np.int64), mine)
+
+
+@pytest.mark.parametrize("N", [0, 1, 7, 1000])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_client_bounds_partition(N, world):
+    b = [client_bounds(N, world, r) for r in range(world)]
+    assert b[0][0] == 0 and b[-1][1] == N
+    assert all(hi == lo2 for (_, hi), (lo2, _) in zip(b, b[1:]))
+    assert max(hi - lo for lo, hi in b) - min(hi - lo for lo, hi in b) <= 1

@@ -580,6 +580,100 @@ def test_rccl_overlapped_gather_world1(engine):
         dist.destroy_process_group()
 
 
+def test_rccl_client_sharded_secagg_world1(engine):
+    """Client-sharded secure aggregation through the RCCL path, forced at world size 1: share sums
+    of param ranges (no decode), int64 reduce_scatter_tensor, decode kernel on the reduced slice,
+    all_gather_into_tensor -- bit-identical to pgh_secagg's fused sum + decode."""
+    import os
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from pygrid_amd.sharding import OverlappedReduceScatter
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        P, N, S = 1_000_003, 5, 2
+        rng = np.random.default_rng(52)
+        sh = rng.integers(-2**63, 2**63 - 1, size=(N, S, P), dtype=np.int64, endpoint=True)
+        engine.set_layout([P])
+        engine.reserve(N, 1, S)
+        for k in range(N):
+            engine.ingest(k, sh[k])
+        want_s, want_d = engine.secagg()
+        og = OverlappedReduceScatter(P, 1, 0, chunks=8)
+        og.run(lambda a, n, st: engine.secagg_device_range(a, n, og.sums.data_ptr(), 0, 10, 3, st),
+               lambda t, d, st: engine.secagg_decode_device(t.data_ptr(), t.numel(), d.data_ptr(), 10, 3, st),
+               force_collective=True)
+        got = og.assemble()
+        torch.cuda.synchronize()
+        assert np.array_equal(og.total[:P].cpu().numpy(), want_s)
+        assert np.array_equal(bits(got.cpu().numpy()), bits(want_d))
+        idx = rng.integers(0, P, 500)
+        _, od = coracle.secagg(sh[:, :, idx], idx.size)
+        assert np.array_equal(bits(got.cpu().numpy()[idx]), bits(od))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_stats_busy_time_is_union_of_launches(engine):
+    """pgh_stats' kernel_busy_ms_total: the sum of the durations for launches on one stream (no
+    overlap), never more than that sum for ranges alternating over two streams."""
+    import torch
+
+    P, N = 4_000_000, 16
+    engine.set_layout([P])
+    engine.reserve(N)
+    engine.synth_fill(9, N)
+    ck = torch.zeros(P, dtype=torch.float32, device="cuda")
+    out = torch.empty_like(ck)
+    engine.reset_stats()
+    for _ in range(4):
+        engine.fedavg_device(0, ck.data_ptr(), out.data_ptr())
+    st = engine.stats()
+    assert st["kernel_launches"] == 4
+    assert st["kernel_busy_ms_total"] == pytest.approx(st["kernel_ms_total"], rel=1e-3)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    engine.reset_stats()
+    n = P // 8
+    for i in range(8):
+        s = torch.cuda.current_stream() if i % 2 == 0 else side
+        engine.fedavg_device_range(0, i * n, n, ck.data_ptr(), out.data_ptr(), s.cuda_stream)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    st = engine.stats()
+    assert st["kernel_launches"] == 8
+    assert 0 < st["kernel_busy_ms_total"] <= st["kernel_ms_total"] * (1 + 1e-6)
+
+
+def test_secagg_decode_device_edges(engine):
+    """The stand-alone decode kernel on int64 extremes and float32 rounding boundaries equals the
+    oracle's float32(int64) / 1000 bit for bit (and base 2 / prec 0 divisors)."""
+    import torch
+
+    from pygrid_amd import AggregationError
+
+    v = np.array([0, 1, -1, 2**63 - 1, -2**63, 2**24 + 1, -(2**24 + 1), 2**53 + 1, 123456789, -999, 1000,
+                  16_777_217_000], np.int64)
+    v = np.concatenate([v, np.random.default_rng(3).integers(-2**63, 2**63 - 1, 10_001, dtype=np.int64)])
+    t = torch.from_numpy(v).cuda()
+    d = torch.empty(v.size, dtype=torch.float32, device="cuda")
+    for base, prec in ((10, 3), (2, 5), (10, 0)):
+        engine.secagg_decode_device(t.data_ptr(), v.size, d.data_ptr(), base, prec)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(d.cpu().numpy()), bits(O.fix_prec_decode(v, base, prec))), (base, prec)
+    engine.secagg_decode_device(0, 0, 0)  # empty is fine
+    with pytest.raises(AggregationError):
+        engine.secagg_decode_device(t.data_ptr(), 4, d.data_ptr(), 1, 3)  # bad base
+
+
 @pytest.mark.parametrize("variant", [-1, 0, 6, 11, 12, 14, 15, 17])
 def test_iterative_division_shortcut_edges(engine, variant):
     """The iterative fold's reciprocal-multiply division (div shortcut in pgh_kernels.hip) around
