@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--variant", type=int, default=None)
     ap.add_argument("--ring", type=int, default=None, help="stream workloads: HBM ring slots")
     ap.add_argument("--gather-chunks", type=int, default=8, help="N > 1: fold ranges overlapped with all-gather")
+    ap.add_argument("--gather-tail", type=int, default=3,
+                    help="N > 1: halve the last range this many times (shorter exposed collective)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -294,7 +296,7 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
         if ctx.world > 1:
             # fold the shard in 8 param ranges; RCCL all-gathers range i beside the fold of i + 1
             from pygrid_amd.sharding import OverlappedGather
-            og = OverlappedGather(P, ctx.world, ctx.rank, chunks=args.gather_chunks)
+            og = OverlappedGather(P, ctx.world, ctx.rank, chunks=args.gather_chunks, tail=args.gather_tail)
             lp = og.local.data_ptr()
 
             def step():
@@ -310,7 +312,7 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
         if ctx.world > 1:
             # decoded shard gathered range by range beside the share sum of the next range
             from pygrid_amd.sharding import OverlappedGather
-            og = OverlappedGather(P, ctx.world, ctx.rank, chunks=args.gather_chunks)
+            og = OverlappedGather(P, ctx.world, ctx.rank, chunks=args.gather_chunks, tail=args.gather_tail)
             lp = og.local.data_ptr()
 
             def step():
@@ -327,7 +329,7 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
                        + (f" x {parties} parties int64" if dtype == 1 else " fp32") + ", resident in HBM",
            "clients": N, "params_per_gpu": pg, "params_total": P,
            "parallelism": f"param-shard{ctx.world}" + (
-               f" + RCCL all-gather ({args.gather_chunks} ranges overlapped with the fold)" if ctx.world > 1 else ""),
+               f" + RCCL all-gather ({args.gather_chunks} ranges, last halved {args.gather_tail}x, overlapped with the fold)" if ctx.world > 1 else ""),
            "kernel_variant": eng.effective_variant(mode if dtype == 0 else 16)}
     rec = record(ctx, args, args.workload, value, el, dt, cfg,
                  roofline_of(st, args.workload, cfg["kernel_variant"], kernel))
@@ -350,7 +352,7 @@ def run_secagg_clients(ctx, args, eng, N, S, P):
 
     eng.reserve(N, 1, S)
     eng.synth_fill(args.seed + ctx.rank, N)
-    og = OverlappedReduceScatter(P, ctx.world, ctx.rank, chunks=args.gather_chunks)
+    og = OverlappedReduceScatter(P, ctx.world, ctx.rank, chunks=args.gather_chunks, tail=args.gather_tail)
     sp = og.sums.data_ptr()
 
     def step():
@@ -365,7 +367,7 @@ def run_secagg_clients(ctx, args, eng, N, S, P):
                        "clients sharded, resident in HBM",
            "clients": N * ctx.world, "clients_per_gpu": N, "params_per_gpu": P, "params_total": P,
            "parallelism": f"client-shard{ctx.world} + RCCL int64 reduce-scatter / decode / all-gather "
-                          f"({args.gather_chunks} ranges overlapped with the share sum)",
+                          f"({args.gather_chunks} ranges, last halved {args.gather_tail}x, overlapped with the share sum)",
            "kernel_variant": eng.effective_variant(16)}
     # roofline: the share-sum launches (k_secagg); the decode kernel (12 B/param) is not in the stats
     rec = record(ctx, args, "secagg-clients", value, el, "int64", cfg,

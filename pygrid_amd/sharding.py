@@ -40,6 +40,27 @@ def all_shard_bounds(P: int, world: int, align: int = ALIGN) -> List[Tuple[int, 
     return [shard_bounds(P, world, r, align) for r in range(world)]
 
 
+def plan_ranges(length: int, chunks: int, unit: int = ALIGN, tail: int = 0) -> List[Tuple[int, int]]:
+    """Cut ``[0, length)`` into ``chunks`` equal ranges (multiples of ``unit``), then split the
+    last one in halves ``tail`` times (c/2, c/4, ..., c/2^tail, c/2^tail): the collective of the
+    last range is the only one not hidden behind a later fold, so a short last range shortens
+    the exposed tail of the step without cutting every range small."""
+    if length <= 0:
+        return []
+    c = -(-length // max(1, chunks))
+    c = -(-c // unit) * unit
+    cuts = list(range(0, length, c))[1:]
+    last = cuts[-1] if cuts else 0
+    for _ in range(max(0, tail)):
+        half = -(-((length - last) // 2) // unit) * unit
+        if half <= 0 or last + half >= length:
+            break
+        last += half
+        cuts.append(last)
+    edges = [0] + cuts + [length]
+    return [(a, b) for a, b in zip(edges, edges[1:]) if b > a]
+
+
 def gather_flat(shard, P: int, world: int, rank: int, align: int = ALIGN, group=None):
     """All-gather every rank's output shard into the full flat vector (torch tensors).
 
@@ -85,7 +106,7 @@ class OverlappedGather:
     """
 
     def __init__(self, P: int, world: int, rank: int, chunks: int = 4, device="cuda", dtype=None, group=None,
-                 align: int = ALIGN, streams: int = 2):
+                 align: int = ALIGN, streams: int = 2, tail: int = 0):
         import torch
 
         dtype = dtype or torch.float32
@@ -93,9 +114,7 @@ class OverlappedGather:
         self.s = shard_size(P, world, align)
         self.lo, self.hi = shard_bounds(P, world, rank, align)
         self.pg = self.hi - self.lo
-        c = -(-self.s // max(1, chunks))
-        c = -(-c // align) * align
-        self.ranges = [(a, min(a + c, self.s)) for a in range(0, self.s, c)]
+        self.ranges = plan_ranges(self.s, chunks, align, tail)
         self.local = torch.zeros(self.s, dtype=dtype, device=device)
         self.recv = [torch.empty(world * (b - a), dtype=dtype, device=device) for a, b in self.ranges]
         self.out = torch.empty(world * self.s, dtype=dtype, device=device)
@@ -171,15 +190,13 @@ class OverlappedReduceScatter:
     """
 
     def __init__(self, P: int, world: int, rank: int, chunks: int = 8, device="cuda", group=None,
-                 align: int = ALIGN, streams: int = 2):
+                 align: int = ALIGN, streams: int = 2, tail: int = 0):
         import torch
 
         self.P, self.world, self.rank, self.group = P, world, rank, group
         unit = world * align
-        c = -(-P // max(1, chunks))
-        c = -(-c // unit) * unit
-        self.L = -(-P // c) * c
-        self.ranges = [(a, a + c) for a in range(0, self.L, c)]
+        self.L = -(-P // unit) * unit
+        self.ranges = plan_ranges(self.L, chunks, unit, tail)
         self.sums = torch.zeros(self.L, dtype=torch.int64, device=device)
         self.total = torch.empty(self.L // world, dtype=torch.int64, device=device)
         self.dec = torch.empty(self.L // world, dtype=torch.float32, device=device)

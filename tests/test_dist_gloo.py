@@ -43,7 +43,7 @@ def _worker(rank, world, port, P, N, mode, q):
             part = np.empty(0, np.float32)
         full = gather_flat(torch.from_numpy(part), P, world, rank)
         # chunked fold + overlapped all-gather (what bench.py runs at N > 1)
-        og = OverlappedGather(P, world, rank, chunks=3, device="cpu")
+        og = OverlappedGather(P, world, rank, chunks=3, device="cpu", tail=2)
 
         def fold_range(off, n, stream):
             w = np.linspace(0.5, 2.0, N).astype(np.float32)
@@ -123,7 +123,7 @@ def _cs_worker(rank, world, port, P, N, S, chunks, q):
     try:
         sh = _shares(P, N, S)
         c0, c1 = client_bounds(N, world, rank)  # this rank ingests only its own clients
-        og = OverlappedReduceScatter(P, world, rank, chunks=chunks, device="cpu")
+        og = OverlappedReduceScatter(P, world, rank, chunks=chunks, device="cpu", tail=2)
 
         def sum_range(a, n, stream):
             if c1 > c0:
@@ -166,7 +166,7 @@ def test_client_sharded_secagg_reduce_scatter_is_bit_identical(P, N, S, chunks):
         full = np.zeros(L, np.int64)
         full[:P] = want_sum
         m = L // world
-        og_ranges = OverlappedReduceScatter(P, world, rank, chunks=chunks, device="cpu").ranges
+        og_ranges = OverlappedReduceScatter(P, world, rank, chunks=chunks, device="cpu", tail=2).ranges
         mine = np.concatenate([full[a + rank * (b - a) // world: a + (rank + 1) * (b - a) // world]
                                for a, b in og_ranges])
         assert mine.size == m and np.array_equal(np.frombuffer(tot, dtype=np.int64), mine)
@@ -179,3 +179,19 @@ def test_client_bounds_partition(N, world):
     assert b[0][0] == 0 and b[-1][1] == N
     assert all(hi == lo2 for (_, hi), (lo2, _) in zip(b, b[1:]))
     assert max(hi - lo for lo, hi in b) - min(hi - lo for lo, hi in b) <= 1
+
+
+@pytest.mark.parametrize("length,chunks,unit,tail", [(11_689_536, 8, 64, 3), (100, 8, 64, 3), (64, 1, 64, 3),
+                                                     (1, 8, 64, 2), (93_516_288, 8, 512, 3), (640, 3, 64, 9),
+                                                     (0, 4, 64, 1)])
+def test_plan_ranges_partition(length, chunks, unit, tail):
+    from pygrid_amd.sharding import plan_ranges
+
+    r = plan_ranges(length, chunks, unit, tail)
+    if length == 0:
+        assert r == []
+        return
+    assert r[0][0] == 0 and r[-1][1] == length
+    assert all(b > a and a % unit == 0 for a, b in r)
+    assert all(b == a2 for (_, b), (a2, _) in zip(r, r[1:]))
+    assert len(r) <= chunks + tail

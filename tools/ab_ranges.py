@@ -2,7 +2,7 @@
 """Cost of folding the shard in param ranges (the N > 1 bench path: range i is all-gathered beside
 the fold of range i + 1) against one whole-shard fold, on one GPU, interleaved rounds.
 
-    python tools/ab_ranges.py [--chunks 1,2,4,8,16]
+    python tools/ab_ranges.py [--chunks 1,2,4,8,16,8t3]      (8t3: 8 ranges, last one halved 3 times)
 """
 import argparse
 import json
@@ -26,7 +26,7 @@ def main():
     import torch
 
     from pygrid_amd import Engine
-    from pygrid_amd.sharding import ALIGN
+    from pygrid_amd.sharding import ALIGN, plan_ranges
 
     P, N = a.params, a.clients
     eng = Engine(0)
@@ -40,17 +40,16 @@ def main():
     eng.synth_ckpt_device(1, ck.data_ptr(), sp)
     res = {}
     plans = {}
-    for k in [int(x) for x in a.chunks.split(",")]:
-        c = -(-P // k)
-        c = -(-c // ALIGN) * ALIGN
-        plans[k] = [(o, min(c, P - o)) for o in range(0, P, c)]
+    for k in a.chunks.split(","):
+        n, _, t = k.partition("t")
+        plans[k] = [(o, b - o) for o, b in plan_ranges(P, int(n), ALIGN, int(t or 0))]
         res[k] = []
 
     main = torch.cuda.current_stream()
     side = [main] + [torch.cuda.Stream() for _ in range(a.streams - 1)]
 
     def step(k):
-        if k == 1:
+        if k == "1":
             eng.fedavg_device(0, ck.data_ptr(), out.data_ptr(), sp)
         else:
             for s in side[1:]:
