@@ -152,6 +152,50 @@ def cpu_baseline(kind: str, P: int, seed: int, budget_s: float, n: int = 32, all
             "numpy_restatement_1_thread": round(gbs_np, 3), "cpu_model": cpu_model()}
 
 
+def cpu_baseline_state(ck_pb: bytes, d_pbs, P: int, n_target: int, budget_s: float):
+    """The node's whole bytes -> bytes cycle close on the host (oracle.cycle_close_state_torch:
+    State parse + per-tensor torch.tensor conversion, mean, apply, serialize; cycle_manager.py:
+    240-303, model_manager.py:79-103) at th.set_num_threads(1).  With all n_target diffs given it
+    is timed as is (repeated for budget_s); otherwise closes of 1 and len(d_pbs) diffs are timed
+    and the close of n_target diffs extrapolated linearly (fixed + per-diff cost)."""
+    import torch
+
+    from oracle import oracle as O
+
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        def close_s(pbs, min_s):
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                O.cycle_close_state_torch(ck_pb, pbs)
+                reps += 1
+                el = time.perf_counter() - t0
+                if el >= min_s:
+                    return el / reps, reps
+        if len(d_pbs) == n_target:
+            O.cycle_close_state_torch(ck_pb, d_pbs)  # warm
+            t, reps = close_s(d_pbs, budget_s)
+            how = f"{reps} closes of {n_target} diffs timed"
+            extrap = False
+        else:
+            t1, _ = close_s(d_pbs[:1], 0.0)
+            tn, _ = close_s(d_pbs, 0.0)
+            per = (tn - t1) / (len(d_pbs) - 1)
+            t = t1 + (n_target - 1) * per
+            how = (f"extrapolated: closes of 1 and {len(d_pbs)} diffs timed ({t1 * 1e3:.0f} / {tn * 1e3:.0f} ms, "
+                   f"{per * 1e3:.0f} ms per diff), close of {n_target} = fixed + {n_target} x per-diff")
+            extrap = True
+    finally:
+        torch.set_num_threads(threads)
+    return {"value": round(4 * n_target * P / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "oracle.cycle_close_state_torch: State bytes -> new checkpoint bytes (protobuf ParseFromString "
+                      "over the restated schema, torch.tensor(contents_float32) per tensor, reduce(th.add) / th.div / "
+                      f"subtract, contents_float32.extend(tolist()) + SerializeToString), torch {torch.__version__}, "
+                      f"P={P}, 1 thread; {how}",
+            "cycle_close_ms": round(t * 1e3, 2), "extrapolated": extrap, "cpu_model": cpu_model()}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -333,10 +377,18 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
            "kernel_variant": eng.effective_variant(mode if dtype == 0 else 16)}
     rec = record(ctx, args, args.workload, value, el, dt, cfg,
                  roofline_of(st, args.workload, cfg["kernel_variant"], kernel))
+    kind = "secagg" if dtype == 1 else {0: "mean", 1: "iterative", 2: "weighted"}[mode]
+    return attach_cpu_baseline(ctx, args, rec, kind, pg)
+
+
+def attach_cpu_baseline(ctx, args, rec, kind, P, n=32, note=None):
+    """rank 0 at N = 1 only: the reference's arithmetic for this workload timed on the host
+    (cpu_baseline above), on a bounded sample of the same P-param shard."""
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
-        kind = "secagg" if dtype == 1 else {0: "mean", 1: "iterative", 2: "weighted"}[mode]
         try:
-            rec["cpu_baseline"] = cpu_baseline(kind, pg, args.seed, args.cpu_seconds)
+            rec["cpu_baseline"] = cpu_baseline(kind, P, args.seed, args.cpu_seconds, n=n)
+            if note:
+                rec["cpu_baseline"]["sample"] += "; " + note
         except Exception as e:  # noqa: BLE001
             rec["cpu_baseline"] = {"error": str(e)}
     return rec
@@ -372,7 +424,7 @@ def run_secagg_clients(ctx, args, eng, N, S, P):
     # roofline: the share-sum launches (k_secagg); the decode kernel (12 B/param) is not in the stats
     rec = record(ctx, args, "secagg-clients", value, el, "int64", cfg,
                  roofline_of(st, "secagg-clients", cfg["kernel_variant"], "k_secagg"))
-    return rec
+    return attach_cpu_baseline(ctx, args, rec, "secagg", P)
 
 
 def run_c4(ctx, args, eng, N, pg, P):
@@ -409,8 +461,10 @@ def run_c4(ctx, args, eng, N, pg, P):
     extra = {"fold_kernel_client_diff_GBps_aggregated": round(kern_gbs, 1),
              "note": "value includes on-device generation of every chunk (writes 4 B/param/client) "
                      "competing for HBM with the fold; the fold kernels alone are fold_kernel_*"}
-    return record(ctx, args, "c4-stream", value, el, "f32", cfg,
-                  roofline_of(st, "c4-stream", cfg["kernel_variant"], "k_fedavg"), extra)
+    rec = record(ctx, args, "c4-stream", value, el, "f32", cfg,
+                 roofline_of(st, "c4-stream", cfg["kernel_variant"], "k_fedavg"), extra)
+    return attach_cpu_baseline(ctx, args, rec, "mean", pg, n=8,
+                               note=f"extrapolated: per-byte rate of an 8-client sample of the {N}-client shard")
 
 
 def run_c5(ctx, args, eng, N, pg, P):
@@ -457,6 +511,9 @@ def run_c5(ctx, args, eng, N, pg, P):
              "fold_kernel_client_diff_GBps_per_gpu": round(kern_gbs, 1)}
     rec = record(ctx, args, "c5-ingest", value, el, "f32", cfg,
                  roofline_of(st, "c5-ingest", cfg["kernel_variant"], "k_fedavg"), extra)
+    attach_cpu_baseline(ctx, args, rec, "iterative", pg, n=4,
+                        note=f"extrapolated: per-byte rate of a 4-client sample of the {N}-client shard, diffs "
+                             "already in host memory (no ingest)")
     for b in bufs:
         b.free()
     return rec
@@ -494,16 +551,7 @@ def run_mnist_state(ctx, args, eng):
                  {"new_checkpoint_bytes": len(new),
                   "note": "latency-bound: host protobuf scan, 3 H2D copies and a 0.3M-param kernel"})
     if not args.no_cpu_baseline:
-        from oracle import oracle as O  # cpu_baseline leg only
-        t0, reps = time.perf_counter(), 0
-        while time.perf_counter() - t0 < 2.0:
-            O.fedavg_mean(ck, ds)
-            reps += 1
-        cel = (time.perf_counter() - t0) / reps
-        rec["cpu_baseline"] = {"value": round(4 * 3 * P / cel / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-                               "sample": f"oracle numpy mean+apply on the decoded tensors, {reps} reps "
-                                         f"(syft protobuf decode not timed: syft is absent)",
-                               "cycle_close_ms": round(cel * 1e3, 3)}
+        rec["cpu_baseline"] = cpu_baseline_state(ck_pb, d_pb, P, 3, 4.0)
     return rec
 
 
@@ -540,8 +588,11 @@ def run_resnet18_state(ctx, args, eng, N):
              "h2d_ms_per_close": round(st["h2d_ms_total"] / args.steps, 2),
              "new_checkpoint_bytes": len(new),
              "note": "PCIe-inclusive cycle close from host bytes (never `value` for the resident configs)"}
-    return record(ctx, args, "resnet18-state", value, el, "f32", cfg,
-                  roofline_of(st, "resnet18-state", eng.effective_variant(), "k_fedavg"), extra)
+    rec = record(ctx, args, "resnet18-state", value, el, "f32", cfg,
+                 roofline_of(st, "resnet18-state", eng.effective_variant(), "k_fedavg"), extra)
+    if not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline_state(ck_pb, distinct[:3], P, N, 0.0)
+    return rec
 
 
 def run_resnet18_report(ctx, args, eng, N):
@@ -596,8 +647,11 @@ def run_resnet18_report(ctx, args, eng, N):
              "new_checkpoint_bytes": len(new),
              "note": "PCIe-inclusive whole cycle (reports + close); compare close_ms_after_last_report with "
                      "resnet18-state's cycle_close_ms (all diffs folded at close)"}
-    return record(ctx, args, "resnet18-report", value, el, "f32", cfg,
-                  roofline_of(st, "resnet18-report", eng.effective_variant(), "k_fedavg"), extra)
+    rec = record(ctx, args, "resnet18-report", value, el, "f32", cfg,
+                 roofline_of(st, "resnet18-report", eng.effective_variant(), "k_fedavg"), extra)
+    if not args.no_cpu_baseline:  # the reference decodes and folds every diff at close
+        rec["cpu_baseline"] = cpu_baseline_state(ck_pb, distinct[:3], P, N, 0.0)
+    return rec
 
 
 def main():

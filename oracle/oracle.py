@@ -78,6 +78,53 @@ def fedavg_mean_torch(model_params, diffs):
     return [p - a for p, a in zip(model_params, avg)]
 
 
+def _state_tensor(stt):
+    return stt.torch_tensor if stt.HasField("torch_tensor") else stt.torch_param.tensor
+
+
+def unserialize_state_torch(pb: bytes):
+    """``ModelManager.unserialize_model_params`` (model_manager.py:94-103) restated with Google's
+    protobuf runtime over the build's State schema restatement (``pygrid_amd.state_schema``;
+    syft-proto 0.5.2 is absent): ``StatePB.ParseFromString`` (:98-99), then syft 0.2.9's protobuf
+    tensor deserializer, i.e. ``torch.tensor(contents_<dtype>, dtype=...).reshape(shape)`` per
+    tensor (``_unbufferize`` :101, ``state.tensors()`` :102).  Returns (tensors, parsed message)."""
+    import torch as th
+
+    from pygrid_amd.state_schema import classes
+
+    st = classes()["State"]()
+    st.ParseFromString(pb)
+    ts = []
+    for stt in st.tensors:
+        tt = _state_tensor(stt)
+        ts.append(th.tensor(tt.contents_data.contents_float32, dtype=th.float32)
+                  .reshape(tuple(tt.contents_data.shape.dims)))
+    return ts, st
+
+
+def serialize_state_torch(st, params) -> bytes:
+    """``ModelManager.serialize_model_params`` (model_manager.py:79-92) restated: every tensor's
+    values written back into the State message as the repeated ``contents_float32`` field (syft's
+    tensor serializer: ``.extend(tensor.flatten().tolist())``), then ``SerializeToString`` (:90).
+    The parsed checkpoint message is reused as the frame (ids/tags kept), as in the engine."""
+    for stt, t in zip(st.tensors, params):
+        tt = _state_tensor(stt)
+        del tt.contents_data.contents_float32[:]
+        tt.contents_data.contents_float32.extend(t.reshape(-1).tolist())
+    return st.SerializeToString()
+
+
+def cycle_close_state_torch(ckpt_pb: bytes, diff_pbs):
+    """The node's hard-coded cycle close on bytes, ``cycle_manager.py:240-303``: unserialize the
+    checkpoint (:240) and every reported diff (:247-250), mean (:276-288), apply (:293-296),
+    serialize the new checkpoint (:303).  ``bench.py``'s cpu_baseline leg times it (the whole
+    bytes -> bytes close the engine replaces); ``tests/test_oracle.py`` checks its values against
+    ``fedavg_mean``."""
+    params, st = unserialize_state_torch(ckpt_pb)
+    diffs = [unserialize_state_torch(pb)[0] for pb in diff_pbs]
+    return serialize_state_torch(st, fedavg_mean_torch(params, diffs))
+
+
 # ----------------------------------------------------------------------------------------
 # (a6)+(a8) hosted iterative avg plan: cycle_manager.py:266-269 + 01-Create-plan.ipynb:450-454
 # ----------------------------------------------------------------------------------------

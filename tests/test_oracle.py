@@ -172,6 +172,24 @@ def test_mnist_golden(gold):
     assert h(coracle.fedavg(0, diffs, ckpt)) == g["sha256_mean"]
 
 
+def test_state_bytes_cycle_close_restatement(gold):
+    """oracle.cycle_close_state_torch (bytes -> bytes, cycle_manager.py:240-303 over the restated
+    State schema) decodes to the golden MNIST mean and keeps the checkpoint's framing."""
+    from pygrid_amd.state_schema import build_state, parse_state
+
+    g = json.loads((gold / "mnist_synth.json").read_text())
+    diffs, ckpt = mnist_inputs(g["seed"], g["n_clients"])
+    ck = split(ckpt, MNIST_SHAPES)
+    ds = [split(d, MNIST_SHAPES) for d in diffs]
+    ck_pb = build_state(ck, as_param=True)
+    new = O.cycle_close_state_torch(ck_pb, [build_state(d) for d in ds])
+    got = [a for a in parse_state(new)]
+    assert [a.shape for a in got] == [tuple(s) for s in MNIST_SHAPES]
+    flat = np.concatenate([a.reshape(-1) for a in got])
+    assert hashlib.sha256(flat.tobytes()).hexdigest() == g["sha256_mean"]
+    assert len(new) == len(ck_pb)  # same framing, payloads replaced
+
+
 # ---- secure aggregation ------------------------------------------------------------------------
 def test_smpc_integer_share_reconstructs_exactly(gold):
     """test_basic_syft_operations.py:388-394."""
