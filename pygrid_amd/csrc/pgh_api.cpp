@@ -25,6 +25,8 @@
 // (test_basic_syft_operations.py:417-424).  Errors are negative status codes plus a message (the
 // Python shim raises a PyGridError subclass, as tasks/cycle.py:33-37 expects).
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -36,6 +38,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <string>
 #include <thread>
 #include <vector>
@@ -478,9 +481,25 @@ void scatter_out(const uint8_t* src, size_t off, size_t len, const std::vector<O
     pool.run(segs);
 }
 
+// Fault in the pages of a small, freshly allocated host destination with one madvise call
+// (MADV_POPULATE_WRITE, Linux 5.14+) instead of one page fault per 4 KiB during the copy-out; big
+// destinations are left to the copy pool, whose threads fault their own pages in parallel.  Best
+// effort: an older kernel or a non-anonymous mapping just returns an error, which is ignored.
+void prefault_small(uint8_t* p, size_t n) {
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+    if (!p || n == 0 || n >= (4u << 20)) return;
+    static const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
+    const uintptr_t a = (uintptr_t)p & ~(page - 1), b = ((uintptr_t)p + n + page - 1) & ~(page - 1);
+    (void)madvise((void*)a, b - a, MADV_POPULATE_WRITE);
+}
+
 // HBM bytes at `src` (after the work already on stream `s`) -> host pieces, through the pinned
-// ring: the DMA of one slot overlaps the host copy-out of the previous one.
-int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>& pieces, hipStream_t s) {
+// ring: the DMA of one slot overlaps the host copy-out of the previous one.  `overlap`, if given,
+// is host work run while the first DMA is in flight (the checkpoint template's framing copy).
+int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>& pieces, hipStream_t s,
+                     const std::function<void()>& overlap = nullptr) {
     size_t total = 0;
     for (auto& p : pieces) total += p.n;
     size_t off = 0;
@@ -498,6 +517,7 @@ int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>
             CK(c, hipEventRecord(c->pin_ev[cur_slot], s));
             c->pin_used[cur_slot] = true;
         }
+        if (overlap && off == 0) overlap();
         if (prev_slot >= 0) {
             CK(c, hipEventSynchronize(c->pin_ev[prev_slot]));
             scatter_out(c->h_pin[prev_slot], prev_off, prev_len, pieces, *c->pool_copy);
@@ -1257,23 +1277,29 @@ int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out
     std::vector<std::pair<size_t, size_t>> spans;
     RC(state_shard_spans(c, tmpl, n, &spans, "checkpoint template"));
     DeviceGuard g(c->device);
+    std::vector<CopyPool::Seg> gaps;
+    bool ordered = true;
     if (out != tmpl) {  // template bytes outside this shard's payload slices (framing, other shards)
-        std::vector<CopyPool::Seg> gaps;
         size_t pos = 0;
-        bool ordered = true;
         for (auto& sp : spans) {
             ordered = ordered && sp.first >= pos;
             if (sp.first > pos) gaps.push_back({out + pos, tmpl + pos, sp.first - pos});
             pos = sp.first + sp.second;
         }
         if (n > pos) gaps.push_back({out + pos, tmpl + pos, n - pos});
-        if (!ordered) gaps.assign(1, CopyPool::Seg{out, tmpl, n});
-        c->pool_copy->run(gaps);
     }
     std::vector<OutPiece> pieces;
     for (auto& sp : spans) pieces.push_back(OutPiece{out + sp.first, sp.second});
     RC(order_after_ingest(c, c->stream));
-    RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, pieces, c->stream));
+    if (!ordered) {  // overlapping spans (never from the walker): whole template first, then payloads
+        c->pool_copy->run({CopyPool::Seg{out, tmpl, n}});
+        gaps.clear();
+    }
+    // the framing copy (and the pre-fault of a small fresh output) runs while the first slot's DMA flies
+    RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, pieces, c->stream, [&] {
+        if (out != tmpl) prefault_small(out, n);
+        if (!gaps.empty()) c->pool_copy->run(gaps);
+    }));
     return collect_timings(c);
 }
 
@@ -1435,7 +1461,7 @@ int pgh_stream_finish_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, f
 
 int pgh_set_variant(pgh_ctx* c, int variant) {
     if (!c) return PGH_E_ARG;
-    if (variant < -1 || variant > 20) return fail(c, PGH_E_ARG, "variant %d outside [-1,20]", variant);
+    if (variant < -1 || variant > 22) return fail(c, PGH_E_ARG, "variant %d outside [-1,22]", variant);
     c->variant = variant;
     return PGH_OK;
 }

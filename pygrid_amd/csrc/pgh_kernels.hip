@@ -229,6 +229,76 @@ __device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, 
     }
 }
 
+// Software-pipelined column walk (variants 21/22): the loads of row batch i + 1 are issued before
+// batch i is folded, so a lane keeps between U and 2U rows in flight instead of draining to zero
+// between batches.  Two named buffers (no register copies that would wait on the new loads); the
+// fold of one batch and the loads of the next sit in one basic block, so the wait counts only
+// cover the batch being folded.  Same fold order as fedavg_columns: bit-identical.
+template <int MODE, int U, bool NT, int VEC>
+__device__ __forceinline__ void fedavg_columns_pipe(const FedavgArgs& a, int64_t q) {
+    using L = Lane<VEC>;
+    using T = typename L::T;
+    const int n = a.n_rows;
+    const int64_t ld = a.map.ld;
+    const float* col = a.diffs + a.map.at(VEC * q);
+    T acc[1];
+    int r;
+    if (a.flags & FL_FIRST) {
+        acc[0] = L::template load<NT>(col);
+        if constexpr (MODE == MODE_WEIGHTED) acc[0] = acc[0] * a.weights[0];
+        r = 1;
+    } else {
+        acc[0] = L::load_tail(a.acc, q, a.p);
+        r = 0;
+    }
+    T A[U][1], B[U][1];
+    if (r + U <= n) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) A[u][0] = L::template load<NT>(col + (size_t)(r + u) * ld);
+        for (;;) {
+            if (r + 2 * U <= n) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) B[u][0] = L::template load<NT>(col + (size_t)(r + U + u) * ld);
+                fold_rows<MODE, U, 1>(acc, A, a, r, U);
+                r += U;
+            } else {
+                fold_rows<MODE, U, 1>(acc, A, a, r, U);
+                r += U;
+                break;
+            }
+            if (r + 2 * U <= n) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) A[u][0] = L::template load<NT>(col + (size_t)(r + U + u) * ld);
+                fold_rows<MODE, U, 1>(acc, B, a, r, U);
+                r += U;
+            } else {
+                fold_rows<MODE, U, 1>(acc, B, a, r, U);
+                r += U;
+                break;
+            }
+        }
+    }
+    if (r < n) {  // the last partial batch, its loads in flight together
+        const int nv = n - r;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (u < nv) A[u][0] = L::template load<NT>(col + (size_t)(r + u) * ld);
+        fold_rows<MODE, U, 1>(acc, A, a, r, nv);
+    }
+    if (a.flags & FL_FINAL) {
+        const T avg = (MODE == MODE_ITERATIVE) ? acc[0] : acc[0] / a.divisor;  // th.div, :288
+        L::store_tail(a.out, q, a.p, L::load_tail(a.ckpt, q, a.p) - avg);     // :293-296
+    } else {
+        L::store_tail(a.acc, q, a.p, acc[0]);
+    }
+}
+
+template <int MODE, int U, bool NT, int TB, int VEC>
+__global__ __launch_bounds__(TB) void k_fedavg_pipe(FedavgArgs a, int64_t ncol) {
+    for (int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x; q < ncol; q += (int64_t)gridDim.x * TB)
+        fedavg_columns_pipe<MODE, U, NT, VEC>(a, q);
+}
+
 // Grid-stride over tiles of TB x W columns; a partial last tile goes one column per lane.
 template <int MODE, int U, int W, bool NT, int TB, int VEC>
 __global__ __launch_bounds__(TB) void k_fedavg(FedavgArgs a, int64_t ncol) {
@@ -402,10 +472,12 @@ int cu_count() {
 //   18  nt     32                  1              128    1                 one lane per param
 //   19  nt     16                  1              512    4                 one lane per column
 //   20  nt     8                   1              1024   4                 one lane per column
+//   21  nt     8 (+8 next batch)   1              256    4                 one lane per column, pipelined
+//   22  nt     4 (+4 next batch)   1              256    4                 one lane per column, pipelined
 // nt loads won 2-5 % on the once-read diff stream (r01c).  Small shards are bound by lanes / CU
 // balance, not by the loads: the auto choice (variant -1) picks by shard size and mode
 // (auto_variant below, r01l measurements on the column-blocked slab).
-constexpr int N_VARIANTS = 21;
+constexpr int N_VARIANTS = 23;
 constexpr int SECAGG_AUTO_VARIANT = 14;
 
 inline unsigned grid_for(int64_t ncol, int64_t tile, bool persistent) {
@@ -419,6 +491,13 @@ template <int MODE, int U, int W, bool NT, int TB, int VEC>
 hipError_t go_fedavg(const FedavgArgs& a, bool persistent, hipStream_t s) {
     const int64_t ncol = (a.p + VEC - 1) / VEC;
     k_fedavg<MODE, U, W, NT, TB, VEC><<<grid_for(ncol, (int64_t)TB * W, persistent), TB, 0, s>>>(a, ncol);
+    return hipGetLastError();
+}
+
+template <int MODE, int U, int TB, int VEC>
+hipError_t go_fedavg_pipe(const FedavgArgs& a, hipStream_t s) {
+    const int64_t ncol = (a.p + VEC - 1) / VEC;
+    k_fedavg_pipe<MODE, U, true, TB, VEC><<<grid_for(ncol, TB, false), TB, 0, s>>>(a, ncol);
     return hipGetLastError();
 }
 
@@ -446,6 +525,8 @@ hipError_t dispatch_fedavg(const FedavgArgs& a, int variant, hipStream_t s) {
     case 18: return go_fedavg<MODE, 32, 1, true, 128, 1>(a, false, s);
     case 19: return go_fedavg<MODE, 16, 1, true, 512, 4>(a, false, s);
     case 20: return go_fedavg<MODE, 8, 1, true, 1024, 4>(a, false, s);
+    case 21: return go_fedavg_pipe<MODE, 8, 256, 4>(a, s);
+    case 22: return go_fedavg_pipe<MODE, 4, 256, 4>(a, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -460,6 +541,8 @@ hipError_t dispatch_fedavg(const FedavgArgs& a, int variant, hipStream_t s) {
 //   P = 311,650 x 10K:   mean v11 6885 / v15 6645 / v0 5753;  iterative v12 5711 / v14 5670 / v11 5351
 //   P = 100K x 30K:      mean v11 6403 / v12 6251;  iterative v14 4742 / v12 4465 / v11 2784
 //   single block (P < 65,536; layout unchanged from r01g): P = 50K x 60K v14 6088 / v12 4013
+// Pipelined walk (r01w): P = 11.69M x 1K mean v0 6809 / v21 6798 / v22 6822, iterative 6834 / 6864 /
+//   6834, weighted 6816 / 6831 / 6820; 1M x 3K and 12.5M x 1K within 0.4 %: not latency-bound.
 // Iterative fold with the reciprocal-multiply division (r01o, tools/ab_iterative.sh):
 //   P = 50K x 60K v17 3665 / v14 3496;  100K x 30K v14 5970 / v17 5616;  311,650 x 10K v11 6359 /
 //   v14 5894;  1M x 3K v0 6755;  11.69M x 1K v0 6846  (IEEE division: 3209 / 4757 / 5784 / 6753 / 6845)
