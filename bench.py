@@ -24,6 +24,9 @@ Other BASELINE configs (--workload), each printed as its own JSON line of the sa
   mnist-state            config 1: 3 clients' State protobuf bytes -> new checkpoint bytes
   resnet18-state         ResNet-18 (62 tensors) x 100 clients, State bytes on the host -> new
                          checkpoint bytes: the whole cycle close a node runs (PCIe-inclusive)
+  resnet18-secagg-state  config 3 from the wire: ResNet-18 x N clients x 2 parties of int64 shares as
+                         State bytes (packed varints, ~9.5 B per value) in host memory -> HBM as
+                         received -> decoded on the GPU -> Z_2^64 sum + decode (PCIe-inclusive)
   resnet18-report        the same cycle with report-time aggregation: each
                          State diff is folded into HBM as it is reported, the checkpoint uploaded
                          at cycle start; reports the cycle close latency after the last report
@@ -55,6 +58,7 @@ WORKLOADS = {
     "mnist-state": (0, 0, 3, 1, 311_650),
     "resnet18-state": (0, 0, 100, 1, RESNET18_P),
     "resnet18-report": (0, 0, 100, 1, RESNET18_P),
+    "resnet18-secagg-state": (None, 1, 16, 2, RESNET18_P),
 }
 
 
@@ -595,6 +599,72 @@ def run_resnet18_state(ctx, args, eng, N):
     return rec
 
 
+def run_resnet18_secagg_state(ctx, args, eng, N, S):
+    """Secure aggregation from share State bytes: per step, N clients x S parties of int64 shares
+    (State messages with packed-varint payloads, 2 distinct clients re-sent from host memory) go
+    to HBM as they are, are decoded there (k_varint_decode) and summed + decoded (k_secagg)."""
+    import numpy as np
+
+    from pygrid_amd.state_schema import build_state_i64_fast
+    from pygrid_amd.workloads import RESNET18_SHAPES
+
+    numel = [int(np.prod(s)) for s in RESNET18_SHAPES]
+    P = sum(numel)
+    rng = np.random.default_rng(args.seed)
+    msgs = []
+    for _ in range(2):
+        sh = rng.integers(-2**63, 2**63 - 1, (S, P), dtype=np.int64, endpoint=True)
+        parts = [np.split(sh[s], np.cumsum(numel)[:-1]) for s in range(S)]
+        msgs.append([build_state_i64_fast(p) for p in parts])
+    wire = sum(len(m) for m in msgs[0])  # bytes per client (S messages)
+    eng.set_layout(numel)
+    eng.reserve(N, 1, S)
+
+    def step():
+        eng.reset()
+        for c in range(N):
+            eng.ingest_state_shares(c, msgs[c % 2])
+        return eng.secagg(10, 3)
+
+    for _ in range(args.warmup):
+        step()
+    eng.reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    el = time.perf_counter() - t0
+    st = eng.stats()
+    value = 8 * S * N * P * args.steps / el / 1e9
+    cfg = {"workload": f"resnet18-secagg-state: ResNet-18 (62 tensors, P={P}) x {N} clients x {S} parties of int64 "
+                       "shares as State bytes (packed varint) in host memory -> HBM -> GPU varint decode -> Z_2^64 "
+                       "sum + fixed-point decode -> host", "clients": N, "parties": S, "params_per_gpu": P,
+           "params_total": P, "parallelism": "single GPU", "kernel_variant": eng.effective_variant(16)}
+    extra = {"wire_bytes_per_client": wire, "wire_GBps": round(wire * N * args.steps / el / 1e9, 2),
+             "h2d_GBps": round(st["h2d_bytes_total"] / (st["h2d_ms_total"] / 1e3) / 1e9, 2) if st["h2d_ms_total"] else None,
+             "note": "PCIe-inclusive: value counts the decoded int64 share bytes (8 B per value) per second; "
+                     "wire_GBps the varint bytes received"}
+    rec = record(ctx, args, "resnet18-secagg-state", value, el, "int64", cfg,
+                 roofline_of(st, "resnet18-secagg-state", cfg["kernel_variant"], "k_secagg"), extra)
+    if not args.no_cpu_baseline:
+        from oracle import oracle as O  # cpu_baseline leg only
+        import torch
+        threads = torch.get_num_threads()
+        torch.set_num_threads(1)
+        try:
+            t0 = time.perf_counter()
+            O.secagg_close_state_torch([msgs[0]])
+            one = time.perf_counter() - t0
+        finally:
+            torch.set_num_threads(threads)
+        rec["cpu_baseline"] = {
+            "value": round(8 * S * P / one / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "oracle.secagg_close_state_torch on 1 client x 2 parties (protobuf ParseFromString over the "
+                      "restated schema, torch.tensor(contents_int64) per tensor, torch int64 share adds, "
+                      ".float() / 10**3), 1 thread; per-client rate, extrapolated",
+            "cycle_close_ms_per_client": round(one * 1e3, 1), "cpu_model": cpu_model()}
+    return rec
+
+
 def run_resnet18_report(ctx, args, eng, N):
     """Report-time aggregation (pygrid_amd.incremental.IncrementalCycle): per step one cycle of N
     reports (State bytes in host memory, in assignment order) folded through a 16-slot HBM ring as
@@ -682,6 +752,8 @@ def main():
         rec = run_resnet18_state(ctx, args, eng, N)
     elif args.workload == "resnet18-report":
         rec = run_resnet18_report(ctx, args, eng, N)
+    elif args.workload == "resnet18-secagg-state":
+        rec = run_resnet18_secagg_state(ctx, args, eng, N, parties)
     else:
         rec = run_resident(ctx, args, eng, mode, dtype, N, parties, hi - lo, P, lo, hi)
     if ctx.rank == 0:

@@ -104,6 +104,14 @@ int pgh_ingest_raw(pgh_ctx* ctx, int client, const void* flat, size_t nbytes, in
 /* Client diff as syft State protobuf bytes (model_manager.py:94-103 wire format, build-owned
  * schema restatement: DESIGN.md "State codec"); fp32 tensors only. */
 int pgh_ingest_state(pgh_ctx* ctx, int client, const uint8_t* pb, size_t n);
+/* One client's secure-aggregation shares as State bytes, one message per party (n_parties ==
+ * the parties of pgh_reserve): every tensor a packed-varint contents_int64 payload, the State
+ * order of pgh_set_layout (PySyft 0.2.9 int64 share tensors, test_basic_syft_operations.py:
+ * 388-454; wire schema restated, parity unpinned like pgh_ingest_state).  The payload bytes go
+ * to HBM as they are (PCIe carries the varints) and are decoded there (k_varint_decode); the
+ * host only checks the framing, counts the values per 64 KiB chunk and rejects varints longer
+ * than 10 bytes, cut-off payloads and count/layout mismatches (PGH_E_PARSE). */
+int pgh_ingest_state_shares(pgh_ctx* ctx, int client, int n_parties, const uint8_t* const* pbs, const size_t* ns);
 /* Fill slab rows [0, n_clients) with the deterministic synthetic diffs (or shares) of
  * SURVEY.md 8(d) for this shard, generated on the GPU (oracle/oracle.py restates them). */
 int pgh_synth_fill(pgh_ctx* ctx, uint64_t seed, int n_clients);
@@ -198,6 +206,13 @@ int pgh_state_scan(const uint8_t* pb, size_t n, int cap, int64_t* offsets, int64
  * cycle_manager.py:303): `tmpl` with every payload overwritten by `values` (P floats).  `out`
  * has n bytes; out == tmpl patches in place. */
 int pgh_state_patch(const uint8_t* tmpl, size_t n, const float* values, int64_t n_values, uint8_t* out);
+
+/* Secure-aggregation shares as State bytes: every tensor a TensorData.contents_int64 (packed
+ * varint; build-owned schema restatement, field 10).  Per tensor: payload byte offset, payload
+ * bytes and the number of int64 values, validated as protobuf's parser would (varints of at most
+ * 10 bytes, none cut off, count == shape numel when a shape is present).  PGH_E_PARSE otherwise. */
+int pgh_state_scan_i64(const uint8_t* pb, size_t n, int cap, int64_t* offsets, int64_t* nbytes, int64_t* counts,
+                       int* n_tensors);
 
 /* ---- report path (host only): base64 of the diff (fl_events.py:257) ----------------------- */
 size_t pgh_b64_decoded_cap(size_t n);

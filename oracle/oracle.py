@@ -242,6 +242,29 @@ def secagg_sum_torch(shares):
     return s, s.float() / 1000
 
 
+def secagg_close_state_torch(share_msgs, base=10, precision_fractional=3):
+    """Secure aggregation from share State bytes on the host, the way the syft path would: every
+    party message parsed (``StatePB.ParseFromString`` + ``torch.tensor(contents_int64)`` per
+    tensor, as ``unserialize_state_torch`` does for float32), the shares added as torch int64
+    (wrapping), the sum decoded ``.float() / base**prec``.  ``share_msgs[c][s]`` = bytes.
+    ``bench.py``'s cpu_baseline leg for ``resnet18-secagg-state``; ``tests/test_oracle.py`` checks
+    it against ``secagg_sum`` / ``fix_prec_decode``."""
+    import torch as th
+
+    from pygrid_amd.state_schema import classes
+
+    State = classes()["State"]
+    acc = None
+    for client in share_msgs:
+        for pb in client:
+            st = State()
+            st.ParseFromString(pb)
+            flat = th.cat([th.tensor(_state_tensor(stt).contents_data.contents_int64, dtype=th.int64).reshape(-1)
+                           for stt in st.tensors])
+            acc = flat if acc is None else acc + flat
+    return acc, acc.float() / float(base ** precision_fractional)
+
+
 def fix_prec_encode(x, base=10, precision_fractional=3):
     """``x.fix_prec()``: float32 ``x * base**prec`` (one rounding), truncated toward zero
     to int64 (syft 0.2.9 ``.long()``)."""

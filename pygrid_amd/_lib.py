@@ -68,6 +68,7 @@ SIGNATURES = {
     "pgh_reset": (_i, [_vp]),
     "pgh_ingest_raw": (_i, [_vp, _i, _vp, _sz, _i]),
     "pgh_ingest_state": (_i, [_vp, _i, C.c_char_p, _sz]),
+    "pgh_ingest_state_shares": (_i, [_vp, _i, _i, C.POINTER(C.c_char_p), C.POINTER(_sz)]),
     "pgh_synth_fill": (_i, [_vp, _u64, _i]),
     "pgh_synth_ingest": (_i, [_vp, _u64, _i, _i]),
     "pgh_set_weights": (_i, [_vp, C.POINTER(C.c_float), _i]),
@@ -98,6 +99,7 @@ SIGNATURES = {
     "pgh_reset_stats": (_i, [_vp]),
     "pgh_slab": (_i, [_vp, C.POINTER(_vp), _P64, _P64]),
     "pgh_state_scan": (_i, [C.c_char_p, _sz, _i, _P64, _P64, C.POINTER(C.c_int)]),
+    "pgh_state_scan_i64": (_i, [C.c_char_p, _sz, _i, _P64, _P64, _P64, C.POINTER(C.c_int)]),
     "pgh_state_patch": (_i, [C.c_char_p, _sz, _vp, _i64, _vp]),
     "pgh_b64_decoded_cap": (_sz, [_sz]),
     "pgh_b64_decode": (_i, [C.c_char_p, _sz, _vp, C.POINTER(_sz), _i]),

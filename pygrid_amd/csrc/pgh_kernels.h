@@ -76,6 +76,23 @@ hipError_t launch_synth_shares(int64_t* out, const SlabMap& m, int64_t ncols, in
                                int64_t p, uint64_t seed, int64_t client0, int64_t idx0, float enc_scale,
                                hipStream_t s);
 
+// Packed-varint int64 payloads (secagg shares as State bytes) decoded on the GPU.  The payload
+// bytes sit in HBM as received, each tensor's payload starting 16-byte aligned; they are cut into
+// chunks of at most VARINT_CHUNK bytes.  `first` = index (in the flat layout) of the first value
+// whose LAST byte lies in the chunk: the host counts terminator bytes per chunk while staging.
+constexpr int VARINT_CHUNK = 65536;
+struct VChunk {
+    int64_t off;       // chunk start, bytes from the payload buffer base (16-aligned)
+    int64_t span_off;  // start of the tensor payload holding the chunk (nothing before it is read)
+    int64_t first;     // flat index of the first value ending in the chunk
+    int32_t n;         // bytes in the chunk
+    int32_t pad;
+};
+// Decode every chunk into one slab row: value with flat index i goes to row[m.at(i - lo)] when
+// lo <= i < hi.  Requires validated input (no varint longer than 10 bytes).
+hipError_t launch_varint_decode(const uint8_t* bytes, const VChunk* chunks, int n_chunks, int64_t* row,
+                                const SlabMap& m, int64_t lo, int64_t hi, hipStream_t s);
+
 constexpr uint64_t STREAM_DIFF = 0, STREAM_CKPT = 1, STREAM_SECRET = 2, STREAM_SHARE = 3;
 constexpr float DIFF_SCALE = 2.6429e-7f;
 constexpr float CKPT_SCALE = 1.32145e-6f;

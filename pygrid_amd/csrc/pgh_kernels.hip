@@ -437,6 +437,70 @@ __global__ __launch_bounds__(BLOCK) void k_synth_shares(int64_t* out, SlabMap m,
     }
 }
 
+// Packed varints -> int64 (TensorData.contents_int64 of secagg share States).  One workgroup per
+// 64 KiB chunk, walked in 4 KiB windows staged in LDS with the 16 bytes before them (a varint is
+// at most 10 bytes, so its start is always in view).  Lane t owns bytes [16t, 16t + 16) of a
+// window: the terminators among them (bit 7 clear) end its values; a wave prefix sum (shuffles)
+// plus the per-wave totals in LDS give each value's flat index.  Byte-level work on a stream
+// PCIe fills at ~55 GB/s: the kernel only has to keep up, HBM traffic is ~2 bytes per byte in.
+__global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, const VChunk* chunks, int64_t* row,
+                                                       SlabMap m, int64_t lo, int64_t hi) {
+    __shared__ uint4 win4[1 + 256];  // [0]: the 16 bytes before the window, then the window
+    __shared__ int wsum[4];
+    const uint8_t* win = reinterpret_cast<const uint8_t*>(win4);
+    const VChunk ch = chunks[blockIdx.x];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    int64_t base = ch.first;
+    for (int w0 = 0; w0 < ch.n; w0 += 4096) {
+        const int64_t g = ch.off + w0;
+        const int p = 16 * t;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (w0 + p < ch.n) v = *reinterpret_cast<const uint4*>(bytes + g + p);
+        win4[1 + t] = v;
+        if (t == 0) {  // zero bytes read as terminators: nothing before a payload's first byte
+            uint4 b = make_uint4(0, 0, 0, 0);
+            if (g > ch.span_off) b = *reinterpret_cast<const uint4*>(bytes + g - 16);
+            win4[0] = b;
+        }
+        __syncthreads();
+        uint32_t tm = 0;
+        const int lim = ch.n - w0 - p;  // bytes of mine inside the chunk
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (k < lim && !(win[16 + p + k] & 0x80)) tm |= 1u << k;
+        const int cnt = __popc(tm);
+        int x = cnt;  // inclusive prefix over the wave
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int sw = wsum[w];
+            before += w < wave ? sw : 0;
+            total += sw;
+        }
+        int64_t idx = base + before + (x - cnt);
+        while (tm) {
+            const int k = __ffs(tm) - 1;
+            tm &= tm - 1;
+            const int end = 16 + p + k;
+            int st = end;
+            for (int j = 0; j < 9 && (win[st - 1] & 0x80); ++j) --st;  // st - 1 >= end - 10 >= 5
+            uint64_t val = 0;
+            for (int j = st; j <= end; ++j) val |= (uint64_t)(win[j] & 0x7F) << (7 * (j - st));
+            if (idx >= lo && idx < hi) row[m.at(idx - lo)] = (int64_t)val;
+            ++idx;
+        }
+        base += total;
+        __syncthreads();  // win / wsum are rewritten by the next window
+    }
+}
+
 int cu_count() {
     static int cached[64] = {0};
     int dev = 0;
@@ -643,6 +707,16 @@ hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_r
     }
     k_synth_f32<<<dim3((unsigned)gx, (unsigned)gy), BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id, row0,
                                                                   idx0, scale);
+    return hipGetLastError();
+}
+
+hipError_t launch_varint_decode(const uint8_t* bytes, const VChunk* chunks, int n_chunks, int64_t* row,
+                                const SlabMap& m, int64_t lo, int64_t hi, hipStream_t s) {
+    if (n_chunks < 0 || (n_chunks > 0 && (!bytes || !chunks || !row)) || (reinterpret_cast<uintptr_t>(bytes) & 15) ||
+        m.off != 0 || !valid_map(m, 0) || lo > hi)
+        return hipErrorInvalidValue;
+    if (n_chunks == 0) return hipSuccess;
+    k_varint_decode<<<(unsigned)n_chunks, 256, 0, s>>>(bytes, chunks, row, m, lo, hi);
     return hipGetLastError();
 }
 

@@ -3,6 +3,8 @@
 
 #include <cstring>
 
+#include <emmintrin.h>
+
 #include "../../include/pgh_api.h"
 
 namespace pgh_state {
@@ -82,7 +84,7 @@ bool parse_size(const uint8_t* b, const uint8_t* e, std::vector<int64_t>* dims) 
 }
 
 bool parse_tensor_data(const uint8_t* base, const uint8_t* b, const uint8_t* e, Span* s, std::string* msg) {
-    bool have_f32 = false;
+    bool have_f32 = false, have_i64 = false;
     bool ok = each_field(b, e, [&](uint32_t f, uint32_t wt, Reader& r) {
         const uint8_t *pb, *pe;
         if (f == TD_SHAPE && wt == 2) {
@@ -100,14 +102,32 @@ bool parse_tensor_data(const uint8_t* base, const uint8_t* b, const uint8_t* e, 
             if (have_f32) { *msg = "float32 payload split over several fields"; return false; }
             if (!r.len_delim(&pb, &pe)) return false;
             if ((pe - pb) % 4) { *msg = "float32 payload length is not a multiple of 4"; return false; }
+            if (have_i64) { *msg = "tensor holds both float32 and int64 payloads"; return false; }
             s->offset = (size_t)(pb - base);
             s->count = (pe - pb) / 4;
+            s->nbytes = (size_t)(pe - pb);
             have_f32 = true;
+            return true;
+        }
+        if (f == TD_I64) {
+            if (wt != 2) { *msg = "unpacked int64 payload is not supported"; return false; }
+            if (have_i64) { *msg = "int64 payload split over several fields"; return false; }
+            if (have_f32) { *msg = "tensor holds both float32 and int64 payloads"; return false; }
+            if (!r.len_delim(&pb, &pe)) return false;
+            s->offset = (size_t)(pb - base);
+            s->nbytes = (size_t)(pe - pb);
+            s->i64 = true;
+            have_i64 = true;
             return true;
         }
         return r.skip(wt);
     });
-    if (ok && !have_f32) {
+    if (ok && have_i64) {  // element count comes from the shape; the varint pass checks the payload
+        int64_t numel = 1;
+        for (auto d : s->shape) numel *= d;
+        s->count = s->shape.empty() ? -1 : numel;
+    }
+    if (ok && !have_f32 && !have_i64) {
         // proto3 omits an empty packed field: a zero-element tensor has no payload
         int64_t numel = 1;
         for (auto d : s->shape) numel *= d;
@@ -162,7 +182,7 @@ bool parse_state_tensor(const uint8_t* base, const uint8_t* b, const uint8_t* e,
 
 }  // namespace
 
-int scan(const uint8_t* pb, size_t n, std::vector<Span>* spans, std::string* msg) {
+int walk(const uint8_t* pb, size_t n, std::vector<Span>* spans, std::string* msg) {
     spans->clear();
     msg->clear();
     if (!pb && n) { *msg = "null buffer"; return PGH_E_PARSE; }
@@ -182,8 +202,18 @@ int scan(const uint8_t* pb, size_t n, std::vector<Span>* spans, std::string* msg
         if (msg->empty()) *msg = "truncated or malformed protobuf";
         return PGH_E_PARSE;
     }
+    return 0;
+}
+
+int scan(const uint8_t* pb, size_t n, std::vector<Span>* spans, std::string* msg) {
+    int rc = walk(pb, n, spans, msg);
+    if (rc) return rc;
     for (size_t t = 0; t < spans->size(); ++t) {
         const Span& s = (*spans)[t];
+        if (s.i64) {
+            *msg = "tensor " + std::to_string(t) + " holds an int64 payload, expected float32";
+            return PGH_E_PARSE;
+        }
         int64_t numel = 1;
         for (auto d : s.shape) {
             if (d < 0) { *msg = "negative dimension in tensor " + std::to_string(t); return PGH_E_PARSE; }
@@ -200,6 +230,65 @@ int scan(const uint8_t* pb, size_t n, std::vector<Span>* spans, std::string* msg
         }
     }
     return 0;
+}
+
+int scan_i64(const uint8_t* pb, size_t n, std::vector<Span>* spans, std::string* msg) {
+    int rc = walk(pb, n, spans, msg);
+    if (rc) return rc;
+    for (size_t t = 0; t < spans->size(); ++t) {
+        Span& s = (*spans)[t];
+        for (auto d : s.shape)
+            if (d < 0) { *msg = "negative dimension in tensor " + std::to_string(t); return PGH_E_PARSE; }
+        if (!s.i64 && s.nbytes) {
+            *msg = "tensor " + std::to_string(t) + " holds a float32 payload, expected int64 shares";
+            return PGH_E_PARSE;
+        }
+        if (!s.dtype.empty() && s.dtype != "int64" && s.dtype != "torch.int64") {
+            *msg = "tensor " + std::to_string(t) + " has dtype '" + s.dtype + "', expected int64";
+            return PGH_E_PARSE;
+        }
+    }
+    return 0;
+}
+
+namespace {
+// bit i = bit 7 of p[i] (the varint continuation flag), for 64 bytes (SSE2 is x86-64 baseline)
+inline uint64_t msb64(const uint8_t* p) {
+    uint64_t m = 0;
+    for (int k = 0; k < 4; ++k)
+        m |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * k)))
+             << (16 * k);
+    return m;
+}
+}  // namespace
+
+VarintStats varint_stats(const uint8_t* p, size_t n) {
+    VarintStats st;
+    int64_t run = 0;        // continuation bytes since the last terminator
+    bool seen = false;      // a terminator seen yet
+    size_t i = 0;
+    for (; i + 64 <= n; i += 64) {
+        const uint64_t m = msb64(p + i);  // bit j: byte i + j is a continuation byte
+        if (m == ~0ull) { run += 64; if (run > 9) st.overlong = true; continue; }
+        const uint64_t t = ~m;
+        const int lead = __builtin_ctzll(t);  // continuation bytes before the first terminator here
+        if (run + lead > 9) st.overlong = true;
+        if (!seen) { st.lead = run + lead; seen = true; }
+        // runs of >= 10 continuation bytes strictly inside the 64 (the top run is carried on)
+        const uint64_t r2 = m & (m >> 1), r4 = r2 & (r2 >> 2), r8 = r4 & (r4 >> 4);  // bit j: j..j+1/3/7 set
+        if (r8 & (r2 >> 8)) st.overlong = true;                                        // j..j+9 set
+        st.terminators += __builtin_popcountll(t);
+        run = __builtin_clzll(t);
+    }
+    for (; i < n; ++i) {
+        if (p[i] & 0x80) { if (++run > 9) st.overlong = true; continue; }
+        if (!seen) { st.lead = run; seen = true; }
+        st.terminators += 1;
+        run = 0;
+    }
+    if (!seen) st.lead = run;
+    st.trail = run;
+    return st;
 }
 
 int decode_f32(const uint8_t* pb, size_t n, const std::vector<int64_t>& numel, float* out, std::string* msg) {
@@ -239,6 +328,31 @@ int pgh_state_scan(const uint8_t* pb, size_t n, int cap, int64_t* offsets, int64
     for (int t = 0; t < cap && t < (int)spans.size(); ++t) {
         if (offsets) offsets[t] = (int64_t)spans[t].offset;
         if (counts) counts[t] = spans[t].count;
+    }
+    return PGH_OK;
+}
+
+// int64 shares: per tensor the payload byte range and the number of packed varints it holds,
+// validated like protobuf's parser would (no varint longer than 10 bytes, none cut off at the
+// end of the payload, the count equal to the shape's element count when a shape is given).
+int pgh_state_scan_i64(const uint8_t* pb, size_t n, int cap, int64_t* offsets, int64_t* nbytes, int64_t* counts,
+                       int* n_tensors) {
+    if (!n_tensors) return PGH_E_ARG;
+    std::vector<pgh_state::Span> spans;
+    std::string msg;
+    int rc = pgh_state::scan_i64(pb, n, &spans, &msg);
+    if (rc) return rc;
+    *n_tensors = (int)spans.size();
+    for (int t = 0; t < (int)spans.size(); ++t) {
+        const auto& s = spans[t];
+        const pgh_state::VarintStats st = pgh_state::varint_stats(pb + s.offset, s.nbytes);
+        if (st.overlong || st.trail) return PGH_E_PARSE;
+        if (s.count >= 0 && st.terminators != s.count) return PGH_E_PARSE;
+        if (t < cap) {
+            if (offsets) offsets[t] = (int64_t)s.offset;
+            if (nbytes) nbytes[t] = (int64_t)s.nbytes;
+            if (counts) counts[t] = st.terminators;
+        }
     }
     return PGH_OK;
 }

@@ -164,6 +164,15 @@ class Engine:
     def ingest_state(self, client: int, pb: bytes):
         self._check(self._lib.pgh_ingest_state(self._h, int(client), pb, len(pb)), f"ingest_state client {client}")
 
+    def ingest_state_shares(self, client: int, messages: Sequence[bytes]):
+        """One client's secure-aggregation shares, one State message per party (packed-varint
+        int64 payloads, decoded on the GPU; ``pgh_ingest_state_shares``)."""
+        n = len(messages)
+        ptrs = (C.c_char_p * max(n, 1))(*messages)
+        lens = (C.c_size_t * max(n, 1))(*[len(m) for m in messages])
+        self._check(self._lib.pgh_ingest_state_shares(self._h, int(client), n, ptrs, lens),
+                    f"ingest_state_shares client {client}")
+
     def synth_fill(self, seed: int, n_clients: int):
         self._check(self._lib.pgh_synth_fill(self._h, C.c_uint64(seed), int(n_clients)), "synth_fill")
 

@@ -40,6 +40,22 @@ def scan(pb: bytes) -> List[Tuple[int, int]]:
     return [(offs[i], cnts[i]) for i in range(k)]
 
 
+def scan_shares(pb: bytes) -> List[Tuple[int, int, int]]:
+    """(payload byte offset, payload bytes, int64 value count) of every tensor of a secure-
+    aggregation share State (packed-varint contents_int64), validated like protobuf's parser."""
+    lib = _lib.load()
+    n = C.c_int(0)
+    rc = lib.pgh_state_scan_i64(pb, len(pb), 0, None, None, None, C.byref(n))
+    if rc != 0:
+        raise StateParseError(f"malformed share State message ({_lib.STATUS_NAMES.get(rc, rc)})", status=rc)
+    k = n.value
+    offs, nbs, cnts = ((C.c_int64 * max(k, 1))() for _ in range(3))
+    rc = lib.pgh_state_scan_i64(pb, len(pb), k, offs, nbs, cnts, C.byref(n))
+    if rc != 0:
+        raise StateParseError("malformed share State message", status=rc)
+    return [(offs[i], nbs[i], cnts[i]) for i in range(k)]
+
+
 def tensor_numels(pb: bytes) -> List[int]:
     return [c for _, c in scan(pb)]
 

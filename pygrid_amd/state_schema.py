@@ -112,6 +112,89 @@ def build_state(tensors, ids=None, as_param=False) -> bytes:
     return st.SerializeToString()
 
 
+def build_state_i64(tensors, ids=None) -> bytes:
+    """State bytes of int64 share tensors (TensorData.contents_int64, packed varint) via
+    google.protobuf: what a syft stack would send for one party's additive shares."""
+    import numpy as np
+
+    cls = classes()
+    st = cls["State"]()
+    for k, t in enumerate(tensors):
+        a = np.asarray(t, dtype=np.int64)
+        tid = (ids[k] if ids is not None else 2000 + k)
+        ph = st.placeholders.add()
+        ph.id.id_int = tid
+        stt = st.tensors.add()
+        tt = stt.torch_tensor
+        tt.id.id_int = tid
+        tt.serializer = SERIALIZER_ALL
+        tt.contents_data.shape.dims.extend(list(a.shape))
+        tt.contents_data.dtype = "int64"
+        tt.contents_data.contents_int64.extend(a.reshape(-1).tolist())
+    return st.SerializeToString()
+
+
+def parse_state_i64(pb: bytes):
+    """[int64 array] of a share State via google.protobuf (independent of the C++ walker and
+    the GPU decoder)."""
+    import numpy as np
+
+    st = classes()["State"]()
+    st.ParseFromString(pb)
+    out = []
+    for stt in st.tensors:
+        tt = stt.torch_tensor if stt.HasField("torch_tensor") else stt.torch_param.tensor
+        shape = tuple(tt.contents_data.shape.dims)
+        out.append(np.asarray(tt.contents_data.contents_int64, dtype=np.int64).reshape(shape))
+    return out
+
+
+def varint_encode(values) -> bytes:
+    """Packed-varint bytes of int64 values (two's complement as uint64: negatives take 10 bytes),
+    vectorised with numpy."""
+    import numpy as np
+
+    v = np.ascontiguousarray(values, dtype=np.int64).reshape(-1).view(np.uint64)
+    if v.size == 0:
+        return b""
+    nbits = np.zeros(v.size, dtype=np.int64)
+    x = v.copy()
+    for _ in range(10):  # bytes per value: ceil(bit length / 7), at least 1
+        nz = x != 0
+        nbits += nz
+        x >>= np.uint64(7)
+    nb = np.maximum(nbits, 1)
+    starts = np.concatenate(([0], np.cumsum(nb)[:-1]))
+    out = np.empty(int(nb.sum()), dtype=np.uint8)
+    for j in range(10):
+        sel = nb > j
+        byte = ((v[sel] >> np.uint64(7 * j)) & np.uint64(0x7F)).astype(np.uint8)
+        byte |= np.where(nb[sel] > j + 1, 0x80, 0).astype(np.uint8)
+        out[starts[sel] + j] = byte
+    return out.tobytes()
+
+
+def build_state_i64_fast(tensors, ids=None) -> bytes:
+    """Byte-identical to ``build_state_i64(tensors, ids)`` with the varint payload encoded by numpy
+    (``varint_encode``): for building large share messages (bench, tests)."""
+    import numpy as np
+
+    parts = []
+    for k, t in enumerate(tensors):
+        tid = ids[k] if ids is not None else 2000 + k
+        parts.append(_field(1, 2, _field(1, 2, _field(2, 0, value=tid) if tid else b"")))
+    for k, t in enumerate(tensors):
+        a = np.ascontiguousarray(t, dtype=np.int64)
+        tid = ids[k] if ids is not None else 2000 + k
+        dims = b"".join(_varint(d) for d in a.shape)
+        td = (_field(1, 2, _field(1, 2, dims) if dims else b"") + _field(2, 2, b"int64")
+              + (_field(10, 2, varint_encode(a)) if a.size else b""))
+        tt = (_field(1, 2, _field(2, 0, value=tid) if tid else b"") + _field(2, 0, value=SERIALIZER_ALL)
+              + _field(4, 2, td))
+        parts.append(_field(2, 2, _field(1, 2, tt)))
+    return b"".join(parts)
+
+
 def parse_state(pb: bytes):
     """[(shape, float32 array)] via google.protobuf (independent of the C++ walker)."""
     import numpy as np

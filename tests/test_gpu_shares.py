@@ -1,0 +1,180 @@
+"""GPU: secure-aggregation shares ingested as State bytes (packed-varint contents_int64, decoded
+on the GPU by k_varint_decode) -- bit-exact against google.protobuf's parse of the same bytes
+and against the numpy oracle's Z_2^64 sum / fixed-point decode (PySyft 0.2.9 semantics,
+test_basic_syft_operations.py:388-454; wire schema restated, parity unpinned)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pygrid_amd.exceptions import PyGridError
+from pygrid_amd.state_schema import build_state_i64_fast, parse_state_i64, varint_encode, _field, _varint
+
+pytestmark = pytest.mark.gpu
+
+I64_MIN, I64_MAX = -2**63, 2**63 - 1
+
+
+def split(flat, numel):
+    out, o = [], 0
+    for n in numel:
+        out.append(flat[o:o + n])
+        o += n
+    return out
+
+
+def every_length_values(n, rng):
+    """Values whose varints take 1..10 bytes, interleaved at random, plus the int64 extremes."""
+    bits = rng.integers(0, 64, n)
+    v = (rng.integers(0, 2**62, n, dtype=np.int64).view(np.uint64) >> np.uint64(0)) & \
+        ((np.uint64(1) << bits.astype(np.uint64)) - np.uint64(1))
+    v = v.view(np.int64).copy()
+    neg = rng.random(n) < 0.3
+    v[neg] = -v[neg] - 1
+    v[: min(n, 6)] = [0, 1, -1, I64_MIN, I64_MAX, 127][: min(n, 6)]
+    return v
+
+
+def shares_for(rng, n_clients, n_parties, P, kind="uniform"):
+    if kind == "uniform":
+        return rng.integers(I64_MIN, I64_MAX, (n_clients, n_parties, P), dtype=np.int64, endpoint=True)
+    return np.stack([np.stack([every_length_values(P, rng) for _ in range(n_parties)]) for _ in range(n_clients)])
+
+
+def ingest_all(engine, numel, sh):
+    N, S, _ = sh.shape
+    for c in range(N):
+        engine.ingest_state_shares(c, [build_state_i64_fast(split(sh[c, s], numel)) for s in range(S)])
+
+
+@pytest.mark.parametrize("numel,kind", [
+    ([311_650], "uniform"),
+    ([307_328, 392, 3_920, 10], "lengths"),            # MNIST 784-392-10 tensors
+    ([5, 0, 70_000, 1, 0, 123_457], "lengths"),        # empty tensors, multi-chunk payloads
+    ([9_000], "lengths"),                              # one chunk, a partial window
+])
+def test_share_state_ingest_matches_protobuf_and_oracle(engine, numel, kind):
+    rng = np.random.default_rng(sum(numel) % 1000)
+    P, N, S = sum(numel), 3, 2
+    sh = shares_for(rng, N, S, P, kind)
+    engine.set_layout(numel)
+    engine.reserve(N, 1, S)
+    ingest_all(engine, numel, sh)
+    s, d = engine.secagg(10, 3)
+    want = O.secagg_sum(sh)
+    assert np.array_equal(s, want)
+    assert np.array_equal(d.view(np.uint32), O.fix_prec_decode(want).view(np.uint32))
+
+
+def test_share_state_rows_decode_exactly(engine):
+    """One party, one client: the summed row IS the decoded payload; checked against
+    google.protobuf's parse of the very bytes that were ingested."""
+    rng = np.random.default_rng(5)
+    numel = [70_001, 3, 200_000]
+    vals = every_length_values(sum(numel), rng)
+    pb = build_state_i64_fast(split(vals, numel))
+    want = np.concatenate([a.reshape(-1) for a in parse_state_i64(pb)])
+    assert np.array_equal(want, vals)
+    engine.set_layout(numel)
+    engine.reserve(1, 1, 1)
+    engine.ingest_state_shares(0, [pb])
+    s, _ = engine.secagg(10, 3)
+    assert np.array_equal(s, want)
+
+
+def test_share_state_varints_across_chunk_edges(engine):
+    """A 10-byte varint straddling every 64 KiB chunk edge and 4 KiB window edge of the payload."""
+    P = 40_000  # 10-byte varints: 400,000 payload bytes, 7 chunks
+    vals = np.full(P, -5, dtype=np.int64)  # negative: 10 bytes each
+    vals[::7] = 3                           # 1-byte varints shift the alignment
+    pb = build_state_i64_fast([vals])
+    payload = varint_encode(vals)
+    ends = np.flatnonzero(np.frombuffer(payload, np.uint8) < 0x80)
+    assert any(e % 65536 < 9 for e in ends)  # some varint ends just past a chunk edge
+    engine.set_layout([P])
+    engine.reserve(1, 1, 1)
+    engine.ingest_state_shares(0, [pb])
+    s, _ = engine.secagg(10, 3)
+    assert np.array_equal(s, vals)
+
+
+def test_share_state_sharded_context(engine):
+    """A param shard decodes the whole payload and keeps its range (all ranks get every client's
+    shares when clients are not sharded)."""
+    rng = np.random.default_rng(11)
+    numel = [100_000, 50_000]
+    P, N, S = sum(numel), 2, 2
+    sh = shares_for(rng, N, S, P, "lengths")
+    lo, hi = 70_016, 130_048
+    engine.set_layout(numel)
+    engine.set_shard(lo, hi)
+    try:
+        engine.reserve(N, 1, S)
+        ingest_all(engine, numel, sh)
+        s, _ = engine.secagg(10, 3)
+    finally:
+        engine.set_layout(numel)
+    assert np.array_equal(s, O.secagg_sum(sh)[lo:hi])
+
+
+def test_share_state_stream_ring_equals_resident(engine):
+    rng = np.random.default_rng(12)
+    numel = [66_000, 17]
+    P, N, S = sum(numel), 9, 2
+    sh = shares_for(rng, N, S, P, "uniform")
+    engine.set_layout(numel)
+    engine.reserve(4, 1, S)
+    engine.stream_begin(16, 2)  # PGH_STREAM_SECAGG, fold batch 2
+    ingest_all(engine, numel, sh)
+    s, d = engine.stream_finish_secagg(10, 3)
+    assert np.array_equal(s, O.secagg_sum(sh))
+
+
+def _bad_payload_message(payload: bytes, n_values: int) -> bytes:
+    td = _field(1, 2, _field(1, 2, _varint(n_values))) + _field(2, 2, b"int64") + _field(10, 2, payload)
+    tt = _field(2, 0, value=4) + _field(4, 2, td)
+    return _field(2, 2, _field(1, 2, tt))
+
+
+@pytest.mark.parametrize("case", ["overlong_at_chunk_edge", "overlong_inside", "cut_off", "count", "float32"])
+def test_share_state_rejects_malformed_and_leaves_slab(engine, case):
+    P = 40_000  # ~120 KB of payload: two chunks
+    good = np.arange(P, dtype=np.int64) * 3 - 7
+    payload = bytearray(varint_encode(good))
+    n_values = P
+    if case == "overlong_at_chunk_edge":   # 12 continuation bytes around byte 65,536
+        payload[65_530:65_542] = b"\xff" * 12
+    elif case == "overlong_inside":
+        payload[1_000:1_011] = b"\x81" * 11
+    elif case == "cut_off":
+        payload[-1] |= 0x80
+    elif case == "count":
+        n_values = P + 1
+    msg = _bad_payload_message(bytes(payload), n_values)
+    if case == "float32":
+        from pygrid_amd.state_schema import build_state_fast
+        msg = build_state_fast([np.zeros(P, np.float32)])
+    engine.set_layout([P])
+    engine.reserve(1, 1, 1)
+    engine.ingest_state_shares(0, [build_state_i64_fast([good])])
+    with pytest.raises(PyGridError):
+        engine.ingest_state_shares(0, [msg])
+    s, _ = engine.secagg(10, 3)  # the good row is still there, untouched by the rejected message
+    assert np.array_equal(s, good)
+
+
+def test_share_state_resnet18_scale_sampled(engine):
+    """ResNet-18 layout (62 tensors, P = 11,689,512) x 2 clients x 2 parties of uniform shares
+    (~10 bytes per value on the wire): full sum compared with the oracle."""
+    from pygrid_amd.workloads import RESNET18_SHAPES
+
+    numel = [int(np.prod(s)) for s in RESNET18_SHAPES]
+    P, N, S = sum(numel), 2, 2
+    rng = np.random.default_rng(13)
+    sh = rng.integers(I64_MIN, I64_MAX, (N, S, P), dtype=np.int64, endpoint=True)
+    engine.set_layout(numel)
+    engine.reserve(N, 1, S)
+    ingest_all(engine, numel, sh)
+    s, d = engine.secagg(10, 3)
+    want = O.secagg_sum(sh)
+    assert np.array_equal(s, want)
+    assert np.array_equal(d.view(np.uint32), O.fix_prec_decode(want).view(np.uint32))

@@ -10,7 +10,7 @@ import torch as th
 from oracle import oracle as O
 from pygrid_amd import ITERATIVE_MEAN, MEAN, WEIGHTED_MEAN, PlanNotAcceleratedError, StateParseError
 from pygrid_amd import cycle, state
-from pygrid_amd.state_schema import build_state, classes, parse_state
+from pygrid_amd.state_schema import build_state, classes, parse_state, varint_encode
 
 F = np.float32
 
@@ -217,3 +217,73 @@ def test_build_state_fast_is_byte_identical():
     for ts in (_tensors(3), [np.zeros((0,), F), np.ones((2, 3), F), np.array([1.5], F)]):
         assert build_state_fast(ts) == build_state(ts)
         assert build_state_fast(ts, ids=[7, 0, 99, 5][:len(ts)]) == build_state(ts, ids=[7, 0, 99, 5][:len(ts)])
+
+
+# ---- secure-aggregation shares as State bytes (packed-varint int64, host-side checks) -----------
+def _every_length(n, seed):
+    rng = np.random.default_rng(seed)
+    v = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    sh = rng.integers(0, 64, n).astype(np.uint64)
+    v = (v.view(np.uint64) >> sh).view(np.int64)  # 1..10-byte varints
+    v[: min(n, 4)] = [0, -1, -2**63, 2**63 - 1][: min(n, 4)]
+    return v
+
+
+def test_share_state_builders_agree_with_google_protobuf():
+    from pygrid_amd.state_schema import build_state_i64, build_state_i64_fast, parse_state_i64
+
+    ts = [_every_length(n, n).reshape(s) for n, s in ((12, (3, 4)), (0, (0,)), (1000, (10, 100)), (1, (1,)))]
+    fast = build_state_i64_fast(ts)
+    assert fast == build_state_i64(ts)
+    for got, want in zip(parse_state_i64(fast), ts):
+        assert np.array_equal(got, want)
+    spans = state.scan_shares(fast)
+    assert [c for _, _, c in spans] == [t.size for t in ts]
+    assert all(nb == len(varint_encode(t)) for (_, nb, _), t in zip(spans, ts))
+
+
+def test_varint_encode_matches_protobuf_varints():
+    from pygrid_amd.state_schema import _varint
+
+    v = _every_length(3000, 7)
+    assert varint_encode(v) == b"".join(_varint(int(x) & (2**64 - 1)) for x in v)
+
+
+@pytest.mark.parametrize("n", [1, 9, 63, 64, 65, 127, 640, 4097])
+def test_share_scan_counts_and_overlong_fuzz(n):
+    """The walker's per-payload varint count and 10-byte limit against a byte-by-byte Python
+    reference, on random payload bytes around every 64-byte block edge."""
+    from pygrid_amd.state_schema import _field, _varint
+
+    rng = np.random.default_rng(n)
+    for trial in range(40):
+        p = rng.integers(0, 256, n, dtype=np.uint8)
+        cont_rate = rng.choice([0.3, 0.7, 0.9, 0.97])
+        p = np.where(rng.random(n) < cont_rate, p | 0x80, p & 0x7F).astype(np.uint8)
+        p[-1] &= 0x7F if trial % 3 else 0xFF
+        payload = p.tobytes()
+        run, ok, count = 0, True, 0
+        for b in payload:
+            if b & 0x80:
+                run += 1
+                ok = ok and run <= 9
+            else:
+                count += 1
+                run = 0
+        ok = ok and run == 0
+        td = _field(2, 2, b"int64") + _field(10, 2, payload)
+        msg = _field(2, 2, _field(1, 2, _field(4, 2, td)))
+        if ok:
+            assert state.scan_shares(msg) == [(len(msg) - n, n, count)]
+        else:
+            with pytest.raises(StateParseError):
+                state.scan_shares(msg)
+
+
+def test_share_scan_rejects_float_payload_and_f32_scan_rejects_shares():
+    from pygrid_amd.state_schema import build_state_i64_fast
+
+    with pytest.raises(StateParseError):
+        state.scan_shares(build_state([np.ones(3, F)]))
+    with pytest.raises(StateParseError):
+        state.scan(build_state_i64_fast([np.arange(3, dtype=np.int64)]))

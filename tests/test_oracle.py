@@ -190,6 +190,21 @@ def test_state_bytes_cycle_close_restatement(gold):
     assert len(new) == len(ck_pb)  # same framing, payloads replaced
 
 
+def test_secagg_state_restatement_matches_oracle():
+    """oracle.secagg_close_state_torch (share State bytes -> torch int64 adds -> decode) equals the
+    numpy share sum and decode, including int64 wrap."""
+    from pygrid_amd.state_schema import build_state_i64_fast
+
+    rng = np.random.default_rng(21)
+    sh = rng.integers(-2**63, 2**63 - 1, (4, 2, 777), dtype=np.int64, endpoint=True)
+    sh[0, 0, :3] = [2**63 - 1, -2**63, -1]
+    msgs = [[build_state_i64_fast([sh[c, s][:500], sh[c, s][500:]]) for s in range(2)] for c in range(4)]
+    s, d = O.secagg_close_state_torch(msgs)
+    want = O.secagg_sum(sh)
+    assert np.array_equal(s.numpy(), want)
+    assert np.array_equal(bits(d.numpy()), bits(O.fix_prec_decode(want)))
+
+
 # ---- secure aggregation ------------------------------------------------------------------------
 def test_smpc_integer_share_reconstructs_exactly(gold):
     """test_basic_syft_operations.py:388-394."""
