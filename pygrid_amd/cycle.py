@@ -166,6 +166,23 @@ class CycleAggregator:
         return self.engine.secagg(base, precision_fractional)
 
 
+    def secure_aggregate_states(self, numel: Sequence[int], share_msgs: Sequence[Sequence[bytes]],
+                                base: int = 10, precision_fractional: int = 3):
+        """Secure aggregation from the wire: ``share_msgs[client][party]`` = State bytes of that
+        party's int64 shares (packed-varint ``contents_int64``, tensors in ``numel`` order).  The
+        payloads are decoded on the GPU; returns (int64 wrap-sum [P], float32 decoded [P])."""
+        if len(share_msgs) == 0:
+            raise AggregationError("no shares to aggregate")
+        parties = len(share_msgs[0])
+        self._prepare(numel, len(share_msgs), I64, parties)
+        self._resident = None
+        for c, msgs in enumerate(share_msgs):
+            if len(msgs) != parties:
+                raise AggregationError(f"client {c} sent {len(msgs)} share messages, client 0 sent {parties}")
+            self.engine.ingest_state_shares(c, msgs)
+        return self.engine.secagg(base, precision_fractional)
+
+
 def make_average_plan_diffs(aggregator: CycleAggregator, model_manager, process_manager, plan_manager,
                             original: Callable) -> Callable:
     """Build a drop-in ``CycleManager._average_plan_diffs(self, server_config, cycle)``.

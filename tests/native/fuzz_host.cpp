@@ -39,6 +39,25 @@ static std::vector<uint8_t> make_state(std::mt19937_64& rng, int t) {
     return st;
 }
 
+// A valid share State: every tensor a packed-varint contents_int64 payload (field 10).
+static std::vector<uint8_t> make_share_state(std::mt19937_64& rng, int t) {
+    std::vector<uint8_t> st;
+    for (int k = 0; k < t; ++k) {
+        const int n = (int)(rng() % 200);
+        std::vector<uint8_t> dims, size, td, tt, stt, payload;
+        for (int i = 0; i < n; ++i) put_varint(payload, rng() >> (rng() % 64));
+        put_varint(dims, (uint64_t)n);
+        put_field(size, 1, dims);
+        put_field(td, 1, size);
+        put_field(td, 2, std::vector<uint8_t>{'i', 'n', 't', '6', '4'});
+        if (n) put_field(td, 10, payload);
+        put_field(tt, 4, td);
+        put_field(stt, 1, tt);
+        put_field(st, 2, stt);
+    }
+    return st;
+}
+
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 20000;
     std::mt19937_64 rng(12345);
@@ -84,6 +103,33 @@ int main(int argc, char** argv) {
             ++rejected;
         }
         delete[] buf;
+        // int64 share States: the walker plus the varint count / overlong pass
+        std::vector<uint8_t> sh = make_share_state(rng, 1 + (int)(rng() % 4));
+        const int smuts = (int)(rng() % 4);
+        for (int m = 0; m < smuts && !sh.empty(); ++m) {
+            const size_t i = rng() % sh.size();
+            switch (rng() % 3) {
+            case 0: sh[i] |= 0x80; break;   // lengthen a varint
+            case 1: sh.resize(i); break;
+            default: sh[i] = (uint8_t)rng(); break;
+            }
+        }
+        uint8_t* sbuf = new uint8_t[sh.size() ? sh.size() : 1];
+        if (!sh.empty()) std::memcpy(sbuf, sh.data(), sh.size());
+        int64_t so[8], sn[8], sc[8];
+        nt = 0;
+        if (pgh_state_scan_i64(sbuf, sh.size(), 8, so, sn, sc, &nt) == PGH_OK) {
+            ++parsed;
+            for (int k = 0; k < nt && k < 8; ++k) {
+                if (so[k] < 0 || (size_t)(so[k] + sn[k]) > sh.size() || sc[k] > sn[k]) { std::printf("share span out of range\n"); return 6; }
+                int64_t term = 0;  // the count is the number of terminator bytes
+                for (int64_t i = 0; i < sn[k]; ++i) term += !(sbuf[so[k] + i] & 0x80);
+                if (term != sc[k]) { std::printf("share count mismatch\n"); return 7; }
+            }
+        } else {
+            ++rejected;
+        }
+        delete[] sbuf;
         // base64 text with random junk
         std::string s;
         const int len = (int)(rng() % 64);

@@ -178,3 +178,17 @@ def test_share_state_resnet18_scale_sampled(engine):
     want = O.secagg_sum(sh)
     assert np.array_equal(s, want)
     assert np.array_equal(d.view(np.uint32), O.fix_prec_decode(want).view(np.uint32))
+
+
+def test_cycle_aggregator_secure_aggregate_states(engine):
+    from pygrid_amd.cycle import CycleAggregator
+
+    rng = np.random.default_rng(14)
+    numel = [307_328, 392, 3_920, 10]
+    P, N, S = sum(numel), 4, 3
+    sh = shares_for(rng, N, S, P, "uniform")
+    msgs = [[build_state_i64_fast(split(sh[c, s], numel)) for s in range(S)] for c in range(N)]
+    s, d = CycleAggregator(engine).secure_aggregate_states(numel, msgs)
+    want = O.secagg_sum(sh)
+    assert np.array_equal(s, want)
+    assert np.array_equal(d.view(np.uint32), O.fix_prec_decode(want).view(np.uint32))
