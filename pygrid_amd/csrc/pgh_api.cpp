@@ -1134,9 +1134,10 @@ struct ShareMsg {
     std::vector<int> span_of;              // tensor of each chunk
     std::vector<pgh_state::VarintStats> st;
     size_t bytes = 0;                      // device buffer bytes (payloads + alignment padding)
+    size_t base = 0;                       // where they start in the device buffer
 };
 
-int plan_share_msg(pgh_ctx* c, const uint8_t* pb, size_t n, int client, int party, ShareMsg* m) {
+int plan_share_msg(pgh_ctx* c, const uint8_t* pb, size_t n, int client, int party, size_t base, ShareMsg* m) {
     std::vector<pgh_state::Span> spans;
     std::string msg;
     int rc = pgh_state::scan_i64(pb, n, &spans, &msg);
@@ -1144,7 +1145,7 @@ int plan_share_msg(pgh_ctx* c, const uint8_t* pb, size_t n, int client, int part
     if (spans.size() != c->numel.size())
         return fail(c, PGH_E_PARSE, "client %d party %d shares State holds %zu tensors, layout has %zu", client, party,
                     spans.size(), c->numel.size());
-    size_t pos = 0;
+    size_t pos = base;  // this party's payloads follow the previous party's in the device buffer
     for (size_t t = 0; t < spans.size(); ++t) {
         const auto& sp = spans[t];
         if (sp.count >= 0 && sp.count != c->numel[t])
@@ -1159,7 +1160,8 @@ int plan_share_msg(pgh_ctx* c, const uint8_t* pb, size_t n, int client, int part
         }
         pos += sp.nbytes;
     }
-    m->bytes = pos;
+    m->bytes = pos - base;
+    m->base = base;
     m->st.resize(m->chunks.size());
     return PGH_OK;
 }
@@ -1216,11 +1218,9 @@ int grow_device(pgh_ctx* c, void** p, size_t* cap, size_t need, const char* what
 }
 
 // Stage one party message: chunk bytes -> pinned ring (copied and counted by the pool threads)
-// -> HBM byte buffer, then the chunk table, then the decode into slab row (slot, party); all on
-// the copy stream, so a fold ordered after ingest sees the decoded row.
-int ingest_share_msg(pgh_ctx* c, ShareMsg& m, int client, int party, int slot) {
+// -> its region of the HBM byte buffer, on the copy stream.  Nothing is decoded yet.
+int stage_share_msg(pgh_ctx* c, ShareMsg& m) {
     const double t0 = now_ms();
-    RC(grow_device(c, (void**)&c->d_vbytes, &c->vbytes_cap, m.bytes + 16, "share payload buffer"));
     const size_t nk = m.chunks.size();
     size_t k = 0;
     while (k < nk) {
@@ -1247,12 +1247,19 @@ int ingest_share_msg(pgh_ctx* c, ShareMsg& m, int client, int party, int slot) {
     }
     c->st.h2d_ms_total += now_ms() - t0;
     c->st.h2d_bytes_total += m.bytes;
-    RC(check_share_msg(c, &m, client, party));  // nothing decoded into the slab on bad input
-    if (nk == 0) return PGH_OK;                  // every tensor empty
-    // chunk table: pinned staging (waits for its previous upload), device copy, decode
+    return PGH_OK;
+}
+
+// Every party validated: one chunk table for all of them, then one decode per party into its
+// slab row (the shard's range), on the copy stream.
+int decode_share_msgs(pgh_ctx* c, std::vector<ShareMsg>& msgs, int slot) {
+    size_t nk = 0;
+    for (auto& m : msgs) nk += m.chunks.size();
+    if (nk == 0) return PGH_OK;  // every tensor empty
     const size_t tb = nk * sizeof(pgh::VChunk);
+    if (!c->vtab_ev) CK(c, hipEventCreateWithFlags(&c->vtab_ev, hipEventDisableTiming));
+    if (c->vtab_used) CK(c, hipEventSynchronize(c->vtab_ev));  // the previous table upload read h_vtab
     if (tb > c->vtab_cap) {
-        if (c->vtab_used) CK(c, hipEventSynchronize(c->vtab_ev));
         if (c->h_vtab) (void)hipHostFree(c->h_vtab);
         c->h_vtab = nullptr;
         size_t cap = 0;
@@ -1267,16 +1274,23 @@ int ingest_share_msg(pgh_ctx* c, ShareMsg& m, int client, int party, int slot) {
         c->vtab_cap = cap;
         c->vtab_used = false;
     }
-    if (!c->vtab_ev) CK(c, hipEventCreateWithFlags(&c->vtab_ev, hipEventDisableTiming));
-    if (c->vtab_used) CK(c, hipEventSynchronize(c->vtab_ev));
-    std::memcpy(c->h_vtab, m.chunks.data(), tb);
+    size_t at = 0;
+    for (auto& m : msgs) {
+        std::memcpy(c->h_vtab + at, m.chunks.data(), m.chunks.size() * sizeof(pgh::VChunk));
+        at += m.chunks.size();
+    }
     CK(c, hipMemcpyAsync(c->d_vtab, c->h_vtab, tb, hipMemcpyHostToDevice, c->copy));
     CK(c, hipEventRecord(c->vtab_ev, c->copy));
     c->vtab_used = true;
-    const hipError_t e = pgh::launch_varint_decode(c->d_vbytes, c->d_vtab, (int)nk,
-                                                   (int64_t*)slot_row(c, slot, party), slab_map(c), c->lo, c->hi,
-                                                   c->copy);
-    if (e != hipSuccess) return fail(c, PGH_E_HIP, "varint decode launch failed: %s", hipGetErrorString(e));
+    at = 0;
+    for (size_t s = 0; s < msgs.size(); ++s) {
+        const int n = (int)msgs[s].chunks.size();
+        const hipError_t e = pgh::launch_varint_decode(c->d_vbytes, c->d_vtab + at, n,
+                                                       (int64_t*)slot_row(c, slot, (int)s), slab_map(c), c->lo, c->hi,
+                                                       c->copy);
+        if (e != hipSuccess) return fail(c, PGH_E_HIP, "varint decode launch failed: %s", hipGetErrorString(e));
+        at += (size_t)n;
+    }
     return PGH_OK;
 }
 }  // namespace
@@ -1287,15 +1301,22 @@ int pgh_ingest_state_shares(pgh_ctx* c, int client, int n_parties, const uint8_t
     if (n_parties != c->parties)
         return fail(c, PGH_E_ARG, "client %d: %d share messages, context holds %d parties", client, n_parties,
                     c->parties);
+    // all parties are staged and validated before any is decoded: a bad message leaves the slab as it was
     std::vector<ShareMsg> msgs((size_t)n_parties);
+    size_t total = 0;
     for (int s = 0; s < n_parties; ++s) {
         if (!pbs[s] && ns[s]) return fail(c, PGH_E_ARG, "client %d party %d: NULL message", client, s);
-        RC(plan_share_msg(c, pbs[s], ns[s], client, s, &msgs[(size_t)s]));
+        total = (total + 15) & ~(size_t)15;
+        RC(plan_share_msg(c, pbs[s], ns[s], client, s, total, &msgs[(size_t)s]));
+        total += msgs[(size_t)s].bytes;
     }
     DeviceGuard g(c->device);
     int slot = 0;
     RC(claim_slot(c, client, &slot));
-    for (int s = 0; s < n_parties; ++s) RC(ingest_share_msg(c, msgs[(size_t)s], client, s, slot));
+    RC(grow_device(c, (void**)&c->d_vbytes, &c->vbytes_cap, total + 16, "share payload buffer"));
+    for (auto& m : msgs) RC(stage_share_msg(c, m));
+    for (int s = 0; s < n_parties; ++s) RC(check_share_msg(c, &msgs[(size_t)s], client, s));
+    RC(decode_share_msgs(c, msgs, slot));
     return mark_ingested(c, client, slot);
 }
 

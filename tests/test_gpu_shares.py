@@ -154,12 +154,13 @@ def test_share_state_rejects_malformed_and_leaves_slab(engine, case):
         from pygrid_amd.state_schema import build_state_fast
         msg = build_state_fast([np.zeros(P, np.float32)])
     engine.set_layout([P])
-    engine.reserve(1, 1, 1)
-    engine.ingest_state_shares(0, [build_state_i64_fast([good])])
-    with pytest.raises(PyGridError):
-        engine.ingest_state_shares(0, [msg])
-    s, _ = engine.secagg(10, 3)  # the good row is still there, untouched by the rejected message
-    assert np.array_equal(s, good)
+    engine.reserve(1, 1, 2)
+    other = np.full(P, 5, dtype=np.int64)
+    engine.ingest_state_shares(0, [build_state_i64_fast([good]), build_state_i64_fast([other])])
+    with pytest.raises(PyGridError):  # party 0's message is fine, party 1's is not: neither row changes
+        engine.ingest_state_shares(0, [build_state_i64_fast([np.zeros(P, np.int64)]), msg])
+    s, _ = engine.secagg(10, 3)
+    assert np.array_equal(s, good + other)
 
 
 def test_share_state_resnet18_scale_sampled(engine):
