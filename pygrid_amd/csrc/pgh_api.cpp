@@ -24,6 +24,7 @@
 // cycle_manager.py:247-250; fedavg = :252-296; secagg = PySyft share add + .get() + float_prec
 // (test_basic_syft_operations.py:417-424).  Errors are negative status codes plus a message (the
 // Python shim raises a PyGridError subclass, as tasks/cycle.py:33-37 expects).
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
 #include <unistd.h>
@@ -54,6 +55,30 @@ constexpr int KIND_SECAGG = 3;  // stream kind besides the three fedavg modes
 // Host copy engine: a persistent pool that splits one batch of (dst, src, n) segments evenly
 // by bytes across its threads (the caller's thread takes the first share).  Used to fill and
 // drain the pinned staging slots, where payload pieces are many and mostly small.
+// memcpy with non-temporal 16-byte stores for big copies into staging / output buffers (no
+// read-for-ownership of the destination, which is written once and then read by the DMA engine or
+// handed to the caller).  g_nt_copy = PGH_NT_COPY (default on).
+bool g_nt_copy = true;
+void copy_stream(uint8_t* dst, const uint8_t* src, size_t n) {
+    if (!g_nt_copy || n < (256u << 10)) { std::memcpy(dst, src, n); return; }
+    const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
+    std::memcpy(dst, src, head);
+    dst += head; src += head; n -= head;
+    size_t i = 0;
+    for (; i + 64 <= n; i += 64) {
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+    std::memcpy(dst + i, src + i, n - i);
+    _mm_sfence();
+}
+
 class CopyPool {
   public:
     struct Seg {
@@ -122,7 +147,7 @@ class CopyPool {
         size_t base = 0;
         for (auto& sg : segs) {
             const size_t lo = std::max(a, base), hi = std::min(b, base + sg.n);
-            if (lo < hi) std::memcpy(sg.dst + (lo - base), sg.src + (lo - base), hi - lo);
+            if (lo < hi) copy_stream(sg.dst + (lo - base), sg.src + (lo - base), hi - lo);
             base += sg.n;
             if (base >= b) break;
         }
@@ -229,6 +254,7 @@ struct pgh_ctx {
     // PGH_SHARE_FILL_MB: cap on one pinned fill of share payloads (default: the whole slot; r01z:
     // 8 / 16 / 32 / 128 MiB fills gave 29.6 / 30.8 / 34.7 / 41.6 wire GB/s at ResNet-18 x 16 x 2)
     size_t share_fill = ~(size_t)0;
+    bool nt_copy = true;  // PGH_NT_COPY: non-temporal staging copies (host side)
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
     std::vector<float> weights;
@@ -932,6 +958,8 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_SYNTH_WGS")) c->synth_wgs = std::max(0LL, std::atoll(e));
     if (const char* e = std::getenv("PGH_BLOCK_BYTES")) c->block_bytes = (size_t)std::max(0LL, std::atoll(e));
     if (const char* e = std::getenv("PGH_SHARE_FILL_MB")) c->share_fill = (size_t)std::max(1LL, std::atoll(e)) << 20;
+    if (const char* e = std::getenv("PGH_NT_COPY")) c->nt_copy = std::atoi(e) != 0;
+    g_nt_copy = c->nt_copy;
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming) == hipSuccess &&
@@ -1237,8 +1265,9 @@ int stage_share_msg(pgh_ctx* c, ShareMsg& m) {
         c->pool_copy->run_items((int)(k1 - k), fill >= (4u << 20), [&](int i) {
             const size_t q = k + (size_t)i;
             uint8_t* dst = pin + ((size_t)m.chunks[q].off - s0);
-            std::memcpy(dst, m.src[q], (size_t)m.chunks[q].n);
-            m.st[q] = pgh_state::varint_stats(dst, (size_t)m.chunks[q].n);
+            m.st[q] = c->nt_copy ? pgh_state::varint_copy_stats(dst, m.src[q], (size_t)m.chunks[q].n)
+                                 : (std::memcpy(dst, m.src[q], (size_t)m.chunks[q].n),
+                                    pgh_state::varint_stats(dst, (size_t)m.chunks[q].n));
         });
         CK(c, hipMemcpyAsync(c->d_vbytes + s0, pin, fill, hipMemcpyHostToDevice, c->copy));
         CK(c, hipEventRecord(c->pin_ev[ps], c->copy));

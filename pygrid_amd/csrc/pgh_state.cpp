@@ -252,23 +252,29 @@ int scan_i64(const uint8_t* pb, size_t n, std::vector<Span>* spans, std::string*
 }
 
 namespace {
-// bit i = bit 7 of p[i] (the varint continuation flag), for 64 bytes (SSE2 is x86-64 baseline)
-inline uint64_t msb64(const uint8_t* p) {
-    uint64_t m = 0;
-    for (int k = 0; k < 4; ++k)
-        m |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * k)))
-             << (16 * k);
-    return m;
-}
-}  // namespace
-
-VarintStats varint_stats(const uint8_t* p, size_t n) {
+// Varint statistics of 64-byte blocks (bit j of a block mask = byte j has bit 7 set, i.e. is a
+// continuation byte; SSE2 movemask, x86-64 baseline).  COPY also streams the block to dst with
+// non-temporal stores (dst 16-byte aligned): one read of the source for the staging copy and the
+// count together, and no read-for-ownership of the destination.
+template <bool COPY>
+VarintStats stats_impl(uint8_t* dst, const uint8_t* p, size_t n) {
     VarintStats st;
     int64_t run = 0;        // continuation bytes since the last terminator
     bool seen = false;      // a terminator seen yet
     size_t i = 0;
     for (; i + 64 <= n; i += 64) {
-        const uint64_t m = msb64(p + i);  // bit j: byte i + j is a continuation byte
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i + 48));
+        if (COPY) {
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+        }
+        const uint64_t m = (uint64_t)(uint32_t)_mm_movemask_epi8(a) | (uint64_t)(uint32_t)_mm_movemask_epi8(b) << 16 |
+                           (uint64_t)(uint32_t)_mm_movemask_epi8(c) << 32 | (uint64_t)(uint32_t)_mm_movemask_epi8(d) << 48;
         if (m == ~0ull) { run += 64; if (run > 9) st.overlong = true; continue; }
         const uint64_t t = ~m;
         const int lead = __builtin_ctzll(t);  // continuation bytes before the first terminator here
@@ -280,6 +286,10 @@ VarintStats varint_stats(const uint8_t* p, size_t n) {
         st.terminators += __builtin_popcountll(t);
         run = __builtin_clzll(t);
     }
+    if (COPY) {
+        if (i < n) std::memcpy(dst + i, p + i, n - i);
+        _mm_sfence();
+    }
     for (; i < n; ++i) {
         if (p[i] & 0x80) { if (++run > 9) st.overlong = true; continue; }
         if (!seen) { st.lead = run; seen = true; }
@@ -289,6 +299,17 @@ VarintStats varint_stats(const uint8_t* p, size_t n) {
     if (!seen) st.lead = run;
     st.trail = run;
     return st;
+}
+}  // namespace
+
+VarintStats varint_stats(const uint8_t* p, size_t n) { return stats_impl<false>(nullptr, p, n); }
+
+VarintStats varint_copy_stats(uint8_t* dst, const uint8_t* src, size_t n) {
+    if (reinterpret_cast<uintptr_t>(dst) & 15) {
+        std::memcpy(dst, src, n);
+        return stats_impl<false>(nullptr, dst, n);
+    }
+    return stats_impl<true>(dst, src, n);
 }
 
 int decode_f32(const uint8_t* pb, size_t n, const std::vector<int64_t>& numel, float* out, std::string* msg) {

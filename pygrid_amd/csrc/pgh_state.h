@@ -58,6 +58,9 @@ struct VarintStats {
     bool overlong = false;
 };
 VarintStats varint_stats(const uint8_t* p, size_t n);
+// The same statistics while copying [src, src + n) to dst (non-temporal stores when dst is
+// 16-byte aligned): the staging copy into the pinned ring reads each byte once.
+VarintStats varint_copy_stats(uint8_t* dst, const uint8_t* src, size_t n);
 
 // Decode every tensor into `out` (concatenated), checking per-tensor numel against `numel`.
 int decode_f32(const uint8_t* pb, size_t n, const std::vector<int64_t>& numel, float* out, std::string* msg);
