@@ -62,6 +62,12 @@ WORKLOADS = {
 }
 
 
+DATA_DEVICE = "synthetic (on-device counter-based generator, SURVEY.md 8(d); restated in oracle/oracle.py)"
+DATA_HOST = ("synthetic (seeded numpy arrays in host memory, as State protobuf bytes where the workload "
+             "takes bytes: pygrid_amd.state_schema)")
+HOST_DATA_WORKLOADS = {"c5-ingest", "mnist-state", "resnet18-state", "resnet18-report", "resnet18-secagg-state"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -296,7 +302,7 @@ def record(ctx, args, name, value, el, dt, config, roofline, extra=None):
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": ctx.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dt,
-        "data": "synthetic (on-device counter-based generator, SURVEY.md 8(d); restated in oracle/oracle.py)",
+        "data": DATA_HOST if name in HOST_DATA_WORKLOADS else DATA_DEVICE,
         "config": config,
         "pct_hbm_peak_per_gpu": round(100 * value / ctx.world / HBM_PEAK_GBS, 2),
         "cycle_close_ms": round(el / args.steps * 1e3, 4),
