@@ -255,6 +255,10 @@ struct pgh_ctx {
     // 8 / 16 / 32 / 128 MiB fills gave 29.6 / 30.8 / 34.7 / 41.6 wire GB/s at ResNet-18 x 16 x 2)
     size_t share_fill = ~(size_t)0;
     bool nt_copy = true;  // PGH_NT_COPY: non-temporal staging copies (host side)
+    // PGH_D2H_PIECE_MB: HBM -> host results move in pieces of at most this size, the DMA of piece
+    // i + 1 beside the host copy-out of piece i (default / 0: one pinned slot per piece; r01ac: 4,
+    // 8, 16 MiB pieces within the run-to-run noise of the 47 MB report-time close, 3.4-4.6 ms)
+    size_t d2h_piece = ~(size_t)0;
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
     std::vector<float> weights;
@@ -578,7 +582,7 @@ int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>
             cur_slot = c->pin_next;
             c->pin_next ^= 1;
             if (c->pin_used[cur_slot]) CK(c, hipEventSynchronize(c->pin_ev[cur_slot]));
-            cur_len = std::min(total - off, c->pin_slot);
+            cur_len = std::min({total - off, c->pin_slot, c->d2h_piece});
             CK(c, hipMemcpyAsync(c->h_pin[cur_slot], src + off, cur_len, hipMemcpyDeviceToHost, s));
             CK(c, hipEventRecord(c->pin_ev[cur_slot], s));
             c->pin_used[cur_slot] = true;
@@ -959,6 +963,10 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_BLOCK_BYTES")) c->block_bytes = (size_t)std::max(0LL, std::atoll(e));
     if (const char* e = std::getenv("PGH_SHARE_FILL_MB")) c->share_fill = (size_t)std::max(1LL, std::atoll(e)) << 20;
     if (const char* e = std::getenv("PGH_NT_COPY")) c->nt_copy = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PGH_D2H_PIECE_MB")) {
+        const long long mb = std::atoll(e);
+        c->d2h_piece = mb > 0 ? (size_t)mb << 20 : ~(size_t)0;
+    }
     g_nt_copy = c->nt_copy;
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
