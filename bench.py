@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--gather-chunks", type=int, default=8, help="N > 1: fold ranges overlapped with all-gather")
     ap.add_argument("--gather-tail", type=int, default=3,
                     help="N > 1: halve the last range this many times (shorter exposed collective)")
+    ap.add_argument("--synth", choices=["fast", "irwin-hall"], default="fast",
+                    help="c4-stream: on-device generator of the arriving diffs (fast: one hash per 4 params)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -446,6 +448,7 @@ def run_c4(ctx, args, eng, N, pg, P):
     R = args.ring or 1000
     chunk = R // 2
     eng.reserve(R)
+    eng.set_synth_kind(1 if args.synth == "fast" else 0)
     ckpt = torch.empty(pg, dtype=torch.float32, device="cuda")
     out = torch.empty_like(ckpt)
     sp = torch.cuda.current_stream().cuda_stream
@@ -464,8 +467,8 @@ def run_c4(ctx, args, eng, N, pg, P):
     value = diff_bytes * ctx.world * args.steps / el / 1e9
     kern_gbs = ctx.sum_over_ranks(4 * N * pg * args.steps / (st["kernel_ms_total"] / 1e3) / 1e9)
     cfg = {"workload": f"c4-stream: P_shard={pg} params/GPU x {N} clients fp32 (SURVEY 8(d) config 4 shard), "
-                       f"{R}-slot HBM ring, {chunk}-client chunks generated on-device",
-           "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R,
+                       f"{R}-slot HBM ring, {chunk}-client chunks generated on-device ({args.synth} generator)",
+           "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R, "generator": args.synth,
            "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
            "kernel_variant": eng.effective_variant()}
     extra = {"fold_kernel_client_diff_GBps_aggregated": round(kern_gbs, 1),

@@ -115,6 +115,11 @@ int pgh_ingest_state_shares(pgh_ctx* ctx, int client, int n_parties, const uint8
 /* Fill slab rows [0, n_clients) with the deterministic synthetic diffs (or shares) of
  * SURVEY.md 8(d) for this shard, generated on the GPU (oracle/oracle.py restates them). */
 int pgh_synth_fill(pgh_ctx* ctx, uint64_t seed, int n_clients);
+/* Generator of the synthetic fp32 diffs for later pgh_synth_fill / pgh_synth_ingest calls:
+ * 0 = one splitmix64 word per param, Irwin-Hall(4 x u16) (default); 1 = one word
+ * per 4 params, a u16 each, uniform (config 4's on-device data source: write-bound instead of
+ * integer-bound).  Both restated bit for bit by oracle/oracle.py. */
+int pgh_set_synth_kind(pgh_ctx* ctx, int kind);
 /* Ingest synthetic clients [client0, client0 + n) generated on the GPU (either use). */
 int pgh_synth_ingest(pgh_ctx* ctx, uint64_t seed, int client0, int n);
 /* Per-client weights for PGH_WEIGHTED_MEAN (n == clients ingested at reduction time). */

@@ -30,6 +30,7 @@ def lib():
         L.or_secagg.argtypes = [vp, i, i, i64, i64, f, vp, vp]
         L.or_synth_f32.argtypes = [u64, u64, u64, i64, i64, f, vp]
         L.or_synth_u64.argtypes = [u64, u64, u64, i64, i64, vp]
+        L.or_synth_f32_fast.argtypes = [u64, u64, u64, i64, i64, f, vp]
         L.or_weight_total.argtypes = [vp, i]
         L.or_weight_total.restype = f
         L.or_row_key.argtypes = [u64, u64, u64]
@@ -75,6 +76,12 @@ def secagg(shares: np.ndarray, p: int, divisor: float = 1000.0):
 def synth_f32(seed: int, stream: int, row: int, idx0: int, n: int, scale: float) -> np.ndarray:
     out = np.empty(n, np.float32)
     lib().or_synth_f32(seed, stream, row, idx0, n, C.c_float(scale), _p(out))
+    return out
+
+
+def synth_f32_fast(seed: int, stream: int, row: int, idx0: int, n: int, scale: float) -> np.ndarray:
+    out = np.empty(n, np.float32)
+    lib().or_synth_f32_fast(seed, stream, row, idx0, n, C.c_float(scale), _p(out))
     return out
 
 

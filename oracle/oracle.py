@@ -361,6 +361,17 @@ def synth_diff(seed, client, idx):
     return bits_to_f32(synth_bits(seed, STREAM_DIFF, client, idx), DIFF_SCALE)
 
 
+def synth_diff_fast(seed, client, idx):
+    """Generator kind 1 (``pgh_set_synth_kind(ctx, 1)``, config 4's data source): param g takes
+    u16 number g & 3 of splitmix64(row_key + (g >> 2)), centred, times 2 * DIFF_SCALE."""
+    g = np.asarray(idx, dtype=U64)
+    base = U64(row_key(seed, STREAM_DIFF, client))
+    with np.errstate(over="ignore"):
+        h = splitmix64(base + (g >> U64(2)))
+    u = (h >> (U64(16) * (g & U64(3)))) & U64(0xFFFF)
+    return ((u.astype(I64) - I64(32768)).astype(F32) * (F32(2) * DIFF_SCALE)).astype(F32)
+
+
 def synth_ckpt(seed, idx):
     return bits_to_f32(synth_bits(seed, STREAM_CKPT, 0, idx), CKPT_SCALE)
 

@@ -68,6 +68,7 @@ SIGNATURES = {
     "pgh_reset": (_i, [_vp]),
     "pgh_ingest_raw": (_i, [_vp, _i, _vp, _sz, _i]),
     "pgh_ingest_state": (_i, [_vp, _i, C.c_char_p, _sz]),
+    "pgh_set_synth_kind": (_i, [_vp, _i]),
     "pgh_ingest_state_shares": (_i, [_vp, _i, _i, C.POINTER(C.c_char_p), C.POINTER(_sz)]),
     "pgh_synth_fill": (_i, [_vp, _u64, _i]),
     "pgh_synth_ingest": (_i, [_vp, _u64, _i, _i]),

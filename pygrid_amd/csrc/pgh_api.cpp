@@ -215,6 +215,7 @@ struct pgh_ctx {
     int bshift = 62;
     int64_t bmask = 0;
     size_t block_bytes = 256u << 10;  // PGH_BLOCK_BYTES; 0 = one block (plain row-major rows)
+    int synth_kind = 0;        // pgh_set_synth_kind: generator of synthetic diffs (0 Irwin-Hall, 1 fast)
     int64_t synth_wgs = 8192;  // PGH_SYNTH_WGS: STREAM synthetic fill grid cap (0 = a grid row per row; r01t)
 
     int slots = 0, dtype = PGH_F32, parties = 1;
@@ -1383,7 +1384,7 @@ int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
         if (c->dtype == PGH_F32)
             e = pgh::launch_synth_f32((float*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->pg, seed,
                                       pgh::STREAM_DIFF, client, c->lo, pgh::DIFF_SCALE, c->copy,
-                                      c->streaming ? c->synth_wgs : 0);
+                                      c->streaming ? c->synth_wgs : 0, c->synth_kind);
         else
             e = pgh::launch_synth_shares((int64_t*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->parties,
                                          c->pg, seed, client, c->lo, 1000.0f, c->copy);
@@ -1395,6 +1396,13 @@ int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
         if (c->streaming) RC(maybe_fold(c, false));
         k += run;
     }
+    return PGH_OK;
+}
+
+int pgh_set_synth_kind(pgh_ctx* c, int kind) {
+    if (!c) return PGH_E_ARG;
+    if (kind != 0 && kind != 1) return fail(c, PGH_E_ARG, "synthetic generator kind %d is not 0 or 1", kind);
+    c->synth_kind = kind;
     return PGH_OK;
 }
 

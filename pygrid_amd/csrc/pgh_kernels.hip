@@ -391,6 +391,11 @@ __global__ __launch_bounds__(BLOCK) void k_secagg_decode(const int64_t* sum, flo
         dec[i] = (float)sum[i] / divisor;
 }
 
+// KIND 0: one splitmix64 word per param -> Irwin-Hall(4 x u16).  KIND 1 ("fast", config 4's
+// on-device data source): one word per 4 consecutive params (global index g >> 2), param g takes
+// u16 number g & 3 of it, centred, times 2 * scale (same sigma ~ 1e-2): a quarter of the integer
+// work, so the fill is bound by its HBM writes instead of the 64-bit multiplies (r01af).
+template <int KIND>
 __global__ __launch_bounds__(BLOCK) void k_synth_f32(float* out, SlabMap m, int64_t ncols, int n_rows, int64_t p,
                                                      uint64_t seed, uint64_t stream_id, int64_t row0, int64_t idx0,
                                                      float scale) {
@@ -399,13 +404,32 @@ __global__ __launch_bounds__(BLOCK) void k_synth_f32(float* out, SlabMap m, int6
         float* row = out + (size_t)r * m.ld;
         for (int64_t q = (int64_t)blockIdx.x * BLOCK + threadIdx.x; q < ncols / 4; q += (int64_t)gridDim.x * BLOCK) {
             f32x4 v;
-            const uint64_t k0 = key + (uint64_t)(idx0 + 4 * q);
-            if (4 * q + 4 <= p) {  // branch-free: four independent hash chains interleave
+            if constexpr (KIND == 0) {
+                const uint64_t k0 = key + (uint64_t)(idx0 + 4 * q);
+                if (4 * q + 4 <= p) {  // branch-free: four independent hash chains interleave
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = bits_to_f32(sm64(k0 + (uint64_t)e), scale);
+                    for (int e = 0; e < 4; ++e) v[e] = bits_to_f32(sm64(k0 + (uint64_t)e), scale);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        v[e] = (4 * q + e < p) ? bits_to_f32(sm64(k0 + (uint64_t)e), scale) : 0.f;
+                }
             } else {
+                const float s2 = 2.0f * scale;  // exact
+                const int64_t g0 = idx0 + 4 * q;
+                if ((g0 & 3) == 0) {  // the four params share one word
+                    const uint64_t h = sm64(key + (uint64_t)(g0 >> 2));
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = (4 * q + e < p) ? bits_to_f32(sm64(k0 + (uint64_t)e), scale) : 0.f;
+                    for (int e = 0; e < 4; ++e)
+                        v[e] = (4 * q + e < p) ? (float)((int32_t)((h >> (16 * e)) & 0xFFFF) - 32768) * s2 : 0.f;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int64_t g = g0 + e;
+                        const uint64_t h = sm64(key + (uint64_t)(g >> 2));
+                        v[e] = (4 * q + e < p) ? (float)((int32_t)((h >> (16 * (g & 3))) & 0xFFFF) - 32768) * s2 : 0.f;
+                    }
+                }
             }
             *reinterpret_cast<f32x4*>(row + m.at(4 * q)) = v;  // 4 params never straddle a block
         }
@@ -693,8 +717,9 @@ hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s) {
 
 hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_rows, int64_t p, uint64_t seed,
                             uint64_t stream_id, int64_t row0, int64_t idx0, float scale, hipStream_t s,
-                            int64_t max_wgs) {
+                            int64_t max_wgs, int kind) {
     if (!out || n_rows < 0 || n_rows > 65535 || ncols < p || (ncols & 3) || m.off != 0 || !valid_map(m, 0) ||
+        (kind != 0 && kind != 1) ||
         (m.bshift == 62 && ncols > m.ld) || (reinterpret_cast<uintptr_t>(out) & 15))
         return hipErrorInvalidValue;
     if (n_rows == 0 || ncols == 0) return hipSuccess;
@@ -705,8 +730,12 @@ hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_r
         if (gx > max_wgs) gx = max_wgs;
         gy = std::max<int64_t>(1, std::min<int64_t>(n_rows, max_wgs / gx));
     }
-    k_synth_f32<<<dim3((unsigned)gx, (unsigned)gy), BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id, row0,
-                                                                  idx0, scale);
+    if (kind == 1)
+        k_synth_f32<1><<<dim3((unsigned)gx, (unsigned)gy), BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id,
+                                                                         row0, idx0, scale);
+    else
+        k_synth_f32<0><<<dim3((unsigned)gx, (unsigned)gy), BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id,
+                                                                         row0, idx0, scale);
     return hipGetLastError();
 }
 

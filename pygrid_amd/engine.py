@@ -173,6 +173,10 @@ class Engine:
         self._check(self._lib.pgh_ingest_state_shares(self._h, int(client), n, ptrs, lens),
                     f"ingest_state_shares client {client}")
 
+    def set_synth_kind(self, kind: int):
+        """0: Irwin-Hall(4 x u16) per param (default); 1: fast, one hash word per 4 params."""
+        self._check(self._lib.pgh_set_synth_kind(self._h, int(kind)), "set_synth_kind")
+
     def synth_fill(self, seed: int, n_clients: int):
         self._check(self._lib.pgh_synth_fill(self._h, C.c_uint64(seed), int(n_clients)), "synth_fill")
 

@@ -209,8 +209,8 @@ def test_blocked_ring_small_staging(mode):
     assert same(got, coracle.fedavg(mode, d, c))
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_config4_shard_full_size_sampled(engine, mode):
+@pytest.mark.parametrize("mode,kind", [(0, 0), (1, 0), (0, 1)])
+def test_config4_shard_full_size_sampled(engine, mode, kind):
     """BASELINE config 4, one GPU's shard at full size: 12.5 M params x 10,000 clients (500 GB of
     diffs) through a 1,000-slot ring, generated on the GPU in 500-client chunks exactly like
     `bench.py --workload c4-stream`; bit-exact on sampled params (block edges included) against
@@ -220,18 +220,23 @@ def test_config4_shard_full_size_sampled(engine, mode):
     P, N, R, chunk, seed = 12_500_000, 10_000, 1000, 500, 4242
     engine.set_layout([P])
     engine.reserve(R)
-    engine.stream_begin(mode, chunk)
-    for c0 in range(0, N, chunk):
-        engine.synth_ingest(seed, c0, min(chunk, N - c0))
-    ck = torch.empty(P, dtype=torch.float32, device="cuda")
-    out = torch.empty_like(ck)
-    engine.synth_ckpt_device(seed, ck.data_ptr())
-    engine.stream_finish_device(ck.data_ptr(), out.data_ptr())
-    torch.cuda.synchronize()
+    engine.set_synth_kind(kind)  # 1: the fast generator bench.py's c4-stream uses
+    try:
+        engine.stream_begin(mode, chunk)
+        for c0 in range(0, N, chunk):
+            engine.synth_ingest(seed, c0, min(chunk, N - c0))
+        ck = torch.empty(P, dtype=torch.float32, device="cuda")
+        out = torch.empty_like(ck)
+        engine.synth_ckpt_device(seed, ck.data_ptr())
+        engine.stream_finish_device(ck.data_ptr(), out.data_ptr())
+        torch.cuda.synchronize()
+    finally:
+        engine.set_synth_kind(0)
     edges = np.array([k * 65536 + e for k in (1, 95, 190) for e in (-1, 0)])
     idx = np.unique(np.concatenate([[0, 1], np.random.default_rng(mode).integers(0, P, 300), edges, [P - 1]]))
     u = idx.astype(np.uint64)
-    d = np.stack([O.synth_diff(seed, k, u) for k in range(N)])
+    gen = O.synth_diff_fast if kind else O.synth_diff
+    d = np.stack([gen(seed, k, u) for k in range(N)])
     want = coracle.fedavg(mode, d, O.synth_ckpt(seed, u))
     assert same(out.cpu().numpy()[idx], want)
     engine.set_layout([1])  # release the ring
@@ -268,3 +273,30 @@ def test_config5_shard_full_size_pinned_sampled(engine):
         for b in bufs:
             b.free()
         engine.set_layout([1])
+
+
+@pytest.mark.parametrize("lo", [0, 70_001])
+def test_fast_generator_matches_oracle(engine, lo):
+    """Generator kind 1 on a shard starting anywhere (lo % 4 != 0: per-param words), resident."""
+    import torch
+
+    P, N, seed = 300_007, 40, 9
+    engine.set_layout([P])
+    engine.set_shard(lo, P)
+    pg = P - lo
+    try:
+        engine.reserve(N)
+        engine.set_synth_kind(1)
+        engine.synth_fill(seed, N)
+        ck = torch.empty(pg, dtype=torch.float32, device="cuda")
+        out = torch.empty_like(ck)
+        engine.synth_ckpt_device(seed, ck.data_ptr())
+        engine.fedavg_device(0, ck.data_ptr(), out.data_ptr())
+        torch.cuda.synchronize()
+    finally:
+        engine.set_synth_kind(0)
+        engine.set_layout([P])
+    u = np.arange(lo, P, dtype=np.uint64)
+    d = np.stack([O.synth_diff_fast(seed, k, u) for k in range(N)])
+    want = coracle.fedavg(0, d, O.synth_ckpt(seed, u))
+    assert same(out.cpu().numpy(), want)

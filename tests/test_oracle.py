@@ -150,6 +150,15 @@ def test_generator_c_matches_numpy():
     assert np.array_equal(u, O.synth_bits(77, O.STREAM_SHARE, 5, np.arange(10, 110, dtype=np.uint64)))
 
 
+@pytest.mark.parametrize("idx0", [0, 64, 70_001])
+def test_fast_generator_c_matches_numpy(idx0):
+    n = 50_003
+    a = coracle.synth_f32_fast(11, O.STREAM_DIFF, 5, idx0, n, float(O.DIFF_SCALE))
+    b = O.synth_diff_fast(11, 5, np.arange(idx0, idx0 + n, dtype=np.uint64))
+    assert np.array_equal(bits(a), bits(b))
+    assert abs(float(b.mean())) < 2e-4 and 0.0095 < float(b.std()) < 0.0105
+
+
 def test_generator_statistics():
     x = O.synth_diff(1234, 0, np.arange(200_000, dtype=np.uint64))
     assert abs(float(x.mean())) < 1e-4 and 0.0095 < float(x.std()) < 0.0105
