@@ -62,17 +62,24 @@ class PinnedBuffer:
 
 class _Serialized:
     """The library with every call made under one lock: a context is single-owner, and ctypes
-    releases the GIL, so two Python threads sharing an Engine would otherwise enter it together."""
+    releases the GIL, so two Python threads sharing an Engine would otherwise enter it together.
+    A failing call's message (``pgh_last_error``, one per context) is read under the same lock
+    and kept per thread, so another thread's call cannot overwrite it before ``_check`` sees it."""
 
     def __init__(self, lib, lock):
         self._l, self._m = lib, lock
+        self.errors = threading.local()
 
     def __getattr__(self, name):
         fn = getattr(self._l, name)
 
         def call(*args):
             with self._m:
-                return fn(*args)
+                rc = fn(*args)
+                if isinstance(rc, int) and rc < 0:
+                    ctx = args[0] if args and isinstance(args[0], C.c_void_p) else None
+                    self.errors.msg = self._l.pgh_last_error(ctx).decode(errors="replace")
+                return rc
         return call
 
 
@@ -82,7 +89,7 @@ class Engine:
         h = C.c_void_p()
         rc = self._lib.pgh_create(int(device), int(pinned_bytes), C.byref(h))
         if rc != 0:
-            msg = self._lib.pgh_last_error(None).decode()
+            msg = getattr(self._lib.errors, "msg", "")
             raise EngineUnavailableError(f"pgh_create(device={device}) failed: {msg}")
         self._h = h
         self.device = int(device)
@@ -100,7 +107,7 @@ class Engine:
     # ---- plumbing ----------------------------------------------------------------------------
     def _check(self, rc: int, what: str):
         if rc != 0:
-            msg = self._lib.pgh_last_error(self._h).decode()
+            msg = getattr(self._lib.errors, "msg", "")
             cls = StateParseError if rc == -5 else AggregationError
             raise cls(f"{what}: {_lib.STATUS_NAMES.get(rc, rc)}: {msg}", status=rc)
 

@@ -287,3 +287,34 @@ def test_share_scan_rejects_float_payload_and_f32_scan_rejects_shares():
         state.scan_shares(build_state([np.ones(3, F)]))
     with pytest.raises(StateParseError):
         state.scan(build_state_i64_fast([np.arange(3, dtype=np.int64)]))
+
+
+# ---- Engine plumbing: a failing call's message survives another thread's call ---------------------
+def test_serialized_keeps_error_message_per_thread():
+    import ctypes as C
+    import threading
+
+    from pygrid_amd.engine import _Serialized
+
+    class FakeLib:
+        """Stands in for libpygrid_hip: one error string per context, as pgh_last_error has."""
+        err = b""
+
+        def pgh_fail(self, ctx, tag):
+            FakeLib.err = tag
+            return -3
+
+        def pgh_ok(self, ctx):
+            return 0
+
+        def pgh_last_error(self, ctx):
+            return FakeLib.err
+
+    lib = _Serialized(FakeLib(), threading.RLock())
+    h = C.c_void_p(1)
+    assert lib.pgh_fail(h, b"first") == -3
+    t = threading.Thread(target=lambda: lib.pgh_fail(h, b"other thread"))
+    t.start()
+    t.join()
+    assert lib.pgh_ok(h) == 0
+    assert lib.errors.msg == "first"
