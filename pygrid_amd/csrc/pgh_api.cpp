@@ -260,6 +260,7 @@ struct pgh_ctx {
     // i + 1 beside the host copy-out of piece i (default / 0: one pinned slot per piece; r01ac: 4,
     // 8, 16 MiB pieces within the run-to-run noise of the 47 MB report-time close, 3.4-4.6 ms)
     size_t d2h_piece = ~(size_t)0;
+    bool prefault = true;  // PGH_PREFAULT: pre-fault big fresh checkpoint outputs in parallel (patch)
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
     std::vector<float> weights;
@@ -564,6 +565,22 @@ void prefault_small(uint8_t* p, size_t n) {
     static const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
     const uintptr_t a = (uintptr_t)p & ~(page - 1), b = ((uintptr_t)p + n + page - 1) & ~(page - 1);
     (void)madvise((void*)a, b - a, MADV_POPULATE_WRITE);
+}
+
+// The same for a big fresh destination, split over the copy pool's threads: run while the fold
+// and the first D2H are still in flight, so the copy-out afterwards writes to resident pages
+// instead of taking a page fault per 4 KiB (PGH_PREFAULT=0 turns it off).
+void prefault_parallel(uint8_t* p, size_t n, CopyPool& pool) {
+    if (!p || n == 0) return;
+    if (n < (4u << 20)) { prefault_small(p, n); return; }
+    static const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
+    const uintptr_t a = (uintptr_t)p & ~(page - 1), b = ((uintptr_t)p + n + page - 1) & ~(page - 1);
+    const int k = pool.threads();
+    const uintptr_t per = ((b - a) / k + page - 1) & ~(page - 1);
+    pool.run_items(k, true, [&](int i) {
+        const uintptr_t lo = a + per * (uintptr_t)i, hi = std::min(b, lo + per);
+        if (lo < hi) (void)madvise((void*)lo, hi - lo, MADV_POPULATE_WRITE);
+    });
 }
 
 // HBM bytes at `src` (after the work already on stream `s`) -> host pieces, through the pinned
@@ -964,6 +981,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_BLOCK_BYTES")) c->block_bytes = (size_t)std::max(0LL, std::atoll(e));
     if (const char* e = std::getenv("PGH_SHARE_FILL_MB")) c->share_fill = (size_t)std::max(1LL, std::atoll(e)) << 20;
     if (const char* e = std::getenv("PGH_NT_COPY")) c->nt_copy = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PGH_PREFAULT")) c->prefault = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_D2H_PIECE_MB")) {
         const long long mb = std::atoll(e);
         c->d2h_piece = mb > 0 ? (size_t)mb << 20 : ~(size_t)0;
@@ -1582,7 +1600,10 @@ int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out
     }
     // the framing copy (and the pre-fault of a small fresh output) runs while the first slot's DMA flies
     RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, pieces, c->stream, [&] {
-        if (out != tmpl) prefault_small(out, n);
+        if (out != tmpl) {
+            if (c->prefault) prefault_parallel(out, n, *c->pool_copy);
+            else prefault_small(out, n);
+        }
         if (!gaps.empty()) c->pool_copy->run(gaps);
     }));
     return collect_timings(c);
