@@ -257,9 +257,10 @@ struct pgh_ctx {
     size_t share_fill = ~(size_t)0;
     bool nt_copy = true;  // PGH_NT_COPY: non-temporal staging copies (host side)
     // PGH_D2H_PIECE_MB: HBM -> host results move in pieces of at most this size, the DMA of piece
-    // i + 1 beside the host copy-out of piece i (default / 0: one pinned slot per piece; r01ac: 4,
-    // 8, 16 MiB pieces within the run-to-run noise of the 47 MB report-time close, 3.4-4.6 ms)
-    size_t d2h_piece = ~(size_t)0;
+    // i + 1 beside the host copy-out of piece i (0: one pinned slot per piece).  r01ac: 4, 8, 16 MiB
+    // within the noise of the 47 MB report-time close while the copy-out took page faults; with
+    // the parallel pre-fault (r01ak) 8 MiB pieces close in 2.3-2.4 ms vs 2.6-2.7 for one piece.
+    size_t d2h_piece = 8u << 20;
     bool prefault = true;  // PGH_PREFAULT: pre-fault big fresh checkpoint outputs in parallel (patch)
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
