@@ -1001,13 +1001,14 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
             return fail(nullptr, PGH_E_OOM, "pinned host allocation of %zu bytes failed", c->pin_slot);
         }
     // Warm-up (PGH_WARMUP=0 skips it): the first kernel launch loads the code object and the first
-    // copies load the runtime's blit kernels -- ~11 ms that would otherwise land on the node's
-    // first cycle close (profiles/r01am).  One tiny launch plus an H2D and a D2H on both streams.
+    // copies set up the runtime's copy engines (the first ~1 MB H2D from the pinned ring took 8.3 ms
+    // of host time, r01ao) -- ~11 ms that would otherwise land on the node's first cycle close
+    // (profiles/r01am).  One small launch plus an H2D and a D2H of up to 2 MiB on the two streams.
     const char* wu = std::getenv("PGH_WARMUP");
     if (!wu || std::atoi(wu) != 0) {
-        constexpr int64_t n = 512;  // 4 KiB of int64: fits the smallest pinned slot
+        const int64_t n = (int64_t)std::min(c->pin_slot, (size_t)2 << 20) / 8;  // int64 values
         void* d = nullptr;
-        ok = hipMalloc(&d, 16 * n) == hipSuccess;
+        ok = hipMalloc(&d, 12 * n) == hipSuccess;
         if (ok) {
             int64_t* d_sum = (int64_t*)d;
             float* d_dec = (float*)((uint8_t*)d + 8 * n);
@@ -1015,7 +1016,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
             ok = hipMemcpyAsync(d_sum, c->h_pin[0], 8 * n, hipMemcpyHostToDevice, c->copy) == hipSuccess &&
                  hipStreamSynchronize(c->copy) == hipSuccess &&
                  pgh::launch_secagg_decode(d_sum, d_dec, n, 1.0f, c->stream) == hipSuccess &&
-                 hipMemcpyAsync(c->h_pin[1], d_dec, 4 * n, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+                 hipMemcpyAsync(c->h_pin[1], d_sum, 8 * n, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
                  hipStreamSynchronize(c->stream) == hipSuccess;
             (void)hipFree(d);
         }
