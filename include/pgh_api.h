@@ -73,7 +73,9 @@ typedef struct {
 int pgh_abi_version(void);
 int pgh_device_count(int* n);
 /* Bind a context to GPU `device`, with a pinned host staging ring of `pinned_bytes` total
- * (0 = default 256 MiB, split into 2 slots). */
+ * (0 = default 256 MiB, split into 2 slots).  Also warms the device up (one small kernel launch
+ * and a host -> HBM -> host copy; PGH_WARMUP=0 skips it) so the node's first cycle close does not
+ * pay for the code-object load and the copy engines' first use. */
 int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out);
 void pgh_destroy(pgh_ctx* ctx);
 const char* pgh_last_error(const pgh_ctx* ctx);   /* ctx may be NULL (creation errors) */
