@@ -86,10 +86,73 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="resident config-2 lines: skip the bytes -> bytes end-to-end close measured beside them")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="form the world (gloo, no GPU), print the world size on rank 0 and exit")
     return ap.parse_args()
 
 
-def cpu_baseline(kind: str, P: int, seed: int, budget_s: float, n: int = 32, all_cores: int = 16):
+def usable_cores() -> tuple:
+    """CPUs this process may run on: the affinity mask, capped by a cgroup v2/v1 CPU quota (a GPU
+    lease's share of a bigger machine shows in the quota, not in os.cpu_count()).  Returns (cores,
+    how they were determined)."""
+    n = len(os.sched_getaffinity(0))
+    how = "sched_getaffinity"
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+            per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None and int(quota) < n:
+        n, how = max(1, int(quota)), "cgroup cpu quota"
+    return n, how
+
+
+def spawn_ranks(args) -> int:
+    """``--gpus N`` (N > 1) started without a launcher: start N rank processes of this script with
+    the environment torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE,
+    MASTER_ADDR=127.0.0.1, a free MASTER_PORT) and return the worst exit status.  The parent imports
+    neither torch nor the engine, so it never touches a GPU; if one rank fails the others are
+    stopped (their own PIDs) instead of waiting in a collective forever."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0:
+                rc = rc or r
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def cpu_baseline(kind: str, P: int, seed: int, budget_s: float, n: int = 32, all_cores: int = 0):
     """The reference's path as the node runs it, in torch on CPU tensors at th.set_num_threads(1)
     (the node's setting, main/__init__.py:8), on a bounded sample: the same P-param shard, `n`
     synthetic clients, repeated until `budget_s` of CPU work.
@@ -97,10 +160,14 @@ def cpu_baseline(kind: str, P: int, seed: int, budget_s: float, n: int = 32, all
       iterative  cycle_manager.py:266-269 + the plan     (oracle.fedavg_iterative_torch)
       secagg     syft share adds + fix-prec decode       (oracle.secagg_sum_torch), 2 parties
       weighted   no reference counterpart: the numpy oracle (oracle.fedavg_weighted)
-    Also reported: the same at `all_cores` threads (the GPU box's CPU share) and the numpy
-    restatement at 1 thread."""
+    Also reported: the same at `all_cores` threads (default: usable_cores(), the GPU box's CPU
+    share) and the numpy restatement at 1 thread."""
     import numpy as np
     import torch
+
+    cores_how = "given"
+    if all_cores <= 0:
+        all_cores, cores_how = usable_cores()
 
     from oracle import coracle
     from oracle import oracle as O
@@ -159,7 +226,7 @@ def cpu_baseline(kind: str, P: int, seed: int, budget_s: float, n: int = 32, all
             "sample": f"{what}, {f'torch {torch.__version__} CPU tensors' if ref else 'numpy'}, P={P}, {n} clients, "
                       f"{reps} passes in {el:.1f}s, 1 thread (the node's th.set_num_threads(1))",
             "cycle_close_ms_per_1000_clients": close_1000(gbs),
-            "all_cores": ({"value": round(gbs_all, 3), "cores": all_cores,
+            "all_cores": ({"value": round(gbs_all, 3), "cores": all_cores, "cores_from": cores_how,
                            "cycle_close_ms_per_1000_clients": close_1000(gbs_all)} if gbs_all else None),
             "numpy_restatement_1_thread": round(gbs_np, 3), "cpu_model": cpu_model()}
 
@@ -247,18 +314,26 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world != args.gpus and self.rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {self.world}", file=sys.stderr)
+        if self.world != args.gpus:
+            # main() spawns the ranks itself when no launcher did; a launcher with another world
+            # size would measure a different configuration than the one named
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher formed WORLD_SIZE {self.world}")
         # PGH_BENCH_DEVICE / PGH_DIST_BACKEND only exist to rehearse the N > 1 path with several
         # ranks on one GPU over gloo; the driver's runs use one GPU per rank and RCCL ("nccl").
+        self.dry = args.dry_run
         self.device = int(os.environ.get("PGH_BENCH_DEVICE", self.local))
-        self.backend = os.environ.get("PGH_DIST_BACKEND", "nccl")
-        torch.cuda.set_device(self.device)
+        self.backend = "gloo" if self.dry else os.environ.get("PGH_DIST_BACKEND", "nccl")
+        self.tdev = "cpu" if self.dry else "cuda"
+        if not self.dry:
+            torch.cuda.set_device(self.device)
         if self.world > 1:
             if self.backend == "nccl":
                 dist.init_process_group("nccl", device_id=torch.device("cuda", self.device))
             else:
                 dist.init_process_group(self.backend)
+            formed = int(self.sum_over_ranks(1.0))
+            if formed != args.gpus:
+                raise SystemExit(f"bench.py: formed a world of {formed} ranks, --gpus {args.gpus}")
 
     def barrier(self):
         if self.world > 1:
@@ -267,14 +342,14 @@ class Ctx:
     def max_over_ranks(self, x: float) -> float:
         if self.world == 1:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.tdev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
     def sum_over_ranks(self, x: float) -> float:
         if self.world == 1:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.tdev)
         self.dist.all_reduce(t)
         return float(t.item())
 
@@ -299,7 +374,10 @@ def timed(ctx, step, steps, warmup, eng):
     return ctx.max_over_ranks(el), eng.stats()
 
 
-def record(ctx, args, name, value, el, dt, config, roofline, extra=None):
+def record(ctx, args, name, value, el, dt, config, roofline, extra=None, step_is="kernel"):
+    """One JSON line.  `step_is` names what one timed step is: "kernel" (the resident lines: the
+    fold of HBM-resident diffs, plus the collective at N > 1) -> `kernel_ms`; "close" (bytes in ->
+    bytes out: the whole _average_plan_diffs slice) -> `cycle_close_ms`."""
     rec = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": ctx.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
@@ -307,7 +385,7 @@ def record(ctx, args, name, value, el, dt, config, roofline, extra=None):
         "data": DATA_HOST if name in HOST_DATA_WORKLOADS else DATA_DEVICE,
         "config": config,
         "pct_hbm_peak_per_gpu": round(100 * value / ctx.world / HBM_PEAK_GBS, 2),
-        "cycle_close_ms": round(el / args.steps * 1e3, 4),
+        ("kernel_ms" if step_is == "kernel" else "cycle_close_ms"): round(el / args.steps * 1e3, 4),
         "roofline": roofline, "cpu_baseline": None,
     }
     if extra:
@@ -562,7 +640,7 @@ def run_mnist_state(ctx, args, eng):
     rec = record(ctx, args, "mnist-state", value, el, "f32", cfg,
                  roofline_of(st, "mnist-state", eng.effective_variant(), "k_fedavg"),
                  {"new_checkpoint_bytes": len(new),
-                  "note": "latency-bound: host protobuf scan, 3 H2D copies and a 0.3M-param kernel"})
+                  "note": "latency-bound: host protobuf scan, 3 H2D copies and a 0.3M-param kernel"}, step_is="close")
     if not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline_state(ck_pb, d_pb, P, 3, 4.0)
     return rec
@@ -602,7 +680,7 @@ def run_resnet18_state(ctx, args, eng, N):
              "new_checkpoint_bytes": len(new),
              "note": "PCIe-inclusive cycle close from host bytes (never `value` for the resident configs)"}
     rec = record(ctx, args, "resnet18-state", value, el, "f32", cfg,
-                 roofline_of(st, "resnet18-state", eng.effective_variant(), "k_fedavg"), extra)
+                 roofline_of(st, "resnet18-state", eng.effective_variant(), "k_fedavg"), extra, step_is="close")
     if not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline_state(ck_pb, distinct[:3], P, N, 0.0)
     return rec
@@ -653,7 +731,7 @@ def run_resnet18_secagg_state(ctx, args, eng, N, S):
              "note": "PCIe-inclusive: value counts the decoded int64 share bytes (8 B per value) per second; "
                      "wire_GBps the varint bytes received"}
     rec = record(ctx, args, "resnet18-secagg-state", value, el, "int64", cfg,
-                 roofline_of(st, "resnet18-secagg-state", cfg["kernel_variant"], "k_secagg"), extra)
+                 roofline_of(st, "resnet18-secagg-state", cfg["kernel_variant"], "k_secagg"), extra, step_is="close")
     if not args.no_cpu_baseline:
         from oracle import oracle as O  # cpu_baseline leg only
         import torch
@@ -727,7 +805,7 @@ def run_resnet18_report(ctx, args, eng, N):
              "note": "PCIe-inclusive whole cycle (reports + close); compare close_ms_after_last_report with "
                      "resnet18-state's cycle_close_ms (all diffs folded at close)"}
     rec = record(ctx, args, "resnet18-report", value, el, "f32", cfg,
-                 roofline_of(st, "resnet18-report", eng.effective_variant(), "k_fedavg"), extra)
+                 roofline_of(st, "resnet18-report", eng.effective_variant(), "k_fedavg"), extra, step_is="close")
     if not args.no_cpu_baseline:  # the reference decodes and folds every diff at close
         rec["cpu_baseline"] = cpu_baseline_state(ck_pb, distinct[:3], P, N, 0.0)
     return rec
@@ -735,7 +813,14 @@ def run_resnet18_report(ctx, args, eng, N):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))  # no launcher: form the N-rank world here (no GPU touched yet)
     ctx = Ctx(args)
+    if args.dry_run:
+        if ctx.rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": ctx.world, "backend": ctx.backend}), flush=True)
+        ctx.close()
+        return
     from pygrid_amd import Engine
     from pygrid_amd.sharding import shard_bounds
 

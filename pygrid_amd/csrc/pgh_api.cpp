@@ -223,6 +223,9 @@ struct pgh_ctx {
     size_t slab_bytes = 0;
     float* d_ckpt = nullptr;
     float* d_out = nullptr;
+    // d_ckpt holds a checkpoint (uploaded, or the output of a resident fold); a fresh slab's is
+    // uninitialised memory, which a resident fold / download / patch must refuse to read
+    bool ckpt_valid = false;
     float* d_acc = nullptr;
     uint64_t* d_uacc = nullptr;
     int64_t* d_sum = nullptr;
@@ -262,6 +265,7 @@ struct pgh_ctx {
     // the parallel pre-fault (r01ak) 8 MiB pieces close in 2.3-2.4 ms vs 2.6-2.7 for one piece.
     size_t d2h_piece = 8u << 20;
     bool prefault = true;  // PGH_PREFAULT: pre-fault big fresh checkpoint outputs in parallel (patch)
+    bool warmup_skipped = false;  // pgh_create's warm-up failed (e.g. no device memory left): skipped
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
     std::vector<float> weights;
@@ -333,6 +337,7 @@ void free_slab(pgh_ctx* c) {
     (void)hipFree(c->d_slab); c->d_slab = nullptr; c->slab_bytes = 0;
     (void)hipFree(c->d_ckpt); c->d_ckpt = nullptr;
     (void)hipFree(c->d_out); c->d_out = nullptr;
+    c->ckpt_valid = false;
     (void)hipFree(c->d_acc); c->d_acc = nullptr;
     (void)hipFree(c->d_uacc); c->d_uacc = nullptr;
     (void)hipFree(c->d_sum); c->d_sum = nullptr;
@@ -359,6 +364,13 @@ int check_ready(pgh_ctx* c) {
 int check_dtype(pgh_ctx* c, int dtype) {
     RC(check_ready(c));
     if (c->dtype != dtype) return fail(c, PGH_E_STATE, "slab holds dtype %d, call needs %d", c->dtype, dtype);
+    return PGH_OK;
+}
+
+int check_ckpt(pgh_ctx* c, const char* what) {
+    if (!c->ckpt_valid)
+        return fail(c, PGH_E_STATE, "%s: no checkpoint in HBM (pgh_ckpt_upload* since the last pgh_reserve / layout "
+                    "change)", what);
     return PGH_OK;
 }
 
@@ -1020,10 +1032,11 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
                  hipStreamSynchronize(c->stream) == hipSuccess;
             (void)hipFree(d);
         }
-        if (!ok) {
-            const hipError_t e = hipGetLastError();
-            pgh_destroy(c);
-            return fail(nullptr, PGH_E_HIP, "warm-up launch / copies failed: %s", hipGetErrorString(e));
+        if (!ok) {  // best effort: a latency optimisation must not cost the node its engine
+            (void)hipGetLastError();
+            (void)hipStreamSynchronize(c->copy);
+            (void)hipStreamSynchronize(c->stream);
+            c->warmup_skipped = true;
         }
     }
     *out = c;
@@ -1473,6 +1486,7 @@ int pgh_synth_ckpt_device(pgh_ctx* c, uint64_t seed, float* d_ckpt, void* stream
         return PGH_OK;
     }
     if (!c->d_ckpt) return fail(c, PGH_E_STATE, "pgh_reserve has not been called");
+    c->ckpt_valid = false;  // the resident checkpoint is used as scratch here
     hipError_t e = pgh::launch_synth_f32(c->d_ckpt, pgh::single_block(c->pvec), c->pvec, 1, c->pg, seed,
                                          pgh::STREAM_CKPT, 0, c->lo, pgh::CKPT_SCALE, s);
     if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic checkpoint failed: %s", hipGetErrorString(e));
@@ -1537,7 +1551,9 @@ int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
     const double t0 = now_ms();
     const size_t bytes = sizeof(float) * (size_t)c->pg;
     RC(order_before_overwrite(c));
+    c->ckpt_valid = false;
     RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
+    c->ckpt_valid = true;
     RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
     if (is_pinned(out)) {
         CK(c, hipMemcpyAsync(out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
@@ -1561,7 +1577,10 @@ int pgh_ckpt_upload(pgh_ctx* c, const float* ckpt, size_t nbytes) {
     DeviceGuard g(c->device);
     RC(order_before_overwrite(c));
     const uint8_t* src = (const uint8_t*)ckpt + (nbytes == whole ? 4 * (size_t)c->lo : 0);
-    return stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), src, shard, is_pinned(ckpt));
+    c->ckpt_valid = false;
+    RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), src, shard, is_pinned(ckpt)));
+    c->ckpt_valid = true;
+    return PGH_OK;
 }
 
 int pgh_ckpt_upload_state(pgh_ctx* c, const uint8_t* pb, size_t n) {
@@ -1573,11 +1592,15 @@ int pgh_ckpt_upload_state(pgh_ctx* c, const uint8_t* pb, size_t n) {
     for (auto& sp : spans) pieces.push_back(Piece{pb + sp.first, sp.second});
     DeviceGuard g(c->device);
     RC(order_before_overwrite(c));
-    return stage_pieces_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), pieces);
+    c->ckpt_valid = false;
+    RC(stage_pieces_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), pieces));
+    c->ckpt_valid = true;
+    return PGH_OK;
 }
 
 int pgh_fedavg_resident(pgh_ctx* c, int mode) {
     RC(check_dtype(c, PGH_F32));
+    RC(check_ckpt(c, "pgh_fedavg_resident"));
     DeviceGuard g(c->device);
     const double t0 = now_ms();
     RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
@@ -1589,6 +1612,7 @@ int pgh_fedavg_resident(pgh_ctx* c, int mode) {
 int pgh_ckpt_download(pgh_ctx* c, float* out) {
     RC(check_dtype(c, PGH_F32));
     if (!out) return fail(c, PGH_E_ARG, "out is NULL");
+    RC(check_ckpt(c, "pgh_ckpt_download"));
     DeviceGuard g(c->device);
     const size_t bytes = 4 * (size_t)c->pg;
     RC(order_after_ingest(c, c->stream));
@@ -1604,6 +1628,7 @@ int pgh_ckpt_download(pgh_ctx* c, float* out) {
 int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out) {
     RC(check_dtype(c, PGH_F32));
     if (!tmpl || !out) return fail(c, PGH_E_ARG, "tmpl / out is NULL");
+    RC(check_ckpt(c, "pgh_ckpt_patch_state"));
     std::vector<std::pair<size_t, size_t>> spans;
     RC(state_shard_spans(c, tmpl, n, &spans, "checkpoint template"));
     DeviceGuard g(c->device);
@@ -1745,6 +1770,7 @@ int pgh_stream_finish_device(pgh_ctx* c, const float* d_ckpt, float* d_out, void
 
 int pgh_stream_finish_resident(pgh_ctx* c) {
     RC(check_dtype(c, PGH_F32));
+    RC(check_ckpt(c, "pgh_stream_finish_resident"));
     DeviceGuard g(c->device);
     const double t0 = now_ms();
     RC(pgh_stream_finish_device(c, c->d_ckpt, c->d_out, c->stream));
@@ -1759,7 +1785,13 @@ int pgh_stream_finish(pgh_ctx* c, const float* ckpt, float* out) {
     DeviceGuard g(c->device);
     const double t0 = now_ms();
     const size_t bytes = sizeof(float) * (size_t)c->pg;
-    CK(c, hipMemcpyAsync(c->d_ckpt, ckpt, bytes, hipMemcpyHostToDevice, c->stream));
+    // staged like pgh_fedavg's checkpoint: on the copy stream after every fold that may still read
+    // d_ckpt, so fold_run's order_after_ingest orders the final fold after it (a pageable
+    // pgh_ckpt_upload's last ring DMA can no longer land after this copy)
+    RC(order_before_overwrite(c));
+    c->ckpt_valid = false;
+    RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
+    c->ckpt_valid = true;
     RC(pgh_stream_finish_device(c, c->d_ckpt, c->d_out, c->stream));
     CK(c, hipMemcpyAsync(out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));

@@ -121,9 +121,13 @@ class CycleAggregator:
             self.engine.ingest_state(i, d)
         if mode == WEIGHTED_MEAN:
             self.engine.set_weights(weights)
+        # From the fold on, HBM holds the NEW checkpoint: until its bytes exist, nobody may take the
+        # resident copy for `checkpoint` (a retry after a failed patch would fold twice).
+        self.engine.ckpt_owner = None
+        self._resident = None
         self.engine.fedavg_resident(mode)  # :252-296
-        self.engine.ckpt_owner = self
         new = self.engine.ckpt_patch_state(checkpoint)  # :303
+        self.engine.ckpt_owner = self
         self._resident = new
         return new
 

@@ -1,0 +1,71 @@
+"""bench.py forms the N-rank world itself (no GPU: --dry-run uses gloo on the CPU).
+
+The driver runs ``python bench.py --gpus N`` under torch.distributed.run for N > 1, but a plain
+``python bench.py --gpus N`` must measure N ranks too, never one rank labelled N.
+"""
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], cwd=str(ROOT), env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _json_line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_plain_bench_forms_two_ranks():
+    r = _run(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    rec = _json_line(r.stdout)
+    assert rec == {"dry_run": True, "n_gpus": 2, "backend": "gloo"}
+
+
+def test_plain_bench_forms_three_ranks():
+    r = _run(["--gpus", "3", "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    assert _json_line(r.stdout)["n_gpus"] == 3
+
+
+def test_single_rank_dry_run():
+    r = _run(["--dry-run"])
+    assert r.returncode == 0, r.stderr
+    assert _json_line(r.stdout)["n_gpus"] == 1
+
+
+def test_launcher_world_mismatch_fails_loudly():
+    # a launcher that formed 1 rank while --gpus says 2: exit non-zero, print no result line
+    r = _run(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "WORLD_SIZE 1" in r.stderr
+
+
+def test_torchrun_launch_forms_two_ranks():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29517", str(ROOT / "bench.py"),
+                        "--gpus", "2", "--dry-run"], cwd=str(ROOT), env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr
+    assert _json_line(r.stdout)["n_gpus"] == 2
+
+
+def test_usable_cores_reports_a_positive_count():
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    n, how = bench.usable_cores()
+    assert n >= 1 and n <= len(os.sched_getaffinity(0))
+    assert how in ("sched_getaffinity", "cgroup cpu quota")
