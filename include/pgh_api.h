@@ -151,6 +151,20 @@ int pgh_ckpt_download(pgh_ctx* ctx, float* out);  /* P_shard floats */
 /* out (n bytes) = tmpl with this shard's slice of every payload taken from the resident checkpoint. */
 int pgh_ckpt_patch_state(pgh_ctx* ctx, const uint8_t* tmpl, size_t n, uint8_t* out);
 
+/* ---- report-time folds of scattered slots -----------------------------
+ * RESIDENT slab.  Diffs are ingested into whichever slot is free when they are reported (client
+ * index = slot); the fold order is the reference's close-time order -- completed WorkerCycles in
+ * assignment (row id) order, cycle_manager.py:243-245 -- which the caller gives as slot lists:
+ * pgh_fold_slots folds `slots` (n entries, in list order) into the running fold state as soon as
+ * their positions are certain, and frees them for new ingests; the k-th slot folded since
+ * pgh_reset / pgh_reserve is fold client k (the iterative plan's k, weight index k; weights are set
+ * in fold order with pgh_set_weights).  pgh_fold_slots_finish_resident folds the rest (n may be 0)
+ * and writes ckpt - avg into the resident checkpoint (pgh_ckpt_upload*), like
+ * pgh_fedavg_resident: bit-identical to folding every diff contiguously at close.  `mode` stays the
+ * same within a cycle. */
+int pgh_fold_slots(pgh_ctx* ctx, int mode, const int32_t* slots, int n);
+int pgh_fold_slots_finish_resident(pgh_ctx* ctx, int mode, const int32_t* slots, int n);
+
 /* Z_2^64 share sum over all clients x parties, then decode float32(sum) / base**prec.
  * sum_out (int64) and dec_out (float32) are host arrays of P_shard; either may be NULL. */
 int pgh_secagg(pgh_ctx* ctx, int base, int prec, int64_t* sum_out, float* dec_out);

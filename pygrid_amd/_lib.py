@@ -79,6 +79,8 @@ SIGNATURES = {
     "pgh_ckpt_upload": (_i, [_vp, _vp, _sz]),
     "pgh_ckpt_upload_state": (_i, [_vp, C.c_char_p, _sz]),
     "pgh_fedavg_resident": (_i, [_vp, _i]),
+    "pgh_fold_slots": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
+    "pgh_fold_slots_finish_resident": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
     "pgh_ckpt_download": (_i, [_vp, _vp]),
     "pgh_ckpt_patch_state": (_i, [_vp, C.c_char_p, _sz, _vp]),
     "pgh_secagg": (_i, [_vp, _i, _i, _vp, _vp]),

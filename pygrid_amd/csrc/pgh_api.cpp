@@ -272,6 +272,7 @@ struct pgh_ctx {
     bool weights_on_device = false;
 
     bool streaming = false;
+    int slot_mode = -1;  // pgh_fold_slots: averaging mode of the cycle being folded slot by slot
     int kind = 0;
     int fold_batch = 1;
     int64_t folded = 0;  // stream: clients [0, folded) are in the running state
@@ -344,6 +345,7 @@ void free_slab(pgh_ctx* c) {
     (void)hipFree(c->d_dec); c->d_dec = nullptr;
     (void)hipFree(c->d_w); c->d_w = nullptr; c->w_cap = 0;
     c->slots = 0;
+    c->slot_mode = -1;
     c->slot_client.clear();
     for (auto& m : c->marks) c->mark_pool.push_back(m.ev);
     c->marks.clear();
@@ -1156,6 +1158,7 @@ int pgh_reset(pgh_ctx* c) {
     c->weights.clear();
     c->weights_on_device = false;
     c->streaming = false;
+    c->slot_mode = -1;
     c->folded = 0;
     c->st.n_clients = 0;
     c->st.n_folded = 0;
@@ -1497,7 +1500,7 @@ int pgh_synth_ckpt_device(pgh_ctx* c, uint64_t seed, float* d_ckpt, void* stream
 int pgh_set_weights(pgh_ctx* c, const float* w, int n) {
     if (!c) return PGH_E_ARG;
     if (!w || n <= 0) return fail(c, PGH_E_ARG, "need a non-empty weight vector");
-    if (c->streaming && c->folded > 0) {
+    if (c->folded > 0) {  // stream or slot folds: clients [0, folded) are in the running state
         for (int64_t k = 0; k < c->folded && k < n && k < (int64_t)c->weights.size(); ++k)
             if (std::memcmp(&w[k], &c->weights[(size_t)k], 4) != 0)
                 return fail(c, PGH_E_STATE, "weight of already folded client %lld changed", (long long)k);
@@ -1712,6 +1715,96 @@ int pgh_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out)
     CK(c, hipStreamSynchronize(c->stream));
     c->st.close_ms_last = now_ms() - t0;
     return collect_timings(c);
+}
+
+// ---- report-time folds of scattered slots (pgh_fold_slots) -------------------------------------
+
+namespace {
+int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
+    RC(check_dtype(c, PGH_F32));
+    if (!valid_mode(mode)) return fail(c, PGH_E_ARG, "unknown averaging mode %d", mode);
+    if (c->streaming) return fail(c, PGH_E_STATE, "context is streaming: slot folds need a RESIDENT slab");
+    if (n < 0 || (n > 0 && !slots)) return fail(c, PGH_E_ARG, "bad slot list (n=%d)", n);
+    if (c->slot_mode >= 0 && c->slot_mode != mode)
+        return fail(c, PGH_E_STATE, "averaging mode changed from %d to %d within a cycle", c->slot_mode, mode);
+    std::vector<char> seen((size_t)c->slots, 0);
+    for (int k = 0; k < n; ++k) {
+        const int32_t sl = slots[k];
+        if (sl < 0 || sl >= c->slots) return fail(c, PGH_E_ARG, "slot %d outside [0,%d)", sl, c->slots);
+        if (c->slot_client[(size_t)sl] < 0) return fail(c, PGH_E_STATE, "slot %d holds no unfolded diff", sl);
+        if (seen[(size_t)sl]) return fail(c, PGH_E_ARG, "slot %d listed twice", sl);
+        seen[(size_t)sl] = 1;
+    }
+    const int64_t c0 = c->folded, total = c0 + n;
+    FinalArgs fa;
+    if (final) {
+        RC(check_ckpt(c, "pgh_fold_slots_finish_resident"));
+        if (total == 0) return fail(c, PGH_E_STATE, "no diffs folded");
+        RC(fedavg_divisor(c, mode, total, &fa.divisor));
+    } else if (n == 0) {
+        return PGH_OK;
+    }
+    DeviceGuard g(c->device);
+    const hipStream_t s = c->stream;
+    RC(order_after_ingest(c, s));
+    if (mode == PGH_WEIGHTED_MEAN && n > 0) {
+        if ((int64_t)c->weights.size() < total)
+            return fail(c, PGH_E_STATE, "weighted mean: %zu weights for %lld clients", c->weights.size(),
+                        (long long)total);
+        RC(sync_weights(c, s));
+    }
+    if (mode == PGH_ITERATIVE_MEAN && n > 0) RC(ensure_recips(c, total, s));
+    const uint64_t pg = (uint64_t)c->pg;
+    int done = 0;
+    do {
+        const int m = std::min(n - done, pgh::ROWTAB_MAX);
+        pgh::RowTab tab;
+        for (int k = 0; k < m; ++k) tab.rows[k] = slots[done + k] * c->parties;
+        const bool first = (c0 + done == 0), last = (done + m == n);
+        pgh::FedavgArgs a{};
+        a.diffs = (const float*)c->d_slab;
+        a.map = slab_map(c);
+        a.n_rows = m;
+        a.client0 = c0 + done;
+        a.p = c->pg;
+        a.weights = c->d_w ? c->d_w + (c0 + done) : nullptr;
+        a.recips = c->d_rec ? c->d_rec + (c0 + done) : nullptr;
+        a.acc = c->d_acc;
+        a.ckpt = c->d_ckpt;
+        a.out = c->d_out;
+        a.divisor = fa.divisor;
+        a.flags = (first ? pgh::FL_FIRST : 0) | (final && last ? pgh::FL_FINAL : 0);
+        a.mode = mode;
+        a.variant = c->variant;
+        const uint64_t bytes = 4ull * (uint64_t)m * pg + (first ? 0 : 4 * pg) + ((a.flags & pgh::FL_FINAL) ? 8 * pg : 4 * pg);
+        RC(timed_launch(c, s, bytes, [&] { return pgh::launch_fedavg_rows(a, tab, s); }));
+        done += m;
+    } while (done < n);
+    RC(record_fold(c, s));
+    for (int k = 0; k < n; ++k) c->slot_client[(size_t)slots[k]] = -1;  // free for the next ingests
+    c->folded = total;
+    c->st.n_folded = total;
+    c->slot_mode = mode;
+    if (final) {
+        std::swap(c->d_ckpt, c->d_out);  // the new checkpoint is the next cycle's input
+        c->folded = 0;  // the next cycle folds from scratch
+        c->slot_mode = -1;
+    }
+    return PGH_OK;
+}
+}  // namespace
+
+int pgh_fold_slots(pgh_ctx* c, int mode, const int32_t* slots, int n) {
+    if (!c) return PGH_E_ARG;
+    return slot_fold(c, mode, slots, n, false);
+}
+
+int pgh_fold_slots_finish_resident(pgh_ctx* c, int mode, const int32_t* slots, int n) {
+    if (!c) return PGH_E_ARG;
+    const double t0 = now_ms();
+    RC(slot_fold(c, mode, slots, n, true));
+    c->st.close_ms_last = now_ms() - t0;
+    return PGH_OK;
 }
 
 // ---- STREAM reductions ---------------------------------------------------------------------------

@@ -49,6 +49,17 @@ struct FedavgArgs {
 };
 hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s);
 
+// Slab rows of one fold launch given by index instead of contiguous from `diffs`: row r of the
+// launch is slab row rows[r] (a.diffs = the slab at row 0).  Report-time aggregation folds the
+// reported diffs where they landed, in assignment order, skipping workers that never reported
+// (cycle_manager.py:243-245).  Passed by value as a kernel argument (scalar loads from the
+// kernarg segment), so a launch folds at most ROWTAB_MAX rows.
+constexpr int ROWTAB_MAX = 512;
+struct RowTab {
+    int32_t rows[ROWTAB_MAX];
+};
+hipError_t launch_fedavg_rows(const FedavgArgs& a, const RowTab& t, hipStream_t s);
+
 struct SecaggArgs {
     const int64_t* shares;  // slab at the first row (rows = clients x parties)
     SlabMap map;

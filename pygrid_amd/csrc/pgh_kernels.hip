@@ -126,6 +126,15 @@ __device__ __forceinline__ f32x4 iter_step(f32x4 acc, f32x4 v, float kf, double 
     return o;
 }
 
+// Slab row of the launch's row r: r itself (contiguous rows from a.diffs), or the r-th entry of
+// the row table (IDX: report-time folds of scattered slots; the index is wave-uniform, so it is a
+// scalar load from the kernarg segment).
+template <bool IDX>
+__device__ __forceinline__ size_t row_at(const RowTab* t, int r) {
+    if constexpr (IDX) return (size_t)(uint32_t)t->rows[r];
+    else return (size_t)r;
+}
+
 // Fold rows r .. r + nv - 1 (nv <= U, already loaded in v) into acc, in order.  nv is U for full
 // batches (the guards fold away) and the wave-uniform remainder for the last one.
 template <int MODE, int U, int W, class T>
@@ -175,8 +184,8 @@ __device__ __forceinline__ void fold_rows(T (&acc)[W], const T (&v)[U][W], const
 
 // W columns per lane (q0, q0 + qstep, ...: each load instruction of a wave still reads one
 // contiguous span), all rows of the chunk, in order.  VEC consecutive params per column.
-template <int MODE, int U, int W, bool NT, int VEC>
-__device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, int64_t qstep) {
+template <int MODE, int U, int W, bool NT, int VEC, bool IDX = false>
+__device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, const RowTab* tab, int64_t q0, int64_t qstep) {
     using L = Lane<VEC>;
     using T = typename L::T;
     const int n = a.n_rows;
@@ -189,7 +198,7 @@ __device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, 
     if (a.flags & FL_FIRST) {
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            acc[w] = L::template load<NT>(col[w]);  // fold starts at d0, not 0
+            acc[w] = L::template load<NT>(col[w] + row_at<IDX>(tab, 0) * ld);  // fold starts at d0, not 0
             if constexpr (MODE == MODE_WEIGHTED) acc[w] = acc[w] * a.weights[0];
         }
         r = 1;
@@ -204,7 +213,7 @@ __device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, 
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int w = 0; w < W; ++w)
-                v[u][w] = L::template load<NT>(col[w] + (size_t)(r + u) * ld);
+                v[u][w] = L::template load<NT>(col[w] + row_at<IDX>(tab, r + u) * ld);
         fold_rows<MODE, U, W>(acc, v, a, r, U);
     }
     if (r < n) {  // the last partial batch, its loads in flight together
@@ -214,7 +223,7 @@ __device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, int64_t q0, 
         for (int u = 0; u < U; ++u)
             if (u < nv)
 #pragma unroll
-                for (int w = 0; w < W; ++w) v[u][w] = L::template load<NT>(col[w] + (size_t)(r + u) * ld);
+                for (int w = 0; w < W; ++w) v[u][w] = L::template load<NT>(col[w] + row_at<IDX>(tab, r + u) * ld);
         fold_rows<MODE, U, W>(acc, v, a, r, nv);
     }
 #pragma unroll
@@ -300,17 +309,29 @@ __global__ __launch_bounds__(TB) void k_fedavg_pipe(FedavgArgs a, int64_t ncol) 
 }
 
 // Grid-stride over tiles of TB x W columns; a partial last tile goes one column per lane.
-template <int MODE, int U, int W, bool NT, int TB, int VEC>
-__global__ __launch_bounds__(TB) void k_fedavg(FedavgArgs a, int64_t ncol) {
+template <int MODE, int U, int W, bool NT, int TB, int VEC, bool IDX>
+__device__ __forceinline__ void fedavg_tiles(const FedavgArgs& a, const RowTab* tab, int64_t ncol) {
     const int64_t tile = (int64_t)TB * W;
     for (int64_t t0 = (int64_t)blockIdx.x * tile; t0 < ncol; t0 += (int64_t)gridDim.x * tile) {
         const int64_t q0 = t0 + threadIdx.x;
         if (t0 + tile <= ncol) {
-            fedavg_columns<MODE, U, W, NT, VEC>(a, q0, TB);
+            fedavg_columns<MODE, U, W, NT, VEC, IDX>(a, tab, q0, TB);
         } else {
-            for (int64_t q = q0; q < ncol && q < t0 + tile; q += TB) fedavg_columns<MODE, U, 1, NT, VEC>(a, q, TB);
+            for (int64_t q = q0; q < ncol && q < t0 + tile; q += TB)
+                fedavg_columns<MODE, U, 1, NT, VEC, IDX>(a, tab, q, TB);
         }
     }
+}
+
+template <int MODE, int U, int W, bool NT, int TB, int VEC>
+__global__ __launch_bounds__(TB) void k_fedavg(FedavgArgs a, int64_t ncol) {
+    fedavg_tiles<MODE, U, W, NT, TB, VEC, false>(a, nullptr, ncol);
+}
+
+// The same fold over the slab rows listed in `tab` (report-time aggregation, pgh_fold_slots).
+template <int MODE, int U, int W, bool NT, int TB, int VEC>
+__global__ __launch_bounds__(TB) void k_fedavg_rows(FedavgArgs a, int64_t ncol, RowTab tab) {
+    fedavg_tiles<MODE, U, W, NT, TB, VEC, true>(a, &tab, ncol);
 }
 
 // Z_2^64 lane element: VEC = 2 (16-byte column of 2 int64) or 1 (one int64 per lane).
@@ -582,6 +603,25 @@ hipError_t go_fedavg(const FedavgArgs& a, bool persistent, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int MODE, int U, int W, bool NT, int TB, int VEC>
+hipError_t go_fedavg_rows(const FedavgArgs& a, const RowTab& t, hipStream_t s) {
+    const int64_t ncol = (a.p + VEC - 1) / VEC;
+    k_fedavg_rows<MODE, U, W, NT, TB, VEC><<<grid_for(ncol, (int64_t)TB * W, false), TB, 0, s>>>(a, ncol, t);
+    return hipGetLastError();
+}
+
+// Indexed folds exist for the shapes the auto choice picks (auto_variant); an explicitly chosen
+// variant outside them runs the auto shape for its shard.
+template <int MODE>
+hipError_t dispatch_fedavg_rows(const FedavgArgs& a, const RowTab& t, int variant, hipStream_t s) {
+    switch (variant) {
+    case 11: return go_fedavg_rows<MODE, 16, 1, true, 64, 4>(a, t, s);
+    case 14: return go_fedavg_rows<MODE, 32, 1, true, 64, 1>(a, t, s);
+    case 17: return go_fedavg_rows<MODE, 64, 1, true, 64, 1>(a, t, s);
+    default: return go_fedavg_rows<MODE, 8, 1, true, 256, 4>(a, t, s);  // variant 0
+    }
+}
+
 template <int MODE, int U, int TB, int VEC>
 hipError_t go_fedavg_pipe(const FedavgArgs& a, hipStream_t s) {
     const int64_t ncol = (a.p + VEC - 1) / VEC;
@@ -677,6 +717,28 @@ hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
     case MODE_MEAN: return dispatch_fedavg<MODE_MEAN>(a, v, s);
     case MODE_ITERATIVE: return dispatch_fedavg<MODE_ITERATIVE>(a, v, s);
     case MODE_WEIGHTED: return dispatch_fedavg<MODE_WEIGHTED>(a, v, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_fedavg_rows(const FedavgArgs& a, const RowTab& t, hipStream_t s) {
+    if (a.n_rows > ROWTAB_MAX) return hipErrorInvalidValue;
+    if (a.p <= 0 || a.n_rows < 0 || !valid_map(a.map, a.p)) return hipErrorInvalidValue;
+    if ((a.flags & FL_FIRST) && a.n_rows < 1) return hipErrorInvalidValue;
+    if (a.n_rows > 0 && (!a.diffs || (reinterpret_cast<uintptr_t>(a.diffs) & 15))) return hipErrorInvalidValue;
+    if (!(a.flags & FL_FIRST) && (!a.acc || (reinterpret_cast<uintptr_t>(a.acc) & 15))) return hipErrorInvalidValue;
+    if (!(a.flags & FL_FINAL) && (!a.acc || (reinterpret_cast<uintptr_t>(a.acc) & 15))) return hipErrorInvalidValue;
+    if ((a.flags & FL_FINAL) && (!a.ckpt || !a.out || (reinterpret_cast<uintptr_t>(a.ckpt) & 15) ||
+                                 (reinterpret_cast<uintptr_t>(a.out) & 15)))
+        return hipErrorInvalidValue;
+    if (a.mode == MODE_WEIGHTED && a.n_rows > 0 && !a.weights) return hipErrorInvalidValue;
+    if (a.mode == MODE_ITERATIVE && a.n_rows > 0 && !a.recips) return hipErrorInvalidValue;
+    int v = auto_variant(a.p, a.mode);
+    if (a.variant == 0 || a.variant == 11 || a.variant == 14 || a.variant == 17) v = a.variant;
+    switch (a.mode) {
+    case MODE_MEAN: return dispatch_fedavg_rows<MODE_MEAN>(a, t, v, s);
+    case MODE_ITERATIVE: return dispatch_fedavg_rows<MODE_ITERATIVE>(a, t, v, s);
+    case MODE_WEIGHTED: return dispatch_fedavg_rows<MODE_WEIGHTED>(a, t, v, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -230,6 +230,19 @@ class Engine:
         """Fold into the resident checkpoint: afterwards it IS the new checkpoint."""
         self._check(self._lib.pgh_fedavg_resident(self._h, int(mode)), "fedavg_resident")
 
+    def fold_slots(self, mode: int, slots: Sequence[int]):
+        """Fold the diffs in ``slots`` (in this order) into the running state; frees the slots."""
+        a = np.ascontiguousarray(slots, dtype=np.int32)
+        self._check(self._lib.pgh_fold_slots(self._h, int(mode), a.ctypes.data_as(C.POINTER(C.c_int32)), a.size),
+                    "fold_slots")
+
+    def fold_slots_finish_resident(self, mode: int, slots: Sequence[int] = ()):
+        """Fold ``slots`` and finish into the resident checkpoint (it IS the new checkpoint then)."""
+        a = np.ascontiguousarray(slots, dtype=np.int32)
+        self._check(self._lib.pgh_fold_slots_finish_resident(self._h, int(mode),
+                                                             a.ctypes.data_as(C.POINTER(C.c_int32)), a.size),
+                    "fold_slots_finish_resident")
+
     def ckpt_download(self) -> np.ndarray:
         out = np.empty(self.p_shard, dtype=np.float32)
         self._check(self._lib.pgh_ckpt_download(self._h, _ptr(out)), "ckpt_download")

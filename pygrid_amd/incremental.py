@@ -1,63 +1,89 @@
 """Fold diffs into HBM as they are reported.
 
 The reference stores every reported diff in the DB (``submit_worker_diff``,
-``cycle_manager.py:151-178``) and reads them all back at cycle close
-(``_average_plan_diffs``, ``:243-250``) in the order of the completed-WorkerCycle query
+``cycle_manager.py:151-178``) and reads them all back at cycle close (``_average_plan_diffs``,
+``:243-250``) in the order of the completed-WorkerCycle query
 (``self._worker_cycles.query(cycle_id=..., is_completed=True)``: row-id order, i.e. the order in
-which workers were assigned, ``cycle_manager.assign``).  The fp32 fold depends on that order, so a
-diff can be folded early only once its position is certain: when every worker assigned before it
-has already reported.  ``IncrementalCycle`` keeps that rule:
+which workers were assigned, ``cycle_manager.assign``), skipping the workers that never reported
+(the reference expects ~20 % of them not to: ``routes.py:314``).  The fp32 fold depends on that
+order, so ``IncrementalCycle`` separates WHERE a diff lives from WHEN it is folded:
 
-* ``assigned(wid)`` records assignment order (WorkerCycle id order);
-* ``reported(wid, diff)`` folds the longest prefix of assigned workers that have all reported
-  (engine STREAM use: H2D of later diffs overlaps the folds) and parks the rest on the host;
-* ``close(checkpoint)`` drops the workers that never reported (the reference's query skips
-  incomplete rows), folds the parked diffs in id order, and returns the new checkpoint bytes --
-  bit-identical to folding everything at close time.
+* ``reported(wid, diff)`` copies the diff into HBM at once, into whichever slab slot is free
+  (``pgh_ingest_state``: PCIe + host copy happen while the report is handled, in any arrival
+  order);
+* the fold follows assignment order: a diff's position is certain once every worker assigned
+  before it has reported, and the certain prefix is folded from its scattered slots
+  (``pgh_fold_slots``: the kernel reads the slots through a row table), freeing them;
+* ``close(checkpoint)`` drops the workers that never reported and folds the remaining reporters'
+  slots in id order into the resident checkpoint (``pgh_fold_slots_finish_resident``), then patches
+  the new State bytes from HBM -- bit-identical to folding everything at close time.
+
+So a missing early worker no longer parks later diffs on the host: they wait in HBM, and close
+costs the fold of the not-yet-folded rows (HBM-bound, ~6.8 TB/s) plus the patch.  Only when every
+slot is taken does a diff wait on the host (``slots`` is the HBM budget in diffs); one slot is
+always kept for the fold front, so the front can never be starved by later diffs.
 
 Thread safety: the node calls ``reported`` from request handlers and ``close`` from its executor
 thread (``tasks/cycle.py``), so every method holds the cycle's lock (the engine context itself is
 single-owner).  A report that arrives after ``close`` started raises ``AggregationError`` -- the
-reference likewise averages only the diffs its query saw (``cycle_manager.py:243-245``).
+reference likewise averages only the diffs its query saw (``cycle_manager.py:243-245``).  A
+malformed diff is rejected in its own ``reported`` call (``StateParseError``, nothing recorded),
+so one bad client cannot break the cycle for the others.
 
 The checkpoint can be handed over when the cycle starts (``checkpoint=``): its payloads are then
-uploaded into HBM while clients report, and ``close`` only folds the last partial batch into it
-and patches the new State bytes from HBM -- O(P) work after the last report instead of the
-reference's N + 1 unserializations and N-way fold.
+uploaded into HBM while clients report, and ``close`` touches only the rows not folded yet.
 """
 from __future__ import annotations
 
 import threading
 from typing import Dict, List, Optional
 
+from . import state as state_codec
 from .engine import F32, MEAN, Engine
-from .exceptions import AggregationError
+from .exceptions import AggregationError, StateParseError
+
+DEFAULT_HBM_BUDGET = 64 << 30  # bytes of diffs kept in HBM per cycle when `slots` is not given
+MAX_DEFAULT_SLOTS = 4096
+
+
+def default_slots(P: int, budget: int = DEFAULT_HBM_BUDGET) -> int:
+    return int(max(4, min(MAX_DEFAULT_SLOTS, budget // max(4 * P, 1))))
 
 
 class IncrementalCycle:
-    def __init__(self, engine: Engine, numel, mode: int = MEAN, ring_slots: int = 64, fold_batch: int = 0,
+    def __init__(self, engine: Engine, numel, mode: int = MEAN, slots: Optional[int] = None, fold_batch: int = 8,
                  weights_by_worker: Optional[Dict[object, float]] = None, checkpoint: Optional[bytes] = None):
         self.engine = engine
         self.mode = mode
+        self._numel = tuple(int(n) for n in numel)
+        self.slots = int(slots) if slots else default_slots(sum(self._numel))
+        if self.slots < 2:
+            raise AggregationError("report-time aggregation needs at least 2 HBM slots")
+        self.fold_batch = max(1, int(fold_batch))
         self._order: List[object] = []      # assigned workers, assignment order
         self._pos: Dict[object, int] = {}
-        self._parked: Dict[object, bytes] = {}
         self._reported = set()
-        self._front = 0                     # next assigned position not yet folded / skipped
-        self._next_client = 0               # next engine client index (fold order)
+        self._slot_of: Dict[object, int] = {}  # reported, in HBM, not folded
+        self._parked: Dict[object, bytes] = {}  # reported, no free slot yet (host)
+        self._free: List[int] = list(range(self.slots - 1, -1, -1))
+        self._ready: List[object] = []      # position certain, in HBM, not folded yet (fold order)
+        self._front = 0                     # next assigned position not yet certain
+        self._n_folded = 0
         self._weights_by_worker = weights_by_worker
-        self._weights: List[float] = []
+        self._weights: List[float] = []     # fold order
         self.folded_early = 0
         self._lock = threading.Lock()
         self._closed = False
-        # keep the engine's ring when a cycle of the same model follows (no re-allocation)
-        if tuple(getattr(engine, "numel", ())) != tuple(int(n) for n in numel) or \
-                getattr(engine, "max_clients", 0) != ring_slots or getattr(engine, "dtype", None) != F32:
-            engine.set_layout(list(numel))
-            engine.reserve(ring_slots)
-        engine.stream_begin(mode, fold_batch)
+        # keep the engine's slab when a cycle of the same model follows (no re-allocation)
+        if tuple(getattr(engine, "numel", ())) != self._numel or getattr(engine, "max_clients", 0) != self.slots \
+                or getattr(engine, "dtype", None) != F32:
+            engine.set_layout(list(self._numel))
+            engine.reserve(self.slots)
+        else:
+            engine.reset()
         self._ckpt: Optional[bytes] = None  # checkpoint bytes whose payloads are resident in HBM
         if checkpoint is not None:
+            engine.ckpt_owner = None
             engine.ckpt_upload_state(checkpoint)
             engine.ckpt_owner = self
             self._ckpt = checkpoint
@@ -77,27 +103,59 @@ class IncrementalCycle:
                 raise AggregationError(f"worker {worker!r} reported without being assigned to the cycle")
             if worker in self._reported:
                 raise AggregationError(f"worker {worker!r} reported twice")
+            front = self._pos[worker] == self._front
+            # a diff that cannot fold yet leaves one slot free for the fold front
+            if self._free and (front or len(self._free) > 1):
+                self._to_hbm(worker, diff)  # raises StateParseError on a malformed diff: nothing recorded
+            else:
+                self._check_layout(worker, diff)
+                self._parked[worker] = diff
             self._reported.add(worker)
-            self._parked[worker] = diff
             self._advance(final=False)
 
-    def _ingest(self, worker):
-        if self._weights_by_worker is not None:
-            self._weights.append(float(self._weights_by_worker[worker]))
+    def _check_layout(self, worker, diff: bytes):
+        got = tuple(state_codec.tensor_numels(diff))
+        if got != self._numel:
+            raise StateParseError(f"worker {worker!r}: diff holds tensors of {got} floats, the model {self._numel}")
+
+    def _to_hbm(self, worker, diff: bytes):
+        slot = self._free.pop()
+        try:
+            self.engine.ingest_state(slot, diff)
+        except Exception:
+            self._free.append(slot)
+            raise
+        self._slot_of[worker] = slot
+
+    def _fold_ready(self, final: bool):
+        ws = self._ready
+        self._ready = []
+        slots = [self._slot_of.pop(w) for w in ws]
+        if self._weights_by_worker is not None and ws:
+            self._weights.extend(float(self._weights_by_worker[w]) for w in ws)
             self.engine.set_weights(self._weights)
-        self.engine.ingest_state(self._next_client, self._parked.pop(worker))
-        self._next_client += 1
+        if final:
+            self.engine.fold_slots_finish_resident(self.mode, slots)
+        else:
+            self.engine.fold_slots(self.mode, slots)
+            self.folded_early += len(slots)
+        self._free.extend(reversed(slots))
+        self._n_folded += len(slots)
 
     def _advance(self, final: bool):
         while self._front < len(self._order):
             w = self._order[self._front]
             if w in self._reported:
-                if not final:
-                    self.folded_early += 1
-                self._ingest(w)
+                if w in self._parked:  # its turn: it needs a slot now
+                    if not self._free:
+                        self._fold_ready(final=False)  # frees >= 1 slot (see the invariant above)
+                    self._to_hbm(w, self._parked.pop(w))
+                self._ready.append(w)
             elif not final:
-                return  # an earlier worker may still report: later positions are not certain yet
+                break  # an earlier worker may still report: later positions are not certain yet
             self._front += 1  # at close, a worker that never reported is dropped
+            if not final and len(self._ready) >= self.fold_batch:
+                self._fold_ready(final=False)
 
     def close(self, checkpoint: bytes) -> bytes:
         """New checkpoint bytes (``cycle_manager.py:293-303``)."""
@@ -106,15 +164,24 @@ class IncrementalCycle:
                 raise AggregationError("cycle already closed")
             self._closed = True
             self._advance(final=True)
-            if self._next_client == 0:
+            if self._n_folded + len(self._ready) == 0:
                 raise AggregationError("no diffs to average")
             if checkpoint is not self._ckpt or getattr(self.engine, "ckpt_owner", None) is not self:
+                self.engine.ckpt_owner = None
                 self.engine.ckpt_upload_state(checkpoint)  # scan + staged H2D of the payload spans
-            self.engine.stream_finish_resident()
+            # from the fold on, HBM holds the NEW checkpoint: nobody may take it for `checkpoint`
+            self.engine.ckpt_owner = None
+            self._ckpt = None
+            self._fold_ready(final=True)
+            new = self.engine.ckpt_patch_state(checkpoint)
             self.engine.ckpt_owner = self
-            self._ckpt = None  # HBM now holds the NEW checkpoint
-            return self.engine.ckpt_patch_state(checkpoint)
+            return new
 
     @property
     def n_folded(self) -> int:
-        return self._next_client
+        return self._n_folded
+
+    @property
+    def n_parked(self) -> int:
+        """Reported diffs waiting on the host because every HBM slot was taken."""
+        return len(self._parked)

@@ -13,9 +13,10 @@ def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
+@pytest.mark.parametrize("slots", [3, 8, 32])
 @pytest.mark.parametrize("ckpt_at_start", [False, True])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_incremental_cycle_matches_reference_order(engine, mode, ckpt_at_start):
+def test_incremental_cycle_matches_reference_order(engine, mode, ckpt_at_start, slots):
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast, parse_state
 
@@ -27,7 +28,7 @@ def test_incremental_cycle_matches_reference_order(engine, mode, ckpt_at_start):
     reporters = [w for w in range(n_assigned) if w % 5 != 3]  # workers 3, 8, 13, 18, 23 never report
     ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
     ckpt_pb = build_state_fast(ckpt)
-    inc = IncrementalCycle(engine, [int(np.prod(s)) for s in shapes], mode=mode, ring_slots=8, fold_batch=2,
+    inc = IncrementalCycle(engine, [int(np.prod(s)) for s in shapes], mode=mode, slots=slots, fold_batch=2,
                            weights_by_worker=weights if mode == 2 else None,
                            checkpoint=ckpt_pb if ckpt_at_start else None)
     for w in range(n_assigned):
@@ -68,7 +69,7 @@ def test_shared_engine_resident_checkpoint_is_not_trusted_after_another_user(eng
     want1 = O.fedavg_mean(ck0, d1)
     # someone else uses the engine in between
     other_ck = mk(1.0)
-    inc = IncrementalCycle(engine, numel, ring_slots=4, fold_batch=2, checkpoint=build_state_fast(other_ck))
+    inc = IncrementalCycle(engine, numel, slots=4, fold_batch=2, checkpoint=build_state_fast(other_ck))
     inc.assigned(0)
     inc.reported(0, build_state_fast(mk(1e-2)))
     inc.close(build_state_fast(other_ck))
@@ -78,3 +79,68 @@ def test_shared_engine_resident_checkpoint_is_not_trusted_after_another_user(eng
     want2 = O.fedavg_mean(want1, d2)
     for got, w in zip(parse_state(new2), want2):
         assert np.array_equal(bits(got), bits(w))
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_dropouts_at_position_zero_shuffled_arrival(engine, mode):
+    """routes.py:314: ~20 % of assigned workers never report, here including the very first one,
+    so nothing can fold before close: every reporter waits in its HBM slot and close folds them
+    through the row table (> ROWTAB_MAX rows: several indexed launches) -- bit-exact."""
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(170 + mode)
+    shapes = [(129, 33), (33,)]
+    n_assigned = 700
+    reporters = [w for w in range(n_assigned) if w != 0 and rng.random() >= 0.2]
+    diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in reporters}
+    weights = {w: float(rng.uniform(0.5, 3.0)) for w in range(n_assigned)}
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    ckpt_pb = build_state_fast(ckpt)
+    inc = IncrementalCycle(engine, [int(np.prod(s)) for s in shapes], mode=mode, slots=n_assigned, fold_batch=8,
+                           weights_by_worker=weights if mode == 2 else None, checkpoint=ckpt_pb)
+    for w in range(n_assigned):
+        inc.assigned(w)
+    for w in rng.permutation(reporters):
+        inc.reported(int(w), build_state_fast(diffs[int(w)]))
+    assert inc.n_folded == 0 and inc.n_parked == 0
+    new = inc.close(ckpt_pb)
+    ref = [diffs[w] for w in sorted(reporters)]
+    if mode == 0:
+        want = O.fedavg_mean(ckpt, ref)
+    elif mode == 1:
+        want = O.fedavg_iterative(ckpt, ref)
+    else:
+        want = O.fedavg_weighted(ckpt, ref, np.array([weights[w] for w in sorted(reporters)], F))
+    for got, w in zip(parse_state(new), want):
+        assert np.array_equal(bits(got), bits(w))
+    assert inc.n_folded == len(reporters)
+
+
+def test_fold_slots_api_edges(engine):
+    """pgh_fold_slots rejects empty / foreign / duplicate slots and a mode change; a finish with no
+    new slots after early folds writes the average of what was folded."""
+    from pygrid_amd.exceptions import AggregationError
+
+    rng = np.random.default_rng(181)
+    P = 1000
+    d = (rng.standard_normal((6, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    engine.set_layout([P])
+    engine.reserve(8)
+    engine.ckpt_upload(c)
+    for k, slot in enumerate([5, 2, 7, 0, 3, 1]):
+        engine.ingest(slot, d[k])
+    with pytest.raises(AggregationError):
+        engine.fold_slots(0, [4])          # slot 4 holds nothing
+    with pytest.raises(AggregationError):
+        engine.fold_slots(0, [5, 5])       # listed twice
+    engine.fold_slots(0, [5, 2, 7])
+    with pytest.raises(AggregationError):
+        engine.fold_slots(1, [0])          # mode changed mid-cycle
+    with pytest.raises(AggregationError):
+        engine.fold_slots(0, [5])          # already folded (slot freed)
+    engine.fold_slots(0, [0, 3])
+    engine.fold_slots_finish_resident(0, [])
+    want = O.fedavg_mean([c], [[x] for x in d[:5]])[0]
+    assert np.array_equal(bits(engine.ckpt_download()), bits(want))

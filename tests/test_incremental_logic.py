@@ -1,93 +1,153 @@
 """CPU: fold order of report-time aggregation (pygrid_amd/incremental.py) with a recording
-engine: the engine must see clients in WorkerCycle-id order with non-reporters dropped, and fold
-early only when the position is certain."""
+engine.  Every reported diff must reach HBM at once (any arrival order), and the engine must fold
+the clients in WorkerCycle-id order with non-reporters dropped (cycle_manager.py:243-245),
+folding early only what is certain."""
 import numpy as np
 import pytest
 
-from pygrid_amd.exceptions import AggregationError
+from pygrid_amd.exceptions import AggregationError, StateParseError
 from pygrid_amd.incremental import IncrementalCycle
+from pygrid_amd.state_schema import build_state_fast
 
 
 class RecordingEngine:
-    def __init__(self):
+    """Slots hold payloads; folds are recorded as payload lists in fold order."""
+
+    def __init__(self, fail_on=None):
         self.calls = []
         self.weights = []
+        self.slot = {}
+        self.folds = []  # (final, [payload, ...])
+        self.fail_on = fail_on
 
     def set_layout(self, numel):
         self.calls.append(("layout", tuple(numel)))
 
     def reserve(self, n):
         self.calls.append(("reserve", n))
+        self.max_slots = n
 
-    def stream_begin(self, mode, batch):
-        self.calls.append(("begin", mode, batch))
+    def reset(self):
+        self.calls.append(("reset",))
 
     def set_weights(self, w):
         self.weights = list(w)
 
     def ingest_state(self, k, pb):
+        if self.fail_on is not None and pb == self.fail_on:
+            raise StateParseError("malformed diff")
+        assert 0 <= k < self.max_slots and k not in self.slot, (k, self.slot)
+        self.slot[k] = pb
         self.calls.append(("ingest", k, pb))
+
+    def fold_slots(self, mode, slots):
+        self.folds.append((False, [self.slot.pop(s) for s in slots]))
+        self.calls.append(("fold", len(slots)))
+
+    def fold_slots_finish_resident(self, mode, slots):
+        self.folds.append((True, [self.slot.pop(s) for s in slots]))
+        self.calls.append(("finish",))
 
     def ckpt_upload_state(self, pb):
         self.calls.append(("upload", pb))
-
-    def stream_finish_resident(self):
-        self.calls.append(("finish",))
 
     def ckpt_patch_state(self, pb):
         self.calls.append(("patch", pb))
         return pb
 
 
-def ingests(eng):
-    return [(c[1], c[2]) for c in eng.calls if c[0] == "ingest"]
+def folded(eng):
+    return [p for _, ps in eng.folds for p in ps]
 
 
-def test_in_order_reports_fold_immediately():
+def mk(w: int) -> bytes:
+    """A valid 3-float State diff that identifies worker w (parked diffs are scanned)."""
+    return build_state_fast([np.full(3, w, np.float32)])
+
+
+def test_in_order_reports_fold_in_batches():
     eng = RecordingEngine()
-    inc = IncrementalCycle(eng, [10])
+    inc = IncrementalCycle(eng, [10], fold_batch=2, slots=8)
     for w in ("a", "b", "c"):
         inc.assigned(w)
     for w in ("a", "b", "c"):
         inc.reported(w, w.encode())
-    assert ingests(eng) == [(0, b"a"), (1, b"b"), (2, b"c")]
-    assert inc.folded_early == 3
+    assert folded(eng) == [b"a", b"b"]  # c waits for a full batch (or close)
+    assert inc.folded_early == 2
+    inc.close(b"ck")
+    assert folded(eng) == [b"a", b"b", b"c"] and eng.folds[-1] == (True, [b"c"])
 
 
-def test_out_of_order_waits_for_earlier_workers():
+def test_out_of_order_reports_go_to_hbm_at_once_and_fold_in_id_order():
     eng = RecordingEngine()
-    inc = IncrementalCycle(eng, [10])
+    inc = IncrementalCycle(eng, [10], fold_batch=1, slots=8)
     for w in range(5):
         inc.assigned(w)
     inc.reported(2, b"2")
     inc.reported(1, b"1")
-    assert ingests(eng) == []            # worker 0 may still report
+    assert sorted(eng.slot.values()) == [b"1", b"2"]  # in HBM although worker 0 may still report
+    assert folded(eng) == []
     inc.reported(0, b"0")
-    assert ingests(eng) == [(0, b"0"), (1, b"1"), (2, b"2")]
+    assert folded(eng) == [b"0", b"1", b"2"]
     inc.reported(4, b"4")
-    assert len(ingests(eng)) == 3        # worker 3 outstanding
+    assert len(folded(eng)) == 3 and b"4" in eng.slot.values()  # worker 3 outstanding
 
 
 def test_close_drops_non_reporters_and_keeps_id_order():
-    from pygrid_amd.state_schema import build_state_fast
-
     eng = RecordingEngine()
-    inc = IncrementalCycle(eng, [3])
+    inc = IncrementalCycle(eng, [3], slots=8)
     for w in range(6):
         inc.assigned(w)
     for w in (5, 1, 4, 2):
         inc.reported(w, bytes([w]))
-    assert ingests(eng) == []            # worker 0 never reports
+    assert folded(eng) == []            # worker 0 never reports
+    assert sorted(eng.slot.values()) == [bytes([w]) for w in (1, 2, 4, 5)]
     ck = build_state_fast([np.array([1.0, 2.0, 3.0], np.float32)])
     assert inc.close(ck) == ck
-    assert ingests(eng) == [(0, b"\x01"), (1, b"\x02"), (2, b"\x04"), (3, b"\x05")]
+    assert eng.folds == [(True, [b"\x01", b"\x02", b"\x04", b"\x05"])]
     assert inc.n_folded == 4 and inc.folded_early == 0
     assert [c[0] for c in eng.calls[-3:]] == ["upload", "finish", "patch"]
 
 
+def test_twenty_percent_dropouts_shuffled_arrival():
+    """The reference's expected failure rate (routes.py:314), reports in random order: every
+    reporter is in HBM before close, and the close folds exactly the reporters in id order."""
+    rng = np.random.default_rng(5)
+    eng = RecordingEngine()
+    n = 100
+    inc = IncrementalCycle(eng, [3], slots=n, fold_batch=4)
+    for w in range(n):
+        inc.assigned(w)
+    reporters = [w for w in range(n) if rng.random() >= 0.2]
+    order = list(rng.permutation(reporters))
+    for w in order:
+        inc.reported(int(w), int(w).to_bytes(2, "little"))
+        assert inc.n_parked == 0
+    inc.close(b"ck")
+    assert folded(eng) == [w.to_bytes(2, "little") for w in sorted(reporters)]
+
+
+def test_slot_pressure_parks_on_host_but_never_starves_the_front():
+    """Fewer slots than reporters: later diffs wait on the host, one slot stays for the fold front,
+    and the fold order is still the id order."""
+    rng = np.random.default_rng(6)
+    for trial in range(20):
+        eng = RecordingEngine()
+        n, slots = 40, int(rng.integers(2, 7))
+        inc = IncrementalCycle(eng, [3], slots=slots, fold_batch=int(rng.integers(1, 5)))
+        for w in range(n):
+            inc.assigned(w)
+        reporters = [w for w in range(n) if rng.random() >= 0.25]
+        for w in rng.permutation(reporters):
+            inc.reported(int(w), mk(int(w)))
+            assert len(eng.slot) <= slots
+        inc.close(b"ck")
+        assert folded(eng) == [mk(w) for w in sorted(reporters)], trial
+
+
 def test_checkpoint_handed_over_at_start_is_uploaded_once():
     eng = RecordingEngine()
-    inc = IncrementalCycle(eng, [3], checkpoint=b"ck")
+    inc = IncrementalCycle(eng, [3], checkpoint=b"ck", slots=4)
     assert eng.calls[-1] == ("upload", b"ck")  # before any report: the upload overlaps the cycle
     inc.assigned("a")
     inc.reported("a", b"a")
@@ -98,7 +158,8 @@ def test_checkpoint_handed_over_at_start_is_uploaded_once():
 
 def test_weights_follow_fold_order():
     eng = RecordingEngine()
-    inc = IncrementalCycle(eng, [3], mode=2, weights_by_worker={"x": 1.0, "y": 2.0, "z": 3.0})
+    inc = IncrementalCycle(eng, [3], mode=2, slots=4, fold_batch=1,
+                           weights_by_worker={"x": 1.0, "y": 2.0, "z": 3.0})
     for w in ("x", "y", "z"):
         inc.assigned(w)
     inc.reported("z", b"z")
@@ -109,17 +170,53 @@ def test_weights_follow_fold_order():
 
 def test_errors():
     eng = RecordingEngine()
-    inc = IncrementalCycle(eng, [3])
+    inc = IncrementalCycle(eng, [3], slots=4)
     with pytest.raises(AggregationError):
         inc.reported("ghost", b"")
     inc.assigned("a")
     inc.reported("a", b"a")
     with pytest.raises(AggregationError):
         inc.reported("a", b"a")
-    inc2 = IncrementalCycle(RecordingEngine(), [3])
+    inc2 = IncrementalCycle(RecordingEngine(), [3], slots=4)
     inc2.assigned("b")
     with pytest.raises(AggregationError):
         inc2.close(b"")
+
+
+def test_malformed_diff_is_refused_to_its_sender_only():
+    """a bad diff raises in its own report and leaves no trace; the honest workers'
+    reports and the close still work (the reference's report only stores the blob)."""
+    eng = RecordingEngine(fail_on=b"bad")
+    inc = IncrementalCycle(eng, [3], slots=8, fold_batch=1)
+    for w in range(4):
+        inc.assigned(w)
+    with pytest.raises(StateParseError):
+        inc.reported(0, b"bad")
+    inc.reported(1, b"1")
+    inc.reported(0, b"0")  # the worker may retry with a good diff
+    inc.reported(3, b"3")
+    inc.close(b"ck")
+    assert folded(eng) == [b"0", b"1", b"3"]
+
+
+def test_malformed_diff_is_refused_when_it_would_park():
+    """A diff that cannot go to HBM yet (no spare slot) is validated before it is parked."""
+    ck = build_state_fast([np.zeros(3, np.float32)])
+    good = build_state_fast([np.ones(3, np.float32)])
+    bad = build_state_fast([np.ones(4, np.float32)])
+    eng = RecordingEngine()
+    inc = IncrementalCycle(eng, [3], slots=2, fold_batch=4)
+    for w in range(4):
+        inc.assigned(w)
+    inc.reported(2, good)       # takes a slot (one stays for the front)
+    with pytest.raises(StateParseError):
+        inc.reported(3, bad)    # would park: scanned against the layout first
+    inc.reported(3, good)
+    assert inc.n_parked == 1
+    inc.reported(0, good)
+    inc.reported(1, good)
+    inc.close(ck)
+    assert len(folded(eng)) == 4
 
 
 def test_reports_from_many_threads_and_a_late_one():
@@ -128,19 +225,19 @@ def test_reports_from_many_threads_and_a_late_one():
     import threading
 
     eng = RecordingEngine()
-    inc = IncrementalCycle(eng, [3], checkpoint=b"ck")
+    inc = IncrementalCycle(eng, [3], checkpoint=b"ck", slots=16, fold_batch=3)
     workers = list(range(64))
     for w in workers:
         inc.assigned(w)
     rng = np.random.default_rng(4)
     order = [int(w) for w in rng.permutation(workers)]
-    threads = [threading.Thread(target=inc.reported, args=(w, bytes([w]))) for w in order]
+    threads = [threading.Thread(target=inc.reported, args=(w, mk(w))) for w in order]
     for t in threads:
         t.start()
     for t in threads:
         t.join()
-    assert ingests(eng) == [(k, bytes([k])) for k in range(64)]
     inc.close(b"ck")
+    assert folded(eng) == [mk(k) for k in range(64)]
     with pytest.raises(AggregationError):
         inc.reported(0, b"late")
     with pytest.raises(AggregationError):
