@@ -14,8 +14,9 @@
  * pgh_last_error() then holds the message.  Plain pointers and sizes only.  Host buffers
  * passed in are borrowed for the duration of the call.  A context is single-owner and not
  * re-entrant (the reference serialises cycle close with run_task_once,
- * apps/node/src/app/main/model_centric/tasks/cycle.py:9-25).  One context drives one GPU;
- * multi-GPU runs one process (and one context) per GPU, each owning a parameter shard.
+ * apps/node/src/app/main/model_centric/tasks/cycle.py:9-25).  A context drives one GPU
+ * (pgh_create) or several GPUs of one node from one process (pgh_create_group); the
+ * alternative is one process (and one context) per GPU, each owning a parameter shard.
  */
 #ifndef PGH_API_H
 #define PGH_API_H
@@ -27,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PGH_ABI_VERSION 3
+#define PGH_ABI_VERSION 4
 
 typedef struct pgh_ctx pgh_ctx;
 
@@ -78,6 +79,33 @@ int pgh_device_count(int* n);
  * pay for the code-object load and the copy engines' first use. */
 int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out);
 void pgh_destroy(pgh_ctx* ctx);
+
+/* ---- several GPUs of one node in ONE process ----------------------------
+ * The node closes a cycle from one thread of one process (apps/node/src/app/__init__.py:196-199,
+ * tasks/cycle.py:9-25), so the library itself drives every GPU: one context over n_gpus GPUs
+ * (devices[i], or 0 .. n_gpus - 1 when devices is NULL), one child context and one host thread per
+ * GPU.  The parameter axis is cut into contiguous 64-aligned shards, one per GPU; each GPU holds
+ * every client for its shard, so every ingest sends each GPU its slice over its own PCIe link,
+ * every fold runs on all GPUs at once, host outputs are written slice by slice, and fp32 results
+ * are bit-identical to one GPU.  Secure aggregation may shard the CLIENTS instead
+ * (pgh_set_client_sharding before pgh_reserve of an int64 slab): client k lives on GPU
+ * k / ceil(max_clients / n_gpus), each GPU sums its clients over the whole model, the Z_2^64 sums
+ * are reduce-scattered (ncclReduceScatter, uint64 SUM: exact) and each GPU decodes its slice.
+ * Every entry point above and below accepts a group context, except the ones taking device
+ * pointers or returning slab geometry (PGH_E_UNSUPPORTED: they name one GPU -- call them on
+ * pgh_group_child).  Collectives go over RCCL (librccl.so.1, loaded at first use: ncclCommInitAll
+ * over the group's devices) when the devices are distinct, else (or with PGH_RCCL=0) over peer
+ * copies. */
+int pgh_create_group(int n_gpus, const int* devices, size_t pinned_bytes, pgh_ctx** out);
+int pgh_group_size(const pgh_ctx* ctx, int* n);              /* 1 for a single-GPU context */
+int pgh_group_child(pgh_ctx* ctx, int i, pgh_ctx** child);    /* borrowed context of GPU i */
+int pgh_set_client_sharding(pgh_ctx* ctx, int on);
+/* All-gather the resident checkpoint into a full copy on every GPU (ncclAllGather of equal shards
+ * of S = ceil(P / n_gpus) rounded up to 64 floats, or peer copies): GPU g's copy holds shard r at
+ * [r * S, r * S + len_r).  d_full_out (nullable) receives one device pointer per GPU. */
+int pgh_group_allgather_resident(pgh_ctx* ctx, void** d_full_out);
+/* The exchange in use: 1 RCCL, 0 peer copies, -1 none yet (or not a group). */
+int pgh_group_backend(pgh_ctx* ctx, int* rccl);
 const char* pgh_last_error(const pgh_ctx* ctx);   /* ctx may be NULL (creation errors) */
 /* Page-locked host buffers: ingest DMAs them straight to HBM (no staging copy). */
 int pgh_host_alloc(size_t bytes, void** out);

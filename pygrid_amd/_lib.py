@@ -59,6 +59,12 @@ SIGNATURES = {
     "pgh_device_count": (_i, [C.POINTER(C.c_int)]),
     "pgh_create": (_i, [_i, _sz, C.POINTER(_vp)]),
     "pgh_destroy": (None, [_vp]),
+    "pgh_create_group": (_i, [_i, C.POINTER(C.c_int), _sz, C.POINTER(_vp)]),
+    "pgh_group_size": (_i, [_vp, C.POINTER(C.c_int)]),
+    "pgh_group_child": (_i, [_vp, _i, C.POINTER(_vp)]),
+    "pgh_set_client_sharding": (_i, [_vp, _i]),
+    "pgh_group_allgather_resident": (_i, [_vp, C.POINTER(_vp)]),
+    "pgh_group_backend": (_i, [_vp, C.POINTER(C.c_int)]),
     "pgh_last_error": (C.c_char_p, [_vp]),
     "pgh_host_alloc": (_i, [_sz, C.POINTER(_vp)]),
     "pgh_host_free": (_i, [_vp]),
@@ -108,7 +114,7 @@ SIGNATURES = {
     "pgh_b64_decode": (_i, [C.c_char_p, _sz, _vp, C.POINTER(_sz), _i]),
 }
 
-ABI_VERSION = 3  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
+ABI_VERSION = 4  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
 _LIB = None
 
 

@@ -16,8 +16,9 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libpygrid_hip.so"
-SOURCES = [CSRC / "pgh_kernels.hip", CSRC / "pgh_api.cpp", CSRC / "pgh_state.cpp", CSRC / "pgh_b64.cpp"]
-HEADERS = [CSRC / "pgh_kernels.h", CSRC / "pgh_state.h", ROOT / "include" / "pgh_api.h"]
+SOURCES = [CSRC / "pgh_kernels.hip", CSRC / "pgh_api.cpp", CSRC / "pgh_group.cpp", CSRC / "pgh_state.cpp",
+           CSRC / "pgh_b64.cpp"]
+HEADERS = [CSRC / "pgh_kernels.h", CSRC / "pgh_state.h", CSRC / "pgh_internal.h", ROOT / "include" / "pgh_api.h"]
 ARCH = os.environ.get("PGH_OFFLOAD_ARCH", "gfx950")
 
 
@@ -55,8 +56,9 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         subprocess.run(cmd, check=True)
         objs.append(str(obj))
     tmp = LIB.with_suffix(".so.tmp")
+    # -ldl: librccl.so.1 is dlopen'ed at the first multi-GPU collective (no link-time RCCL)
     cmd = [hipcc(), "-shared", "-fPIC", *objs, "-o", str(tmp), f"--offload-arch={ARCH}",
-           "-Wl,-soname,libpygrid_hip.so"]
+           "-Wl,-soname,libpygrid_hip.so", "-ldl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -45,6 +45,7 @@
 #include <vector>
 
 #include "../../include/pgh_api.h"
+#include "pgh_internal.h"
 #include "pgh_kernels.h"
 #include "pgh_state.h"
 
@@ -190,6 +191,7 @@ class CopyPool {
 };
 
 struct pgh_ctx {
+    pgh_group* grp = nullptr;  // set: a multi-GPU group (pgh_create_group); the rest is unused
     int device = 0;
     hipStream_t stream = nullptr;  // reductions
     hipStream_t copy = nullptr;    // ingest H2D and on-device synthetic fill
@@ -266,6 +268,8 @@ struct pgh_ctx {
     size_t d2h_piece = 8u << 20;
     bool prefault = true;  // PGH_PREFAULT: pre-fault big fresh checkpoint outputs in parallel (patch)
     bool warmup_skipped = false;  // pgh_create's warm-up failed (e.g. no device memory left): skipped
+    int64_t vec_min = 0;      // [P_shard] device vectors at least this long (group collectives)
+    int64_t client_base = 0;  // synthetic client k is generated as global client client_base + k
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
     std::vector<float> weights;
@@ -289,14 +293,19 @@ namespace {
 
 thread_local std::string g_create_err;
 
-int fail(pgh_ctx* c, int code, const char* fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
+int vfail(pgh_ctx* c, int code, const char* fmt, va_list ap) {
+    char buf[1024];
     vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
     if (c) c->err = buf; else g_create_err = buf;
     return code;
+}
+
+int fail(pgh_ctx* c, int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    const int r = vfail(c, code, fmt, ap);
+    va_end(ap);
+    return r;
 }
 
 #define CK(c, expr)                                                                            \
@@ -1047,6 +1056,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
 
 void pgh_destroy(pgh_ctx* c) {
     if (!c) return;
+    if (c->grp) { pgh_group_api::destroy(c); return; }
     DeviceGuard g(c->device);
     free_slab(c);
     for (auto& t : c->pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
@@ -1072,6 +1082,7 @@ void pgh_destroy(pgh_ctx* c) {
 }
 
 int pgh_set_layout(pgh_ctx* c, int n_tensors, const int64_t* numel) {
+    if (c && c->grp) return pgh_group_api::set_layout(c, n_tensors, numel);
     if (!c) return PGH_E_ARG;
     if (n_tensors <= 0 || !numel) return fail(c, PGH_E_ARG, "need at least one tensor");
     int64_t P = 0;
@@ -1089,6 +1100,7 @@ int pgh_set_layout(pgh_ctx* c, int n_tensors, const int64_t* numel) {
 }
 
 int pgh_set_shard(pgh_ctx* c, int64_t lo, int64_t hi) {
+    if (c && c->grp) return pgh_group_api::set_shard(c, lo, hi);
     if (!c) return PGH_E_ARG;
     if (!c->layout) return fail(c, PGH_E_STATE, "pgh_set_layout has not been called");
     if (lo < 0 || hi > c->P || lo >= hi)
@@ -1098,12 +1110,13 @@ int pgh_set_shard(pgh_ctx* c, int64_t lo, int64_t hi) {
     c->lo = lo;
     c->hi = hi;
     c->pg = hi - lo;
-    c->pvec = (c->pg + 63) & ~(int64_t)63;
+    c->pvec = std::max((c->pg + 63) & ~(int64_t)63, (c->vec_min + 63) & ~(int64_t)63);
     c->st.p_shard = c->pg;
     return PGH_OK;
 }
 
 int pgh_reserve(pgh_ctx* c, int max_clients, int dtype, int n_parties) {
+    if (c && c->grp) return pgh_group_api::reserve(c, max_clients, dtype, n_parties);
     if (!c) return PGH_E_ARG;
     if (!c->layout) return fail(c, PGH_E_STATE, "pgh_set_layout has not been called");
     if (max_clients <= 0) return fail(c, PGH_E_ARG, "max_clients must be positive");
@@ -1147,6 +1160,7 @@ int pgh_reserve(pgh_ctx* c, int max_clients, int dtype, int n_parties) {
 }
 
 int pgh_reset(pgh_ctx* c) {
+    if (c && c->grp) return pgh_group_api::reset(c);
     if (!c) return PGH_E_ARG;
     DeviceGuard g(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -1166,6 +1180,7 @@ int pgh_reset(pgh_ctx* c) {
 }
 
 int pgh_ingest_raw(pgh_ctx* c, int client, const void* flat, size_t nbytes, int dtype) {
+    if (c && c->grp) return pgh_group_api::ingest_raw(c, client, flat, nbytes, dtype);
     RC(check_dtype(c, dtype));
     if (!flat) return fail(c, PGH_E_ARG, "flat is NULL");
     const size_t es = esize(dtype);
@@ -1187,6 +1202,7 @@ int pgh_ingest_raw(pgh_ctx* c, int client, const void* flat, size_t nbytes, int 
 }
 
 int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
+    if (c && c->grp) return pgh_group_api::ingest_state(c, client, pb, n);
     RC(check_dtype(c, PGH_F32));
     if (!pb && n) return fail(c, PGH_E_ARG, "pb is NULL");
     // The shard's slice of the payloads goes straight from the protobuf buffer into the pinned ring.
@@ -1395,6 +1411,7 @@ int decode_share_msgs(pgh_ctx* c, std::vector<ShareMsg>& msgs, int slot) {
 }  // namespace
 
 int pgh_ingest_state_shares(pgh_ctx* c, int client, int n_parties, const uint8_t* const* pbs, const size_t* ns) {
+    if (c && c->grp) return pgh_group_api::ingest_state_shares(c, client, n_parties, pbs, ns);
     RC(check_dtype(c, PGH_I64));
     if (!pbs || !ns) return fail(c, PGH_E_ARG, "pbs / ns is NULL");
     if (n_parties != c->parties)
@@ -1420,6 +1437,7 @@ int pgh_ingest_state_shares(pgh_ctx* c, int client, int n_parties, const uint8_t
 }
 
 int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
+    if (c && c->grp) return pgh_group_api::synth_ingest(c, seed, client0, n);
     RC(check_ready(c));
     if (n <= 0 || client0 < 0) return fail(c, PGH_E_ARG, "bad client range %d + %d", client0, n);
     DeviceGuard g(c->device);
@@ -1444,11 +1462,11 @@ int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
         hipError_t e;
         if (c->dtype == PGH_F32)
             e = pgh::launch_synth_f32((float*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->pg, seed,
-                                      pgh::STREAM_DIFF, client, c->lo, pgh::DIFF_SCALE, c->copy,
+                                      pgh::STREAM_DIFF, c->client_base + client, c->lo, pgh::DIFF_SCALE, c->copy,
                                       c->streaming ? c->synth_wgs : 0, c->synth_kind);
         else
             e = pgh::launch_synth_shares((int64_t*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->parties,
-                                         c->pg, seed, client, c->lo, 1000.0f, c->copy);
+                                         c->pg, seed, c->client_base + client, c->lo, 1000.0f, c->copy);
         if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic fill failed: %s", hipGetErrorString(e));
         for (int j = 0; j < run; ++j) {
             if (c->slot_client[(size_t)(slot + j)] != client + j) c->st.n_clients += 1;
@@ -1461,6 +1479,7 @@ int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
 }
 
 int pgh_set_synth_kind(pgh_ctx* c, int kind) {
+    if (c && c->grp) return pgh_group_api::set_synth_kind(c, kind);
     if (!c) return PGH_E_ARG;
     if (kind != 0 && kind != 1) return fail(c, PGH_E_ARG, "synthetic generator kind %d is not 0 or 1", kind);
     c->synth_kind = kind;
@@ -1468,6 +1487,7 @@ int pgh_set_synth_kind(pgh_ctx* c, int kind) {
 }
 
 int pgh_synth_fill(pgh_ctx* c, uint64_t seed, int n_clients) {
+    if (c && c->grp) return pgh_group_api::synth_fill(c, seed, n_clients);
     RC(check_ready(c));
     if (c->streaming) return fail(c, PGH_E_STATE, "pgh_synth_fill is for resident slabs; use pgh_synth_ingest");
     if (n_clients <= 0 || n_clients > c->slots)
@@ -1477,6 +1497,7 @@ int pgh_synth_fill(pgh_ctx* c, uint64_t seed, int n_clients) {
 }
 
 int pgh_synth_ckpt_device(pgh_ctx* c, uint64_t seed, float* d_ckpt, void* stream) {
+    if (c && c->grp) return fail(c, PGH_E_UNSUPPORTED, "%s takes device pointers, which name one GPU: call it on pgh_group_child", __func__);
     if (!c) return PGH_E_ARG;
     if (!c->layout) return fail(c, PGH_E_STATE, "pgh_set_layout has not been called");
     if (!d_ckpt || ((uintptr_t)d_ckpt & 15)) return fail(c, PGH_E_ARG, "d_ckpt must be a 16-byte aligned device pointer");
@@ -1498,6 +1519,7 @@ int pgh_synth_ckpt_device(pgh_ctx* c, uint64_t seed, float* d_ckpt, void* stream
 }
 
 int pgh_set_weights(pgh_ctx* c, const float* w, int n) {
+    if (c && c->grp) return pgh_group_api::set_weights(c, w, n);
     if (!c) return PGH_E_ARG;
     if (!w || n <= 0) return fail(c, PGH_E_ARG, "need a non-empty weight vector");
     if (c->folded > 0) {  // stream or slot folds: clients [0, folded) are in the running state
@@ -1514,6 +1536,7 @@ int pgh_set_weights(pgh_ctx* c, const float* w, int n) {
 // ---- RESIDENT reductions -------------------------------------------------------------------------
 
 int pgh_fedavg_device(pgh_ctx* c, int mode, const float* d_ckpt, float* d_out, void* stream) {
+    if (c && c->grp) return fail(c, PGH_E_UNSUPPORTED, "%s takes device pointers, which name one GPU: call it on pgh_group_child", __func__);
     RC(check_dtype(c, PGH_F32));
     if (!valid_mode(mode)) return fail(c, PGH_E_ARG, "unknown averaging mode %d", mode);
     if (!d_ckpt || !d_out) return fail(c, PGH_E_ARG, "d_ckpt / d_out is NULL");
@@ -1531,6 +1554,7 @@ int pgh_fedavg_device(pgh_ctx* c, int mode, const float* d_ckpt, float* d_out, v
 
 int pgh_fedavg_device_range(pgh_ctx* c, int mode, int64_t off, int64_t len, const float* d_ckpt, float* d_out,
                             void* stream) {
+    if (c && c->grp) return fail(c, PGH_E_UNSUPPORTED, "%s takes device pointers, which name one GPU: call it on pgh_group_child", __func__);
     RC(check_dtype(c, PGH_F32));
     if (!valid_mode(mode)) return fail(c, PGH_E_ARG, "unknown averaging mode %d", mode);
     if (!d_ckpt || !d_out || (((uintptr_t)d_ckpt | (uintptr_t)d_out) & 15))
@@ -1548,6 +1572,7 @@ int pgh_fedavg_device_range(pgh_ctx* c, int mode, int64_t off, int64_t len, cons
 }
 
 int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
+    if (c && c->grp) return pgh_group_api::fedavg(c, mode, ckpt, out);
     RC(check_dtype(c, PGH_F32));
     if (!ckpt || !out) return fail(c, PGH_E_ARG, "ckpt / out is NULL");
     DeviceGuard g(c->device);
@@ -1571,6 +1596,7 @@ int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
 // ---- resident checkpoint: the new checkpoint stays in HBM as the next cycle's input ------------
 
 int pgh_ckpt_upload(pgh_ctx* c, const float* ckpt, size_t nbytes) {
+    if (c && c->grp) return pgh_group_api::ckpt_upload(c, ckpt, nbytes);
     RC(check_dtype(c, PGH_F32));
     if (!ckpt) return fail(c, PGH_E_ARG, "ckpt is NULL");
     const size_t whole = 4 * (size_t)c->P, shard = 4 * (size_t)c->pg;
@@ -1587,6 +1613,7 @@ int pgh_ckpt_upload(pgh_ctx* c, const float* ckpt, size_t nbytes) {
 }
 
 int pgh_ckpt_upload_state(pgh_ctx* c, const uint8_t* pb, size_t n) {
+    if (c && c->grp) return pgh_group_api::ckpt_upload_state(c, pb, n);
     RC(check_dtype(c, PGH_F32));
     if (!pb && n) return fail(c, PGH_E_ARG, "pb is NULL");
     std::vector<std::pair<size_t, size_t>> spans;
@@ -1602,6 +1629,7 @@ int pgh_ckpt_upload_state(pgh_ctx* c, const uint8_t* pb, size_t n) {
 }
 
 int pgh_fedavg_resident(pgh_ctx* c, int mode) {
+    if (c && c->grp) return pgh_group_api::fedavg_resident(c, mode);
     RC(check_dtype(c, PGH_F32));
     RC(check_ckpt(c, "pgh_fedavg_resident"));
     DeviceGuard g(c->device);
@@ -1613,6 +1641,7 @@ int pgh_fedavg_resident(pgh_ctx* c, int mode) {
 }
 
 int pgh_ckpt_download(pgh_ctx* c, float* out) {
+    if (c && c->grp) return pgh_group_api::ckpt_download(c, out);
     RC(check_dtype(c, PGH_F32));
     if (!out) return fail(c, PGH_E_ARG, "out is NULL");
     RC(check_ckpt(c, "pgh_ckpt_download"));
@@ -1629,6 +1658,7 @@ int pgh_ckpt_download(pgh_ctx* c, float* out) {
 }
 
 int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out) {
+    if (c && c->grp) return pgh_group_api::ckpt_patch_state(c, tmpl, n, out);
     RC(check_dtype(c, PGH_F32));
     if (!tmpl || !out) return fail(c, PGH_E_ARG, "tmpl / out is NULL");
     RC(check_ckpt(c, "pgh_ckpt_patch_state"));
@@ -1665,6 +1695,7 @@ int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out
 }
 
 int pgh_secagg_device(pgh_ctx* c, int base, int prec, int64_t* d_sum, float* d_dec, void* stream) {
+    if (c && c->grp) return fail(c, PGH_E_UNSUPPORTED, "%s takes device pointers, which name one GPU: call it on pgh_group_child", __func__);
     RC(check_dtype(c, PGH_I64));
     DeviceGuard g(c->device);
     int64_t n = 0;
@@ -1678,6 +1709,7 @@ int pgh_secagg_device(pgh_ctx* c, int base, int prec, int64_t* d_sum, float* d_d
 
 int pgh_secagg_device_range(pgh_ctx* c, int base, int prec, int64_t off, int64_t len, int64_t* d_sum, float* d_dec,
                             void* stream) {
+    if (c && c->grp) return fail(c, PGH_E_UNSUPPORTED, "%s takes device pointers, which name one GPU: call it on pgh_group_child", __func__);
     RC(check_dtype(c, PGH_I64));
     DeviceGuard g(c->device);
     int64_t n = 0;
@@ -1693,6 +1725,7 @@ int pgh_secagg_device_range(pgh_ctx* c, int base, int prec, int64_t off, int64_t
 
 int pgh_secagg_decode_device(pgh_ctx* c, int base, int prec, const int64_t* d_sum, int64_t n, float* d_dec,
                              void* stream) {
+    if (c && c->grp) return fail(c, PGH_E_UNSUPPORTED, "%s takes device pointers, which name one GPU: call it on pgh_group_child", __func__);
     if (!c) return fail(nullptr, PGH_E_ARG, "null context");
     if (n < 0 || (n > 0 && (!d_sum || !d_dec))) return fail(c, PGH_E_ARG, "bad decode arguments (n=%lld)", (long long)n);
     DeviceGuard g(c->device);
@@ -1706,6 +1739,7 @@ int pgh_secagg_decode_device(pgh_ctx* c, int base, int prec, const int64_t* d_su
 }
 
 int pgh_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out) {
+    if (c && c->grp) return pgh_group_api::secagg(c, base, prec, sum_out, dec_out);
     RC(check_dtype(c, PGH_I64));
     DeviceGuard g(c->device);
     const double t0 = now_ms();
@@ -1795,11 +1829,13 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
 }  // namespace
 
 int pgh_fold_slots(pgh_ctx* c, int mode, const int32_t* slots, int n) {
+    if (c && c->grp) return pgh_group_api::fold_slots(c, mode, slots, n, false);
     if (!c) return PGH_E_ARG;
     return slot_fold(c, mode, slots, n, false);
 }
 
 int pgh_fold_slots_finish_resident(pgh_ctx* c, int mode, const int32_t* slots, int n) {
+    if (c && c->grp) return pgh_group_api::fold_slots(c, mode, slots, n, true);
     if (!c) return PGH_E_ARG;
     const double t0 = now_ms();
     RC(slot_fold(c, mode, slots, n, true));
@@ -1810,6 +1846,7 @@ int pgh_fold_slots_finish_resident(pgh_ctx* c, int mode, const int32_t* slots, i
 // ---- STREAM reductions ---------------------------------------------------------------------------
 
 int pgh_stream_begin(pgh_ctx* c, int kind, int fold_batch) {
+    if (c && c->grp) return pgh_group_api::stream_begin(c, kind, fold_batch);
     RC(check_ready(c));
     if (kind == PGH_STREAM_SECAGG) {
         if (c->dtype != PGH_I64) return fail(c, PGH_E_STATE, "secagg stream needs an int64 slab");
@@ -1825,6 +1862,7 @@ int pgh_stream_begin(pgh_ctx* c, int kind, int fold_batch) {
 }
 
 int pgh_stream_flush(pgh_ctx* c) {
+    if (c && c->grp) return pgh_group_api::stream_flush(c);
     RC(check_ready(c));
     if (!c->streaming) return fail(c, PGH_E_STATE, "not streaming");
     DeviceGuard g(c->device);
@@ -1851,6 +1889,7 @@ int stream_finish(pgh_ctx* c, FinalArgs fa, hipStream_t cs, bool fedavg, int mod
 }  // namespace
 
 int pgh_stream_finish_device(pgh_ctx* c, const float* d_ckpt, float* d_out, void* stream) {
+    if (c && c->grp) return fail(c, PGH_E_UNSUPPORTED, "%s takes device pointers, which name one GPU: call it on pgh_group_child", __func__);
     RC(check_dtype(c, PGH_F32));
     if (!d_ckpt || !d_out || (((uintptr_t)d_ckpt | (uintptr_t)d_out) & 15))
         return fail(c, PGH_E_ARG, "d_ckpt / d_out must be 16-byte aligned device pointers");
@@ -1862,6 +1901,7 @@ int pgh_stream_finish_device(pgh_ctx* c, const float* d_ckpt, float* d_out, void
 }
 
 int pgh_stream_finish_resident(pgh_ctx* c) {
+    if (c && c->grp) return pgh_group_api::stream_finish_resident(c);
     RC(check_dtype(c, PGH_F32));
     RC(check_ckpt(c, "pgh_stream_finish_resident"));
     DeviceGuard g(c->device);
@@ -1873,6 +1913,7 @@ int pgh_stream_finish_resident(pgh_ctx* c) {
 }
 
 int pgh_stream_finish(pgh_ctx* c, const float* ckpt, float* out) {
+    if (c && c->grp) return pgh_group_api::stream_finish(c, ckpt, out);
     RC(check_dtype(c, PGH_F32));
     if (!ckpt || !out) return fail(c, PGH_E_ARG, "ckpt / out is NULL");
     DeviceGuard g(c->device);
@@ -1893,6 +1934,7 @@ int pgh_stream_finish(pgh_ctx* c, const float* ckpt, float* out) {
 }
 
 int pgh_stream_finish_secagg_device(pgh_ctx* c, int base, int prec, int64_t* d_sum, float* d_dec, void* stream) {
+    if (c && c->grp) return fail(c, PGH_E_UNSUPPORTED, "%s takes device pointers, which name one GPU: call it on pgh_group_child", __func__);
     RC(check_dtype(c, PGH_I64));
     DeviceGuard g(c->device);
     FinalArgs fa;
@@ -1903,6 +1945,7 @@ int pgh_stream_finish_secagg_device(pgh_ctx* c, int base, int prec, int64_t* d_s
 }
 
 int pgh_stream_finish_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out) {
+    if (c && c->grp) return pgh_group_api::stream_finish_secagg(c, base, prec, sum_out, dec_out);
     RC(check_dtype(c, PGH_I64));
     DeviceGuard g(c->device);
     const double t0 = now_ms();
@@ -1918,6 +1961,7 @@ int pgh_stream_finish_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, f
 // ---- observability -------------------------------------------------------------------------------
 
 int pgh_set_variant(pgh_ctx* c, int variant) {
+    if (c && c->grp) return pgh_group_api::set_variant(c, variant);
     if (!c) return PGH_E_ARG;
     if (variant < -1 || variant > 22) return fail(c, PGH_E_ARG, "variant %d outside [-1,22]", variant);
     c->variant = variant;
@@ -1925,6 +1969,7 @@ int pgh_set_variant(pgh_ctx* c, int variant) {
 }
 
 int pgh_effective_variant(pgh_ctx* c, int mode) {
+    if (c && c->grp) return pgh_group_api::effective_variant(c, mode);
     if (!c) return PGH_E_ARG;
     if (!c->layout) return fail(c, PGH_E_STATE, "pgh_set_layout has not been called");
     if (c->variant >= 0) return c->variant;
@@ -1934,6 +1979,7 @@ int pgh_effective_variant(pgh_ctx* c, int mode) {
 }
 
 int pgh_stats(pgh_ctx* c, pgh_stats_t* out) {
+    if (c && c->grp) return pgh_group_api::stats(c, out);
     if (!c || !out) return PGH_E_ARG;
     DeviceGuard g(c->device);
     RC(collect_timings(c));
@@ -1942,6 +1988,7 @@ int pgh_stats(pgh_ctx* c, pgh_stats_t* out) {
 }
 
 int pgh_reset_stats(pgh_ctx* c) {
+    if (c && c->grp) return pgh_group_api::reset_stats(c);
     if (!c) return PGH_E_ARG;
     DeviceGuard g(c->device);
     RC(collect_timings(c));
@@ -1956,6 +2003,7 @@ int pgh_reset_stats(pgh_ctx* c) {
 }
 
 int pgh_slab(pgh_ctx* c, void** d_slab, int64_t* ld, int64_t* block_pitch) {
+    if (c && c->grp) return fail(c, PGH_E_UNSUPPORTED, "%s takes device pointers, which name one GPU: call it on pgh_group_child", __func__);
     if (!c || !d_slab || !ld || !block_pitch) return PGH_E_ARG;
     *d_slab = c->d_slab;
     *ld = c->bw;
@@ -1964,6 +2012,7 @@ int pgh_slab(pgh_ctx* c, void** d_slab, int64_t* ld, int64_t* block_pitch) {
 }
 
 int pgh_sync(pgh_ctx* c) {
+    if (c && c->grp) return pgh_group_api::sync(c);
     if (!c) return PGH_E_ARG;
     DeviceGuard g(c->device);
     CK(c, hipStreamSynchronize(c->copy));
@@ -1972,3 +2021,71 @@ int pgh_sync(pgh_ctx* c) {
 }
 
 }  // extern "C"
+
+// ---- internals for the multi-GPU group driver (pgh_internal.h) ------------------------------------
+
+namespace pgh_int {
+int fail(pgh_ctx* c, int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    const int r = vfail(c, code, fmt, ap);
+    va_end(ap);
+    return r;
+}
+pgh_group* group_of(const pgh_ctx* c) { return c ? c->grp : nullptr; }
+pgh_ctx* new_group_ctx(pgh_group* g, int device) {
+    auto* c = new pgh_ctx();
+    c->grp = g;
+    c->device = device;
+    return c;
+}
+void free_group_ctx(pgh_ctx* c) { delete c; }
+int device_of(const pgh_ctx* c) { return c->device; }
+hipStream_t stream_of(const pgh_ctx* c) { return c->stream; }
+int64_t shard_lo(const pgh_ctx* c) { return c->lo; }
+int64_t shard_len(const pgh_ctx* c) { return c->pg; }
+int set_vec_min(pgh_ctx* c, int64_t n) {
+    if (n < 0) return fail(c, PGH_E_ARG, "negative vector length");
+    c->vec_min = n;
+    if (c->layout) c->pvec = std::max((c->pg + 63) & ~(int64_t)63, (c->vec_min + 63) & ~(int64_t)63);
+    return PGH_OK;
+}
+int set_copy_threads(pgh_ctx* c, int n) {
+    n = std::max(1, n);
+    if (n == c->copy_threads && c->pool_copy) return PGH_OK;
+    c->copy_threads = n;
+    c->pool_copy.reset(new CopyPool(n));
+    return PGH_OK;
+}
+int set_client_base(pgh_ctx* c, int64_t base) {
+    c->client_base = base;
+    return PGH_OK;
+}
+void* vec(pgh_ctx* c, int which) {
+    switch (which) {
+    case V_CKPT: return c->d_ckpt;
+    case V_SUM: return c->d_sum;
+    case V_DEC: return c->d_dec;
+    default: return nullptr;
+    }
+}
+int patch_payloads(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out) {
+    RC(check_dtype(c, PGH_F32));
+    if (!tmpl || !out) return fail(c, PGH_E_ARG, "tmpl / out is NULL");
+    RC(check_ckpt(c, "pgh_ckpt_patch_state"));
+    std::vector<std::pair<size_t, size_t>> spans;
+    RC(state_shard_spans(c, tmpl, n, &spans, "checkpoint template"));
+    DeviceGuard g(c->device);
+    std::vector<OutPiece> pieces;
+    for (auto& sp : spans) pieces.push_back(OutPiece{out + sp.first, sp.second});
+    RC(order_after_ingest(c, c->stream));
+    RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, pieces, c->stream, [&] {
+        if (out != tmpl && c->prefault && !spans.empty()) {  // this shard's part of the fresh output
+            const size_t a = spans.front().first, b = spans.back().first + spans.back().second;
+            if (b > a) prefault_parallel(out + a, b - a, *c->pool_copy);
+        }
+    }));
+    return collect_timings(c);
+}
+}  // namespace pgh_int
+

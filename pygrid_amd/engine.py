@@ -84,15 +84,37 @@ class _Serialized:
 
 
 class Engine:
-    def __init__(self, device: int = 0, pinned_bytes: int = 0):
-        self._lib = _Serialized(_lib.load(), threading.RLock())
-        h = C.c_void_p()
-        rc = self._lib.pgh_create(int(device), int(pinned_bytes), C.byref(h))
-        if rc != 0:
-            msg = getattr(self._lib.errors, "msg", "")
-            raise EngineUnavailableError(f"pgh_create(device={device}) failed: {msg}")
+    """One libpygrid_hip context: one GPU (``device``), or several GPUs of this node driven from
+    this process (``devices=[0, 1, ...]``: ``pgh_create_group``, parameter shards across the GPUs,
+    bit-identical results, one host thread per GPU inside the library)."""
+
+    def __init__(self, device: int = 0, pinned_bytes: int = 0, devices: Optional[Sequence[int]] = None,
+                 _borrowed=None):
+        self._lib = _Serialized(_lib.load(), threading.RLock()) if _borrowed is None else _borrowed[1]
+        self._owned = _borrowed is None
+        if _borrowed is not None:
+            h = _borrowed[0]
+            devs = [int(device)]
+        elif devices is not None:
+            devs = [int(d) for d in devices]
+            if not devs:
+                raise EngineUnavailableError("a group needs at least one device")
+            h = C.c_void_p()
+            arr = (C.c_int * len(devs))(*devs)
+            rc = self._lib.pgh_create_group(len(devs), arr, int(pinned_bytes), C.byref(h))
+            if rc != 0:
+                msg = getattr(self._lib.errors, "msg", "")
+                raise EngineUnavailableError(f"pgh_create_group(devices={devs}) failed: {msg}")
+        else:
+            devs = [int(device)]
+            h = C.c_void_p()
+            rc = self._lib.pgh_create(int(device), int(pinned_bytes), C.byref(h))
+            if rc != 0:
+                msg = getattr(self._lib.errors, "msg", "")
+                raise EngineUnavailableError(f"pgh_create(device={device}) failed: {msg}")
         self._h = h
-        self.device = int(device)
+        self.devices = devs
+        self.device = devs[0]
         self.numel: Tuple[int, ...] = ()
         self.P = 0
         self.lo = 0
@@ -113,8 +135,42 @@ class Engine:
 
     def close(self):
         if getattr(self, "_h", None):
-            self._lib.pgh_destroy(self._h)
+            if getattr(self, "_owned", True):
+                self._lib.pgh_destroy(self._h)
             self._h = None
+
+    # ---- multi-GPU group ----------------------------------------------------------------------
+    @property
+    def n_gpus(self) -> int:
+        n = C.c_int(0)
+        self._check(self._lib.pgh_group_size(self._h, C.byref(n)), "group_size")
+        return n.value
+
+    def child(self, i: int) -> "Engine":
+        """GPU i's context of a group (borrowed: valid while this engine lives), for the entry points
+        that take device pointers.  A single-GPU engine is its own child 0."""
+        k = C.c_void_p()
+        self._check(self._lib.pgh_group_child(self._h, int(i), C.byref(k)), "group_child")
+        e = Engine(self.devices[i] if i < len(self.devices) else self.device, _borrowed=(k, self._lib))
+        e.numel, e.P = self.numel, self.P
+        return e
+
+    def set_client_sharding(self, on: bool = True):
+        """Group + int64 shares: split the CLIENTS across the GPUs (ncclReduceScatter of the sums)."""
+        self._check(self._lib.pgh_set_client_sharding(self._h, 1 if on else 0), "set_client_sharding")
+
+    def allgather_resident(self):
+        """All-gather the resident checkpoint into a full copy on every GPU; returns the device
+        pointers (GPU g holds shard r at [r * S, r * S + len_r))."""
+        ptrs = (C.c_void_p * len(self.devices))()
+        self._check(self._lib.pgh_group_allgather_resident(self._h, ptrs), "allgather_resident")
+        return [p or 0 for p in ptrs]
+
+    def group_backend(self) -> int:
+        """1: RCCL, 0: peer copies, -1: no collective yet (or a single GPU)."""
+        b = C.c_int(-1)
+        self._check(self._lib.pgh_group_backend(self._h, C.byref(b)), "group_backend")
+        return b.value
 
     def __del__(self):
         try:

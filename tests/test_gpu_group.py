@@ -1,0 +1,306 @@
+"""GPU: the multi-GPU group context (pgh_create_group) against the oracle and against one GPU.
+
+On the one-GPU box a group's children share device 0 ("devices=[0, 0]"): every shard, fan-out
+and peer-copy path of the group runs for real, and the RCCL path runs over a one-GPU group
+(ncclCommInitAll over [0]; a communicator cannot hold one device twice).  The 8-GPU node is the
+driver's.  Bar: bit-exact (fp32 folds included: every GPU folds every client of its shard in the
+reference's order).
+"""
+import ctypes as C
+import hashlib
+import json
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, ROOT
+from oracle import coracle
+from oracle import oracle as O
+from oracle.gen_golden import MNIST_SHAPES, mnist_inputs
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def group2():
+    from pygrid_amd import Engine
+
+    eng = Engine(devices=[0, 0])
+    yield eng
+    eng.close()
+
+
+@pytest.fixture(scope="module")
+def group3():
+    from pygrid_amd import Engine
+
+    eng = Engine(devices=[0, 0, 0])
+    yield eng
+    eng.close()
+
+
+@pytest.fixture(scope="module")
+def group1():
+    from pygrid_amd import Engine
+
+    eng = Engine(devices=[0])
+    yield eng
+    eng.close()
+
+
+def d2h(ptr: int, n: int, dtype=np.float32) -> np.ndarray:
+    """Read n values from device memory (torch already loaded the HIP runtime)."""
+    hip = C.CDLL("libamdhip64.so.7")
+    out = np.empty(n, dtype=dtype)
+    assert hip.hipMemcpy(C.c_void_p(out.ctypes.data), C.c_void_p(ptr), C.c_size_t(out.nbytes), 2) == 0
+    return out
+
+
+# ---- the plain-C binding, on the GPU --------------------------------------------------------------
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_plain_c_consumer_closes_mnist_on_the_gpu(tmp_path, devices):
+    """tests/c_abi_gpu_close.c: MNIST N=3 mean + iterative through the C ABI alone (single context
+    and groups), against the golden SHA-256 (oracle/gen_golden.py)."""
+    g = json.loads((GOLD / "mnist_synth.json").read_text())
+    diffs, ckpt = mnist_inputs(g["seed"], g["n_clients"])
+    numel = [int(np.prod(s)) for s in MNIST_SHAPES]
+    inp, outp, exe = tmp_path / "in.bin", tmp_path / "out.bin", tmp_path / "close"
+    with open(inp, "wb") as f:
+        f.write(np.array([len(numel), diffs.shape[0]], np.int32).tobytes())
+        f.write(np.array(numel, np.int64).tobytes())
+        f.write(np.ascontiguousarray(diffs, F).tobytes())
+        f.write(np.ascontiguousarray(ckpt, F).tobytes())
+    lib_dir = ROOT / "pygrid_amd"
+    subprocess.run(["gcc", "-std=c99", "-O2", "-Wall", "-Werror", "-I", str(ROOT / "include"),
+                    str(ROOT / "tests" / "c_abi_gpu_close.c"), "-L", str(lib_dir), "-lpygrid_hip",
+                    f"-Wl,-rpath,{lib_dir}", "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), str(inp), str(outp), str(len(devices)), *map(str, devices)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    assert r.stdout.startswith(f"ok gpus={len(devices)}")
+    out = np.fromfile(outp, dtype=F).reshape(2, -1)
+    assert sha(out[0]) == g["sha256_mean"]
+    assert sha(out[1]) == g["sha256_iter"]
+
+
+# ---- param shards: bit-identical to one GPU ----------------------------------------------------------
+
+def test_group_shape(group2, group3):
+    assert group2.n_gpus == 2 and group3.n_gpus == 3
+    with pytest.raises(Exception):
+        group2.child(2)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("P", [1000, 4_000_003, 64 * 3 + 5])
+def test_group_fedavg_matches_oracle(group3, mode, P):
+    rng = np.random.default_rng(300 + mode)
+    N = 7
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    w = rng.uniform(0.5, 2.0, N).astype(F)
+    group3.set_layout([P])
+    group3.reserve(N)
+    for k in range(N):
+        group3.ingest(k, d[k])
+    if mode == 2:
+        group3.set_weights(w)
+    got = group3.fedavg(mode, c)
+    assert np.array_equal(bits(got), bits(coracle.fedavg(mode, d, c, w if mode == 2 else None)))
+
+
+def test_group_state_bytes_cycles_match_single_gpu(group2, engine):
+    """CycleAggregator over a group: State bytes in, new checkpoint bytes out, three cycles chained
+    through the resident checkpoint -- byte-identical to the single-GPU engine."""
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.state_schema import build_state_fast
+
+    rng = np.random.default_rng(311)
+    shapes = [(96, 130), (130,), (7, 96), (7,)]
+    ck = build_state_fast([rng.standard_normal(s).astype(F) for s in shapes])
+    a1, a2 = CycleAggregator(engine), CycleAggregator(group2)
+    p1 = p2 = ck
+    for cyc in range(3):
+        diffs = [build_state_fast([(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes]) for _ in range(5)]
+        p1 = a1.average_plan_diffs({}, p1, diffs)
+        p2 = a2.average_plan_diffs({}, p2, diffs)
+        assert p1 == p2, cyc
+
+
+def test_group_subrange_and_stream(group2):
+    """set_shard on a group re-partitions the sub-range; STREAM folds through the ring per GPU."""
+    rng = np.random.default_rng(312)
+    P, N = 50_000, 9
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    group2.set_layout([P])
+    group2.set_shard(1000, 40_000)
+    group2.reserve(4)
+    group2.stream_begin(0, 2)
+    for k in range(N):
+        group2.ingest(k, d[k])
+    got = group2.stream_finish(c[1000:40_000])
+    want = coracle.fedavg(0, d, c)[1000:40_000]
+    assert np.array_equal(bits(got), bits(want))
+
+
+def test_group_report_time_cycle(group2):
+    """IncrementalCycle over a group: shuffled reports with dropouts, folded through the row table
+    on every GPU."""
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(313)
+    shapes = [(200, 41), (41,)]
+    n = 40
+    reporters = [w for w in range(n) if w != 0 and rng.random() >= 0.2]
+    diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in reporters}
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    ck_pb = build_state_fast(ckpt)
+    inc = IncrementalCycle(group2, [int(np.prod(s)) for s in shapes], slots=16, fold_batch=3, checkpoint=ck_pb)
+    for w in range(n):
+        inc.assigned(w)
+    for w in rng.permutation(reporters):
+        inc.reported(int(w), build_state_fast(diffs[int(w)]))
+    new = inc.close(ck_pb)
+    want = O.fedavg_mean(ckpt, [diffs[w] for w in sorted(reporters)])
+    for got, w in zip(parse_state(new), want):
+        assert np.array_equal(bits(got), bits(w))
+
+
+def test_group_allgather_resident_peer_copies(group2):
+    rng = np.random.default_rng(314)
+    P, N = 10_007, 3
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    group2.set_layout([P])
+    group2.reserve(N)
+    group2.ckpt_upload(c)
+    for k in range(N):
+        group2.ingest(k, d[k])
+    group2.fedavg_resident(0)
+    ptrs = group2.allgather_resident()
+    assert group2.group_backend() == 0  # two children on one device: peer copies
+    want = coracle.fedavg(0, d, c)
+    S = -(-(-(-P // 2)) // 64) * 64
+    for p in ptrs:
+        full = d2h(p, 2 * S)
+        got = np.concatenate([full[:S], full[S:S + P - S]])
+        assert np.array_equal(bits(got), bits(want))
+
+
+def test_group1_allgather_over_rccl(group1):
+    rng = np.random.default_rng(315)
+    P, N = 4_099, 4
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    group1.set_layout([P])
+    group1.reserve(N)
+    group1.ckpt_upload(c)
+    for k in range(N):
+        group1.ingest(k, d[k])
+    group1.fedavg_resident(1)
+    (p,) = group1.allgather_resident()
+    assert group1.group_backend() == 1  # ncclCommInitAll over [0]
+    assert np.array_equal(bits(d2h(p, P)), bits(coracle.fedavg(1, d, c)))
+
+
+# ---- secure aggregation: param shards and client shards ----------------------------------------------
+
+def _shares(seed, N, S, P):
+    idx = np.arange(P, dtype=np.uint64)
+    return np.stack([O.synth_shares(seed, k, S, idx) for k in range(N)])
+
+
+@pytest.mark.parametrize("client_shard", [False, True])
+@pytest.mark.parametrize("N", [1, 2, 7])
+def test_group_secagg(group3, client_shard, N):
+    P, S = 3_001, 2
+    sh = _shares(320 + N, N, S, P)
+    sh[0, 0, :5] = [2**63 - 1, -2**63, -1, 1, 0]  # wrap-heavy
+    group3.set_layout([P])
+    group3.set_client_sharding(client_shard)
+    group3.reserve(N, 1, S)
+    for k in range(N):
+        group3.ingest(k, sh[k])
+    s, dec = group3.secagg(10, 3)
+    ws = O.secagg_sum(sh)
+    assert np.array_equal(s, ws)
+    assert np.array_equal(bits(dec), bits(O.fix_prec_decode(ws)))
+    group3.set_client_sharding(False)
+
+
+def test_group_secagg_client_shard_from_share_state_bytes(group2):
+    """Each client's share messages go only to the GPU that owns the client (its own PCIe link),
+    decoded there; the reduce-scatter over peer copies makes the sums whole -- bit-exact."""
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.state_schema import build_state_i64_fast
+
+    N, S = 5, 2
+    numel = [700, 301]
+    P = sum(numel)
+    sh = _shares(330, N, S, P)
+    msgs = [[build_state_i64_fast(np.split(sh[k, p], [numel[0]])) for p in range(S)] for k in range(N)]
+    group2.set_client_sharding(True)
+    try:
+        s, dec = CycleAggregator(group2).secure_aggregate_states(numel, msgs)
+    finally:
+        group2.set_client_sharding(False)
+    ws = O.secagg_sum(sh)
+    assert np.array_equal(s, ws) and np.array_equal(bits(dec), bits(O.fix_prec_decode(ws)))
+
+
+def test_group1_client_sharded_secagg_over_rccl(group1):
+    N, S, P = 3, 2, 2_049
+    sh = _shares(340, N, S, P)
+    group1.set_layout([P])
+    group1.set_client_sharding(True)
+    try:
+        group1.reserve(N, 1, S)
+        group1.synth_fill(77, N)
+        s, dec = group1.secagg(10, 3)
+    finally:
+        group1.set_client_sharding(False)
+    idx = np.arange(P, dtype=np.uint64)
+    ws = O.secagg_sum(np.stack([O.synth_shares(77, k, S, idx) for k in range(N)]))
+    assert group1.group_backend() == 1
+    assert np.array_equal(s, ws) and np.array_equal(bits(dec), bits(O.fix_prec_decode(ws)))
+
+
+def test_group_client_sharded_synth_matches_oracle(group3):
+    """Synthetic clients of a client-sharded group are generated under their GLOBAL index."""
+    N, S, P = 8, 2, 1_500
+    group3.set_layout([P])
+    group3.set_client_sharding(True)
+    try:
+        group3.reserve(N, 1, S)
+        group3.synth_fill(91, N)
+        s, _ = group3.secagg(10, 3)
+    finally:
+        group3.set_client_sharding(False)
+    idx = np.arange(P, dtype=np.uint64)
+    assert np.array_equal(s, O.secagg_sum(np.stack([O.synth_shares(91, k, S, idx) for k in range(N)])))
+
+
+def test_device_pointer_calls_refused_on_a_group(group2):
+    from pygrid_amd.exceptions import AggregationError
+
+    group2.set_layout([1000])
+    group2.reserve(2)
+    with pytest.raises(AggregationError, match="UNSUPPORTED"):
+        group2.fedavg_device(0, 16, 16)
+    with pytest.raises(AggregationError, match="UNSUPPORTED"):
+        group2.slab()
+    kid = group2.child(1)
+    assert kid.slab()[0] != 0  # the child context owns a real slab
