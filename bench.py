@@ -88,6 +88,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-e2e", action="store_true",
                     help="resident config-2 lines: skip the bytes -> bytes end-to-end close measured beside them")
+    ap.add_argument("--group", action="store_true",
+                    help="one process drives all --gpus GPUs through one library context (pgh_create_group: "
+                         "how the node's single process uses the node's GPUs) instead of one rank per GPU")
+    ap.add_argument("--e2e-distinct", type=int, default=64,
+                    help="end-to-end close: distinct client State messages in host memory (re-sent as the others)")
     ap.add_argument("--dry-run", action="store_true",
                     help="form the world (gloo, no GPU), print the world size on rank 0 and exit")
     return ap.parse_args()
@@ -314,7 +319,11 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world != args.gpus:
+        self.group = args.group
+        self.n_gpus = args.gpus if args.group else self.world  # GPUs measured (whole job)
+        if self.group and self.world != 1:
+            raise SystemExit("bench.py --group drives every GPU from one process: launch it once")
+        if not self.group and self.world != args.gpus:
             # main() spawns the ranks itself when no launcher did; a launcher with another world
             # size would measure a different configuration than the one named
             raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher formed WORLD_SIZE {self.world}")
@@ -379,12 +388,12 @@ def record(ctx, args, name, value, el, dt, config, roofline, extra=None, step_is
     fold of HBM-resident diffs, plus the collective at N > 1) -> `kernel_ms`; "close" (bytes in ->
     bytes out: the whole _average_plan_diffs slice) -> `cycle_close_ms`."""
     rec = {
-        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": ctx.world,
+        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": ctx.n_gpus,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dt,
         "data": DATA_HOST if name in HOST_DATA_WORKLOADS else DATA_DEVICE,
         "config": config,
-        "pct_hbm_peak_per_gpu": round(100 * value / ctx.world / HBM_PEAK_GBS, 2),
+        "pct_hbm_peak_per_gpu": round(100 * value / ctx.n_gpus / HBM_PEAK_GBS, 2),
         ("kernel_ms" if step_is == "kernel" else "cycle_close_ms"): round(el / args.steps * 1e3, 4),
         "roofline": roofline, "cpu_baseline": None,
     }
@@ -393,10 +402,12 @@ def record(ctx, args, name, value, el, dt, config, roofline, extra=None, step_is
     return rec
 
 
-def roofline_of(st, workload, variant, kernel):
+def roofline_of(st, workload, variant, kernel, n_gpus=1):
+    """Dominant kernel against one GPU's HBM peak.  A group's stats sum the bytes of its GPUs and
+    take the slowest GPU's times (they run concurrently): bytes are divided by n_gpus here."""
     n = max(st["kernel_launches"], 1)
     ms = st["kernel_ms_total"] / n
-    alg = st["kernel_bytes_total"] / n
+    alg = st["kernel_bytes_total"] / n / n_gpus
     # Launches on two streams (param ranges at N > 1) overlap; each one's event span then includes
     # time shared with its neighbour, so the duration per launch is the busy time (the union of
     # the launch intervals) divided by the launches.  Without overlap the two are equal.
@@ -821,15 +832,176 @@ def run_resnet18_report(ctx, args, eng, N):
     return rec
 
 
+def state_messages(shapes, n_distinct: int, seed: int):
+    """Checkpoint + n_distinct client diffs as State bytes (distinct payloads, so a close of many
+    clients streams from host DRAM rather than from cache): one seeded base vector, the diffs
+    are rolled copies of it written into the template's payload spans by the C++ patcher."""
+    import numpy as np
+
+    from pygrid_amd.state import serialize_model_params
+    from pygrid_amd.state_schema import build_state_fast
+
+    rng = np.random.default_rng(seed)
+    P = sum(int(np.prod(s)) for s in shapes)
+    ck_pb = build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in shapes])
+    base = rng.standard_normal(P, dtype=np.float32) * np.float32(1e-2)
+    diffs = [serialize_model_params(ck_pb, np.roll(base, 9973 * k)) for k in range(n_distinct)]
+    return ck_pb, diffs
+
+
+def e2e_close(ctx, args, eng, n_clients: int, steps: int = 2):
+    """BASELINE.md's cycle close, end to end: n_clients ResNet-18 diffs as State bytes in host
+    memory -> new checkpoint bytes through CycleAggregator.average_plan_diffs (the slice
+    cycle_manager.py:240-303: checkpoint upload, every diff's payload -> HBM over PCIe, fused
+    mean/apply, HBM -> host, State patch).  Wall time per close, 1 warm-up close first."""
+    import numpy as np
+
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.workloads import RESNET18_SHAPES
+
+    ck_pb, distinct = state_messages(RESNET18_SHAPES, min(args.e2e_distinct, n_clients), args.seed)
+    diffs = [distinct[k % len(distinct)] for k in range(n_clients)]
+    agg = CycleAggregator(eng)
+    agg.average_plan_diffs({}, ck_pb, diffs)
+    eng.reset_stats()
+    t = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        new = agg.average_plan_diffs({}, ck_pb, diffs)
+        t.append(time.perf_counter() - t0)
+    st = eng.stats()
+    ms = float(np.median(t)) * 1e3
+    return {"cycle_close_ms": round(ms, 2), "closes_ms": [round(x * 1e3, 2) for x in t], "clients": n_clients,
+            "client_diff_GBps": round(4 * RESNET18_P * n_clients / (ms / 1e3) / 1e9, 2),
+            "h2d_GBps_per_gpu": round(st["h2d_bytes_total"] / max(ctx.n_gpus, 1) / (st["h2d_ms_total"] / 1e3) / 1e9, 2)
+            if st["h2d_ms_total"] else None,
+            "fold_kernel_ms": round(st["kernel_ms_total"] / max(st["kernel_launches"], 1), 3),
+            "new_checkpoint_bytes": len(new), "distinct_messages_in_host_memory": len(distinct),
+            "gpus": ctx.n_gpus,
+            "definition": "wall time of CycleAggregator.average_plan_diffs: ResNet-18 checkpoint + client diffs as "
+                          "State bytes in host memory -> new checkpoint bytes (BASELINE.md cycle close; PCIe-inclusive)"}
+
+
+def run_group_resident(ctx, args, eng, mode, dtype, N, parties, Pg):
+    """The resident configs on a one-process group: GPU g folds its Pg-param shard of a
+    (G x Pg)-param model over all N clients (weak scaling like the per-rank runs), then the new
+    checkpoint is all-gathered into a full copy on every GPU (ncclAllGather); secagg writes the
+    decoded sum into a page-locked host array slice by slice."""
+    import numpy as np
+
+    from pygrid_amd import PinnedBuffer
+
+    G = ctx.n_gpus
+    P = Pg * G
+    eng.set_layout([P])
+    eng.reserve(N, dtype, parties)
+    eng.synth_fill(args.seed, N)
+    bufs = []
+    if dtype == 0:
+        eng.ckpt_upload(np.full(P, 0.01, np.float32))
+        if mode == 2:
+            eng.set_weights([(c % 7 + 1) * 0.5 for c in range(N)])
+
+        def step():
+            eng.fedavg_resident(mode)
+            eng.allgather_resident()
+        diff_bytes, dt, kernel = 4 * N * P, "f32", "k_fedavg"
+    else:
+        bufs = [PinnedBuffer((P,), np.int64), PinnedBuffer((P,), np.float32)]
+
+        def step():
+            eng.secagg(10, 3, out_sum=bufs[0].array, out_dec=bufs[1].array)
+        diff_bytes, dt, kernel = 8 * parties * N * P, "int64", "k_secagg"
+    el, st = timed(ctx, step, args.steps, args.warmup, eng)
+    value = diff_bytes * args.steps / el / 1e9
+    cfg = {"workload": f"{args.workload}: P_shard={Pg} params/GPU x {N} clients"
+                       + (f" x {parties} parties int64" if dtype == 1 else " fp32") + ", resident in HBM",
+           "clients": N, "params_per_gpu": Pg, "params_total": P,
+           "parallelism": f"param-shard{G} in one process (pgh_create_group, one host thread per GPU)" + (
+               " + ncclAllGather of the new checkpoint" if dtype == 0 else " + host slices"),
+           "rccl": eng.group_backend() == 1, "kernel_variant": eng.effective_variant(mode if dtype == 0 else 16)}
+    rec = record(ctx, args, args.workload, value, el, dt, cfg,
+                 roofline_of(st, args.workload, cfg["kernel_variant"], kernel, G))
+    for b in bufs:
+        b.free()
+    return rec
+
+
+def run_group_secagg_clients(ctx, args, eng, N, S, P):
+    """Config 3 client-sharded on a one-process group: GPU g holds its own N clients x S parties
+    over the whole model, the Z_2^64 sums are reduce-scattered (ncclReduceScatter, uint64 SUM), GPU
+    g decodes its slice and writes it into the page-locked host outputs."""
+    import numpy as np
+
+    from pygrid_amd import PinnedBuffer
+
+    G = ctx.n_gpus
+    eng.set_layout([P])
+    eng.set_client_sharding(True)
+    eng.reserve(N * G, 1, S)
+    eng.synth_fill(args.seed, N * G)
+    bufs = [PinnedBuffer((P,), np.int64), PinnedBuffer((P,), np.float32)]
+
+    def step():
+        eng.secagg(10, 3, out_sum=bufs[0].array, out_dec=bufs[1].array)
+    el, st = timed(ctx, step, args.steps, args.warmup, eng)
+    value = 8 * S * N * G * P * args.steps / el / 1e9
+    cfg = {"workload": f"secagg-clients: {N} clients/GPU x {S} parties int64 x P={P} (ResNet-18), clients sharded "
+                       "over the GPUs of one process, resident in HBM",
+           "clients": N * G, "clients_per_gpu": N, "params_per_gpu": P, "params_total": P,
+           "parallelism": f"client-shard{G} in one process (pgh_create_group) + ncclReduceScatter of the Z_2^64 sums "
+                          "+ per-GPU decode + host slices",
+           "rccl": eng.group_backend() == 1, "kernel_variant": eng.effective_variant(16)}
+    rec = record(ctx, args, "secagg-clients", value, el, "int64", cfg,
+                 roofline_of(st, "secagg-clients", cfg["kernel_variant"], "k_secagg", G))
+    for b in bufs:
+        b.free()
+    return rec
+
+
+def main_group(ctx, args):
+    from pygrid_amd import Engine
+
+    mode, dtype, n_default, parties, pg_default = WORKLOADS[args.workload]
+    N = args.clients or n_default
+    Pg = args.params or pg_default
+    # PGH_BENCH_DEVICES (e.g. "0,0") only exists to rehearse a group on a one-GPU box
+    devs = os.environ.get("PGH_BENCH_DEVICES")
+    devices = [int(x) for x in devs.split(",")] if devs else list(range(args.gpus))
+    if len(devices) != args.gpus:
+        raise SystemExit(f"PGH_BENCH_DEVICES names {len(devices)} devices, --gpus {args.gpus}")
+    eng = Engine(devices=devices)
+    if args.variant is not None:
+        eng.set_variant(args.variant)
+    if args.workload == "secagg-clients":
+        rec = run_group_secagg_clients(ctx, args, eng, N, parties, Pg)
+    elif args.workload in ("resnet18-state", "mnist-state", "resnet18-report"):
+        rec = {"resnet18-state": run_resnet18_state, "mnist-state": lambda c, a, e, n: run_mnist_state(c, a, e),
+               "resnet18-report": run_resnet18_report}[args.workload](ctx, args, eng, N)
+        rec["config"]["parallelism"] = f"param-shard{ctx.n_gpus} in one process (pgh_create_group)"
+    elif args.workload in ("c4-stream", "c5-ingest"):
+        raise SystemExit(f"--group: {args.workload} runs per rank (torch.distributed.run)")
+    else:
+        rec = run_group_resident(ctx, args, eng, mode, dtype, N, parties, Pg)
+        if args.workload == "resnet18-fedavg" and not args.no_e2e:
+            rec["cycle_close_e2e"] = e2e_close(ctx, args, eng, N)
+    print(json.dumps(rec), flush=True)
+    eng.close()
+
+
 def main():
     args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.group:
         sys.exit(spawn_ranks(args))  # no launcher: form the N-rank world here (no GPU touched yet)
     ctx = Ctx(args)
     if args.dry_run:
         if ctx.rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": ctx.world, "backend": ctx.backend}), flush=True)
+            print(json.dumps({"dry_run": True, "n_gpus": ctx.n_gpus, "backend": ctx.backend,
+                              "group": ctx.group}), flush=True)
         ctx.close()
+        return
+    if ctx.group:
+        main_group(ctx, args)
         return
     from pygrid_amd import Engine
     from pygrid_amd.sharding import shard_bounds
@@ -860,6 +1032,9 @@ def main():
         rec = run_resnet18_secagg_state(ctx, args, eng, N, parties)
     else:
         rec = run_resident(ctx, args, eng, mode, dtype, N, parties, hi - lo, P, lo, hi)
+        if args.workload == "resnet18-fedavg" and ctx.world == 1 and not args.no_e2e:
+            # the bytes -> bytes close of the same config (BASELINE.md cycle close), beside the kernel line
+            rec["cycle_close_e2e"] = e2e_close(ctx, args, eng, N)
     if ctx.rank == 0:
         print(json.dumps(rec), flush=True)
     eng.close()

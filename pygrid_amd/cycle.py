@@ -83,10 +83,14 @@ def select_mode(server_config: dict, avg_plan: Optional[Callable] = None, weight
 
 
 class CycleAggregator:
-    """Owns one Engine (one GPU) across cycles; the slab is re-used while it fits."""
+    """Owns one Engine across cycles; the slab is re-used while it fits.  ``devices=[0, ..., 7]``
+    gives the node's single process every GPU of the node (``pgh_create_group``: parameter shards,
+    each GPU's slice of every diff over its own PCIe link, bit-identical results)."""
 
-    def __init__(self, engine: Optional[Engine] = None, device: int = 0):
-        self.engine = engine if engine is not None else Engine(device)
+    def __init__(self, engine: Optional[Engine] = None, device: int = 0, devices: Optional[Sequence[int]] = None):
+        if engine is None:
+            engine = Engine(devices=devices) if devices is not None else Engine(device)
+        self.engine = engine
         self._numel: tuple = ()
         self._cap = 0
         self._dtype = None

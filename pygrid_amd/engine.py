@@ -310,10 +310,16 @@ class Engine:
         self._check(self._lib.pgh_ckpt_patch_state(self._h, template, len(template), ptr), "ckpt_patch_state")
         return out
 
-    def secagg(self, base: int = 10, prec: int = 3, want_sum: bool = True,
-               want_dec: bool = True) -> Tuple[Optional[np.ndarray], Optional[np.ndarray]]:
-        s = np.empty(self.p_shard, dtype=np.int64) if want_sum else None
-        d = np.empty(self.p_shard, dtype=np.float32) if want_dec else None
+    def secagg(self, base: int = 10, prec: int = 3, want_sum: bool = True, want_dec: bool = True,
+               out_sum: Optional[np.ndarray] = None,
+               out_dec: Optional[np.ndarray] = None) -> Tuple[Optional[np.ndarray], Optional[np.ndarray]]:
+        """Z_2^64 share sum + decode into host arrays (fresh ones, or ``out_sum`` / ``out_dec``, e.g.
+        page-locked PinnedBuffer arrays that the result is DMA'd into directly)."""
+        s = out_sum if out_sum is not None else (np.empty(self.p_shard, dtype=np.int64) if want_sum else None)
+        d = out_dec if out_dec is not None else (np.empty(self.p_shard, dtype=np.float32) if want_dec else None)
+        for a, dt in ((s, np.int64), (d, np.float32)):
+            if a is not None and (a.dtype != dt or a.size != self.p_shard or not a.flags.c_contiguous):
+                raise AggregationError(f"secagg output must be a contiguous {np.dtype(dt).name}[{self.p_shard}]")
         self._check(self._lib.pgh_secagg(self._h, int(base), int(prec), _ptr(s) if s is not None else None,
                                          _ptr(d) if d is not None else None), "secagg")
         return s, d

@@ -29,7 +29,7 @@ def test_plain_bench_forms_two_ranks():
     r = _run(["--gpus", "2", "--dry-run"])
     assert r.returncode == 0, r.stderr
     rec = _json_line(r.stdout)
-    assert rec == {"dry_run": True, "n_gpus": 2, "backend": "gloo"}
+    assert rec == {"dry_run": True, "n_gpus": 2, "backend": "gloo", "group": False}
 
 
 def test_plain_bench_forms_three_ranks():
@@ -69,3 +69,9 @@ def test_usable_cores_reports_a_positive_count():
     n, how = bench.usable_cores()
     assert n >= 1 and n <= len(os.sched_getaffinity(0))
     assert how in ("sched_getaffinity", "cgroup cpu quota")
+
+
+def test_group_mode_is_one_process_over_n_gpus():
+    r = _run(["--gpus", "4", "--group", "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    assert _json_line(r.stdout) == {"dry_run": True, "n_gpus": 4, "backend": "gloo", "group": True}
