@@ -1683,12 +1683,11 @@ int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out
         c->pool_copy->run({CopyPool::Seg{out, tmpl, n}});
         gaps.clear();
     }
-    // the framing copy (and the pre-fault of a small fresh output) runs while the first slot's DMA flies
+    // the framing copy and the pre-fault of the output run while the first slot's DMA flies (in
+    // place, out == tmpl, is how a freshly framed checkpoint is filled: its pages are fresh too)
     RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, pieces, c->stream, [&] {
-        if (out != tmpl) {
-            if (c->prefault) prefault_parallel(out, n, *c->pool_copy);
-            else prefault_small(out, n);
-        }
+        if (c->prefault) prefault_parallel(out, n, *c->pool_copy);
+        else prefault_small(out, n);
         if (!gaps.empty()) c->pool_copy->run(gaps);
     }));
     return collect_timings(c);
@@ -2080,7 +2079,7 @@ int patch_payloads(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out) {
     for (auto& sp : spans) pieces.push_back(OutPiece{out + sp.first, sp.second});
     RC(order_after_ingest(c, c->stream));
     RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, pieces, c->stream, [&] {
-        if (out != tmpl && c->prefault && !spans.empty()) {  // this shard's part of the fresh output
+        if (c->prefault && !spans.empty()) {  // this shard's part of the (fresh) output
             const size_t a = spans.front().first, b = spans.back().first + spans.back().second;
             if (b > a) prefault_parallel(out + a, b - a, *c->pool_copy);
         }

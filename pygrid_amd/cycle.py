@@ -7,7 +7,8 @@ Reference: ``CycleManager.complete_cycle`` / ``_average_plan_diffs``,
 * ``select_mode`` is the dispatch rule: no hosted plan -> hard-coded mean
   (``:273-288``); hosted plan + ``iterative_plan`` whose behaviour is the canonical
   ``(avg * num + item) / (num + 1)`` (``01-Create-plan.ipynb:450-454``) -> iterative mean
-  (``:266-269``); anything else (a user-defined non-iterative plan, ``:270-271``) raises
+  (``:266-269``); a hosted non-iterative plan (``:270-271``) whose output is bit-identical to
+  ``reduce(th.add) / N`` on probe inputs -> the hard-coded mean; anything else raises
   ``PlanNotAcceleratedError`` so the node keeps running the reference code for it.
 * ``CycleAggregator.average_plan_diffs`` replaces the slice ``:240-303``: checkpoint bytes +
   diff bytes in, new checkpoint bytes out.  DB reads/writes and cycle bookkeeping stay with
@@ -70,13 +71,68 @@ def is_canonical_iterative_plan(avg_plan: Callable) -> bool:
     return True
 
 
+def _mean_probes():
+    """Probe inputs for a non-iterative plan: several client counts, values of mixed magnitude (so a
+    re-associated or pairwise sum rounds differently), exact cancellations, signed zeros,
+    subnormals and an overflow to inf."""
+    rng = np.random.default_rng(11)
+    probes = []
+    for n in (1, 2, 3, 7, 33):
+        diffs = []
+        for c in range(n):
+            mixed = (rng.standard_normal(97) * 10.0 ** rng.integers(-4, 5, 97)).astype(np.float32)
+            special = np.array([-0.0, 3.0e-39 * (c + 1), 1e8 if c % 2 else -1e8, 1.0, 3.0e38, -1e-45],
+                               np.float32)
+            diffs.append([mixed, special])
+        probes.append(diffs)
+    return probes
+
+
+def _reference_mean(diffs):
+    """cycle_manager.py:276-288 on the probe: left fold with th.add, then th.div by the python int N."""
+    import torch as th
+    from functools import reduce
+
+    cols = [[th.from_numpy(d[j].copy()) for d in diffs] for j in range(len(diffs[0]))]
+    return [th.div(reduce(th.add, col), len(diffs)).numpy() for col in cols]
+
+
+def is_mean_plan(avg_plan: Callable) -> bool:
+    """A hosted NON-iterative avg plan (called as ``avg_plan(diffs)``, cycle_manager.py:270-271) is
+    user code; it maps to the hard-coded mean only if, on every probe, its output equals
+    ``reduce(th.add) / N`` (:286-288) bit for bit (NaN-free probes; signed zeros, subnormals and
+    infinities compared exactly).  Anything else -- another order of summation, a mean through a
+    pairwise reduction, a weighting, an exception -- leaves the plan to the node."""
+    import torch as th
+
+    for diffs in _mean_probes():
+        try:
+            res = avg_plan([[th.from_numpy(t.copy()) for t in d] for d in diffs])
+            res = list(res)
+        except Exception as e:  # noqa: BLE001 -- any failure means "not the plain mean"
+            logging.info("avg plan probe failed: %s", e)
+            return False
+        want = _reference_mean(diffs)
+        if len(res) != len(want):
+            return False
+        for got, w in zip(res, want):
+            if not hasattr(got, "detach") or got.dtype != th.float32:
+                return False
+            got = got.detach().cpu().numpy()
+            if got.shape != w.shape or not np.array_equal(got.view(np.uint32), w.view(np.uint32)):
+                return False
+    return True
+
+
 def select_mode(server_config: dict, avg_plan: Optional[Callable] = None, weights=None) -> int:
     if weights is not None:
         return WEIGHTED_MEAN
     if avg_plan is None:
         return MEAN  # "Fallback to simple hardcoded avg plan", cycle_manager.py:274
     if not server_config.get("iterative_plan", False):
-        raise PlanNotAcceleratedError("non-iterative hosted avg plan is user-defined (cycle_manager.py:270-271)")
+        if is_mean_plan(avg_plan):  # :270-271 with a plan that IS the hard-coded mean
+            return MEAN
+        raise PlanNotAcceleratedError("non-iterative hosted avg plan is not reduce(th.add) / N (cycle_manager.py:270-271)")
     if not is_canonical_iterative_plan(avg_plan):
         raise PlanNotAcceleratedError("iterative avg plan is not (avg * num + item) / (num + 1)")
     return ITERATIVE_MEAN
@@ -113,7 +169,13 @@ class CycleAggregator:
 
     # ---- bytes in / bytes out: the replaceable slice cycle_manager.py:240-303 -------------------
     def average_plan_diffs(self, server_config: dict, checkpoint: bytes, diffs: Sequence[bytes],
-                           avg_plan: Optional[Callable] = None, weights=None) -> bytes:
+                           avg_plan: Optional[Callable] = None, weights=None, framing: str = "fresh") -> bytes:
+        """New checkpoint bytes.  ``framing="fresh"`` (default) frames them like the reference's
+        ``serialize_model_params`` (model_manager.py:82-90: new placeholder / tensor ids, plain
+        torch_tensor entries, no tags); ``"template"`` keeps the old checkpoint's framing byte for
+        byte and only replaces the payloads (ids and tags survive)."""
+        if framing not in ("fresh", "template"):
+            raise AggregationError(f"unknown checkpoint framing {framing!r}")
         if len(diffs) == 0:
             raise AggregationError("no diffs to average")
         mode = select_mode(server_config, avg_plan, weights)
@@ -130,7 +192,8 @@ class CycleAggregator:
         self.engine.ckpt_owner = None
         self._resident = None
         self.engine.fedavg_resident(mode)  # :252-296
-        new = self.engine.ckpt_patch_state(checkpoint)  # :303
+        new = (state_codec.fresh_checkpoint(self.engine, checkpoint) if framing == "fresh"  # :303
+               else self.engine.ckpt_patch_state(checkpoint))
         self.engine.ckpt_owner = self
         self._resident = new
         return new

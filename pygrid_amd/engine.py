@@ -310,6 +310,12 @@ class Engine:
         self._check(self._lib.pgh_ckpt_patch_state(self._h, template, len(template), ptr), "ckpt_patch_state")
         return out
 
+    def ckpt_patch_into(self, ptr: int, n: int):
+        """Patch in place: the n bytes at host address ``ptr`` hold a State whose framing is final;
+        its payload slices are written from the resident checkpoint (``state.fresh_checkpoint``)."""
+        self._check(self._lib.pgh_ckpt_patch_state(self._h, C.c_char_p(ptr), n, C.c_void_p(ptr)),
+                    "ckpt_patch_state (in place)")
+
     def secagg(self, base: int = 10, prec: int = 3, want_sum: bool = True, want_dec: bool = True,
                out_sum: Optional[np.ndarray] = None,
                out_dec: Optional[np.ndarray] = None) -> Tuple[Optional[np.ndarray], Optional[np.ndarray]]:

@@ -157,8 +157,9 @@ class IncrementalCycle:
             if not final and len(self._ready) >= self.fold_batch:
                 self._fold_ready(final=False)
 
-    def close(self, checkpoint: bytes) -> bytes:
-        """New checkpoint bytes (``cycle_manager.py:293-303``)."""
+    def close(self, checkpoint: bytes, framing: str = "fresh") -> bytes:
+        """New checkpoint bytes (``cycle_manager.py:293-303``), framed like ``serialize_model_params``
+        (``framing="fresh"``) or as the old checkpoint (``"template"``; see CycleAggregator)."""
         with self._lock:
             if self._closed:
                 raise AggregationError("cycle already closed")
@@ -173,7 +174,8 @@ class IncrementalCycle:
             self.engine.ckpt_owner = None
             self._ckpt = None
             self._fold_ready(final=True)
-            new = self.engine.ckpt_patch_state(checkpoint)
+            new = (state_codec.fresh_checkpoint(self.engine, checkpoint) if framing == "fresh"
+                   else self.engine.ckpt_patch_state(checkpoint))
             self.engine.ckpt_owner = self
             return new
 

@@ -6,9 +6,11 @@ The byte work is done in C++ (``pgh_state_scan`` / ``pgh_state_patch`` in libpyg
 
 * unserialize = locate each tensor's packed float32 payload and view it (no per-element
   Python work, unlike syft's ``_unbufferize``);
-* serialize of the new checkpoint = the current checkpoint's bytes with every payload
-  overwritten (``cycle_manager.py:303`` re-serializes the same tensor list, so shapes,
-  order and message layout are unchanged; ids/tags keep their previous values).
+* serialize of the new checkpoint = a FRESH State, framed like ``serialize_model_params``
+  (``model_manager.py:82-90``: new placeholder and tensor ids from syft's id space, plain
+  ``torch_tensor`` entries, no tags), its float payloads written straight from HBM
+  (``fresh_checkpoint``); or, on request, the current checkpoint's bytes with every payload
+  overwritten (``serialize_model_params`` below / ``pgh_ckpt_patch_state``: ids and tags kept).
 
 Schema: build-owned restatement of syft-proto 0.5.2 (``state_schema.py``); parity unpinned
 until checked against real client bytes (DESIGN.md "State codec").
@@ -85,3 +87,39 @@ def serialize_model_params(template: bytes, values: np.ndarray) -> bytes:
         raise StateParseError(f"cannot patch State ({_lib.STATUS_NAMES.get(rc, rc)}): "
                               f"{v.size} values for this checkpoint?", status=rc)
     return out
+
+
+def fresh_checkpoint(engine, template: bytes, ids=None) -> bytes:
+    """The new checkpoint as ``serialize_model_params`` emits it (model_manager.py:79-92): a fresh
+    State whose framing is built here from the template's tensor shapes and fresh ids
+    (``state_schema.fresh_frame``) and whose payloads the engine writes in place from the resident
+    checkpoint in HBM (``pgh_ckpt_patch_state`` with out == tmpl)."""
+    from . import state_schema
+
+    shapes = state_schema.tensor_shapes(template)
+    ids = list(ids) if ids is not None else state_schema.syft_ids(2 * len(shapes))
+    total, pieces, _ = state_schema.fresh_frame(shapes, ids)
+    out, ptr = _lib.fresh_bytes(total)
+    for off, b in pieces:  # framing; the payload bytes are all written by the engine below
+        C.memmove(ptr + off, b, len(b))
+    engine.ckpt_patch_into(ptr, total)
+    return out
+
+
+def serialize_fresh(shapes, values: np.ndarray, ids=None) -> bytes:
+    """Host-only fresh State of float32 ``values`` (P floats) with ``shapes`` (no GPU involved)."""
+    from . import state_schema
+
+    v = np.ascontiguousarray(values, dtype="<f4").reshape(-1)
+    ids = list(ids) if ids is not None else state_schema.syft_ids(2 * len(shapes))
+    total, pieces, spans = state_schema.fresh_frame(shapes, ids)
+    buf = bytearray(total)
+    for off, b in pieces:
+        buf[off:off + len(b)] = b
+    at = 0
+    for off, n in spans:
+        buf[off:off + n] = v[at:at + n // 4].tobytes()
+        at += n // 4
+    if at != v.size:
+        raise StateParseError(f"{v.size} values for tensors of {at} floats")
+    return bytes(buf)

@@ -251,3 +251,128 @@ def build_state_fast(tensors, ids=None) -> bytes:
               + _field(4, 2, td))
         parts.append(_field(2, 2, _field(1, 2, tt)))
     return b"".join(parts)
+
+
+# ---- fresh checkpoint framing (serialize_model_params, model_manager.py:79-92) ----------------------
+
+def _read_varint(b, i: int):
+    x, shift = 0, 0
+    while True:
+        if i >= len(b):
+            raise ValueError("truncated varint")
+        c = b[i]
+        i += 1
+        x |= (c & 0x7F) << shift
+        if not c & 0x80:
+            return x, i
+        shift += 7
+        if shift > 63:
+            raise ValueError("varint longer than 10 bytes")
+
+
+def _fields(b, a: int, z: int):
+    """(field number, wire type, value-or-(start, end)) of the message bytes b[a:z], payloads skipped
+    by length (nothing is decoded)."""
+    i = a
+    while i < z:
+        key, i = _read_varint(b, i)
+        num, wt = key >> 3, key & 7
+        if wt == 0:
+            v, i = _read_varint(b, i)
+            yield num, wt, v
+        elif wt == 2:
+            n, i = _read_varint(b, i)
+            if i + n > z:
+                raise ValueError("length-delimited field runs past its message")
+            yield num, wt, (i, i + n)
+            i += n
+        elif wt == 5:
+            i += 4
+            yield num, wt, None
+        elif wt == 1:
+            i += 8
+            yield num, wt, None
+        else:
+            raise ValueError(f"unsupported wire type {wt}")
+    if i != z:
+        raise ValueError("message overruns its bytes")
+
+
+def tensor_shapes(pb: bytes):
+    """Shape of every tensor of a State message, State order, from the framing alone (the float
+    payloads are skipped, not parsed): the shapes the new checkpoint keeps (cycle_manager.py:293-296
+    subtracts elementwise)."""
+    b = memoryview(pb)
+    shapes = []
+    for num, wt, v in _fields(b, 0, len(b)):
+        if num != 2 or wt != 2:  # State.tensors
+            continue
+        tt = None
+        for n2, w2, v2 in _fields(b, *v):
+            if n2 == 1 and w2 == 2:  # StateTensor.torch_tensor
+                tt = v2
+            elif n2 == 2 and w2 == 2:  # StateTensor.torch_param -> Parameter.tensor
+                for n3, w3, v3 in _fields(b, *v2):
+                    if n3 == 2 and w3 == 2:
+                        tt = v3
+        dims = []
+        if tt is not None:
+            for n3, w3, v3 in _fields(b, *tt):
+                if n3 == 4 and w3 == 2:  # TorchTensor.contents_data -> TensorData.shape -> Size.dims
+                    for n4, w4, v4 in _fields(b, *v3):
+                        if n4 == 1 and w4 == 2:
+                            for n5, w5, v5 in _fields(b, *v4):
+                                if n5 == 1 and w5 == 0:
+                                    dims.append(v5)
+                                elif n5 == 1 and w5 == 2:  # packed int32
+                                    i, z = v5
+                                    while i < z:
+                                        d, i = _read_varint(b, i)
+                                        dims.append(d)
+        shapes.append(tuple(int(d) for d in dims))
+    return shapes
+
+
+def syft_ids(n: int, rng=None):
+    """n fresh object ids from syft 0.2.9's id space (random ints below 10e10,
+    ``create_random_id``), as PlaceHolder().instantiate(...) and new tensors get them."""
+    import random
+
+    r = rng or random.SystemRandom()
+    return [int(10e10 * r.random()) for _ in range(n)]
+
+
+def fresh_frame(shapes, ids):
+    """Framing of ``State(state_placeholders=[PlaceHolder().instantiate(p) for p in params])`` for
+    float32 params of ``shapes`` (model_manager.py:82-90): per param a placeholder {id} (no tags) and a
+    StateTensor.torch_tensor {id, serializer, contents_data {shape, dtype "float32",
+    contents_float32}} -- plain tensors, as the reference's ``model_param - diff_param`` are.
+    ``ids`` holds 2 per param (placeholder, tensor).  Every float payload is the last field of its
+    tensor entry, so the message is: placeholders, then per tensor (prefix bytes, payload).
+    Returns (total bytes, [(offset, prefix bytes)], [(payload offset, payload bytes)])."""
+    pieces, spans = [], []
+    head = b"".join(_field(1, 2, _field(1, 2, _field(2, 0, value=ids[2 * k]) if ids[2 * k] else b""))
+                    for k in range(len(shapes)))
+    pieces.append((0, head))
+    pos = len(head)
+    for k, shape in enumerate(shapes):
+        n = 1
+        for d in shape:
+            n *= int(d)
+        payload = 4 * n
+        dims = b"".join(_varint(int(d)) for d in shape)
+        tid = ids[2 * k + 1]
+        td_head = _field(1, 2, _field(1, 2, dims) if dims else b"") + _field(2, 2, b"float32")
+        td_pay = (_varint((12 << 3) | 2) + _varint(payload)) if n else b""
+        td_len = len(td_head) + len(td_pay) + (payload if n else 0)
+        tt_head = (_field(1, 2, _field(2, 0, value=tid) if tid else b"") + _field(2, 0, value=SERIALIZER_ALL)
+                   + _varint((4 << 3) | 2) + _varint(td_len))
+        tt_len = len(tt_head) + td_len
+        st_head = _varint((1 << 3) | 2) + _varint(tt_len)
+        st_len = len(st_head) + tt_len
+        prefix = _varint((2 << 3) | 2) + _varint(st_len) + st_head + tt_head + td_head + td_pay
+        pieces.append((pos, prefix))
+        pos += len(prefix)
+        spans.append((pos, payload if n else 0))
+        pos += payload if n else 0
+    return pos, pieces, spans

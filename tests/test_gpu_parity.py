@@ -338,11 +338,54 @@ def test_state_bytes_roundtrip(engine):
     ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
     diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for _ in range(3)]
     agg = CycleAggregator(engine)
-    ck_pb = build_state(ckpt)
-    new_pb = agg.average_plan_diffs({}, ck_pb, [build_state(d, as_param=(i == 1)) for i, d in enumerate(diffs)])
-    assert len(new_pb) == len(ck_pb)
-    for got, want in zip(parse_state(new_pb), O.fedavg_mean(ckpt, diffs)):
-        assert same(got, want)
+    ck_pb = build_state(ckpt, as_param=True)
+    d_pb = [build_state(d, as_param=(i == 1)) for i, d in enumerate(diffs)]
+    want = O.fedavg_mean(ckpt, diffs)
+    # default: a fresh State like serialize_model_params (model_manager.py:82-90)
+    new_pb = agg.average_plan_diffs({}, ck_pb, d_pb)
+    for got, w in zip(parse_state(new_pb), want):
+        assert same(got, w)
+    # the old checkpoint's framing kept byte for byte, payloads replaced
+    tpl_pb = agg.average_plan_diffs({}, ck_pb, d_pb, framing="template")
+    assert len(tpl_pb) == len(ck_pb)
+    for got, w in zip(parse_state(tpl_pb), want):
+        assert same(got, w)
+
+
+def test_new_checkpoint_is_framed_like_serialize_model_params(engine):
+    """model_manager.py:82-90: State(state_placeholders=[PlaceHolder().instantiate(p) ...]) of the
+    plain tensors model_param - diff_param: fresh ids (not the template's, different every close),
+    torch_tensor entries (no inherited torch_param), no tags -- parsed with google.protobuf."""
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.state_schema import build_state, classes
+
+    rng = np.random.default_rng(9)
+    shapes = [(33, 17), (17,), (4, 33), (4,)]
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for _ in range(2)]
+    ck_pb = build_state(ckpt, as_param=True)  # the template: Parameters with tags
+    agg = CycleAggregator(engine)
+    outs = [agg.average_plan_diffs({}, ck_pb, [build_state(d) for d in diffs]) for _ in range(2)]
+    old = classes()["State"]()
+    old.ParseFromString(ck_pb)
+    old_ids = {ph.id.id_int for ph in old.placeholders}
+    want = O.fedavg_mean(ckpt, diffs)
+    seen = set()
+    for pb in outs:
+        st = classes()["State"]()
+        st.ParseFromString(pb)
+        assert len(st.placeholders) == len(st.tensors) == len(shapes)
+        for ph, t, shape, w in zip(st.placeholders, st.tensors, shapes, want):
+            assert list(ph.tags) == [] and not ph.description
+            assert t.HasField("torch_tensor") and not t.HasField("torch_param")
+            tt = t.torch_tensor
+            assert list(tt.tags) == [] and tt.contents_data.dtype == "float32"
+            assert tuple(tt.contents_data.shape.dims) == shape
+            got = np.asarray(tt.contents_data.contents_float32, F).reshape(shape)
+            assert same(got, w)
+            for i in (ph.id.id_int, tt.id.id_int):
+                assert 0 <= i < 10e10 and i not in old_ids and i not in seen
+                seen.add(i)
 
 
 def test_average_params_api(engine):
@@ -721,3 +764,32 @@ def test_iterative_division_exact_subnormal_midpoints(engine):
         finally:
             engine.set_variant(-1)
         assert same(got, coracle.fedavg(1, d, c)), variant
+
+
+def test_non_iterative_mean_plan_is_accelerated(engine):
+    """cycle_manager.py:270-271 with a hosted plan that is the plain mean: the engine runs it (MEAN)
+    and the new checkpoint equals what the node computes with the plan itself -- bit for bit; a
+    plan that sums in another order is declined (the node keeps running it)."""
+    import torch as th
+    from functools import reduce
+
+    from pygrid_amd import PlanNotAcceleratedError
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    def plan(diffs):
+        return [th.div(reduce(th.add, list(col)), len(diffs)) for col in zip(*diffs)]
+
+    rng = np.random.default_rng(12)
+    shapes = [(64, 50), (50,)]
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for _ in range(9)]
+    agg = CycleAggregator(engine)
+    new = agg.average_plan_diffs({"iterative_plan": False}, build_state_fast(ckpt),
+                                 [build_state_fast(d) for d in diffs], avg_plan=plan)
+    avg = plan([[th.from_numpy(t) for t in d] for d in diffs])  # the node's own :270-271 + :293-296
+    for got, c, a in zip(parse_state(new), ckpt, avg):
+        assert same(got, (th.from_numpy(c) - a).numpy())
+    with pytest.raises(PlanNotAcceleratedError):
+        agg.average_plan_diffs({}, build_state_fast(ckpt), [build_state_fast(d) for d in diffs],
+                               avg_plan=lambda ds: [th.stack(list(col)).mean(0) for col in zip(*ds)])

@@ -39,6 +39,45 @@ def reassociated_plan(avg, item, num):  # mathematically equal, rounds different
     return [avg[i] * (num / (num + 1)) + item[i] / (num + 1) for i in range(len(avg))]
 
 
+def mean_plan(diffs):  # a hosted non-iterative plan that is the hard-coded mean, cycle_manager.py:284-288
+    import torch as th
+    from functools import reduce
+
+    return [th.div(reduce(th.add, list(col)), len(diffs)) for col in zip(*diffs)]
+
+
+def loop_mean_plan(diffs):  # the same arithmetic written as a loop: also accepted
+    out = [d.clone() for d in diffs[0]]
+    for d in diffs[1:]:
+        out = [a + b for a, b in zip(out, d)]
+    return [a / len(diffs) for a in out]
+
+
+def stack_mean_plan(diffs):  # th.stack(...).mean(0): another summation order -- declined
+    import torch as th
+
+    return [th.stack(list(col)).mean(0) for col in zip(*diffs)]
+
+
+def zero_start_plan(diffs):  # python sum() starts at int 0: 0 + (-0.0) = +0.0 -- declined
+    return [sum(col) / len(diffs) for col in zip(*diffs)]
+
+
+def reversed_plan(diffs):  # folds the clients last to first -- declined
+    return mean_plan(diffs[::-1])
+
+
+def test_non_iterative_plan_dispatch():
+    """cycle_manager.py:270-271: a non-iterative hosted plan is accelerated only when it is the
+    hard-coded mean bit for bit on the probes; every other plan stays with the node."""
+    assert cycle.is_mean_plan(mean_plan) and cycle.is_mean_plan(loop_mean_plan)
+    assert cycle.select_mode({"iterative_plan": False}, mean_plan) == MEAN
+    for plan in (stack_mean_plan, zero_start_plan, reversed_plan, canonical_plan, lambda d: None):
+        assert not cycle.is_mean_plan(plan), plan
+        with pytest.raises(PlanNotAcceleratedError):
+            cycle.select_mode({}, plan)
+
+
 def test_select_mode_dispatch():
     assert cycle.select_mode({}, None) == MEAN
     assert cycle.select_mode({"iterative_plan": True}, None) == MEAN

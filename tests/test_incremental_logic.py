@@ -74,7 +74,7 @@ def test_in_order_reports_fold_in_batches():
         inc.reported(w, w.encode())
     assert folded(eng) == [b"a", b"b"]  # c waits for a full batch (or close)
     assert inc.folded_early == 2
-    inc.close(b"ck")
+    inc.close(b"ck", framing="template")
     assert folded(eng) == [b"a", b"b", b"c"] and eng.folds[-1] == (True, [b"c"])
 
 
@@ -103,7 +103,7 @@ def test_close_drops_non_reporters_and_keeps_id_order():
     assert folded(eng) == []            # worker 0 never reports
     assert sorted(eng.slot.values()) == [bytes([w]) for w in (1, 2, 4, 5)]
     ck = build_state_fast([np.array([1.0, 2.0, 3.0], np.float32)])
-    assert inc.close(ck) == ck
+    assert inc.close(ck, framing="template") == ck
     assert eng.folds == [(True, [b"\x01", b"\x02", b"\x04", b"\x05"])]
     assert inc.n_folded == 4 and inc.folded_early == 0
     assert [c[0] for c in eng.calls[-3:]] == ["upload", "finish", "patch"]
@@ -123,7 +123,7 @@ def test_twenty_percent_dropouts_shuffled_arrival():
     for w in order:
         inc.reported(int(w), int(w).to_bytes(2, "little"))
         assert inc.n_parked == 0
-    inc.close(b"ck")
+    inc.close(b"ck", framing="template")
     assert folded(eng) == [w.to_bytes(2, "little") for w in sorted(reporters)]
 
 
@@ -141,7 +141,7 @@ def test_slot_pressure_parks_on_host_but_never_starves_the_front():
         for w in rng.permutation(reporters):
             inc.reported(int(w), mk(int(w)))
             assert len(eng.slot) <= slots
-        inc.close(b"ck")
+        inc.close(b"ck", framing="template")
         assert folded(eng) == [mk(w) for w in sorted(reporters)], trial
 
 
@@ -151,7 +151,7 @@ def test_checkpoint_handed_over_at_start_is_uploaded_once():
     assert eng.calls[-1] == ("upload", b"ck")  # before any report: the upload overlaps the cycle
     inc.assigned("a")
     inc.reported("a", b"a")
-    assert inc.close(b"ck") == b"ck"
+    assert inc.close(b"ck", framing="template") == b"ck"
     assert [c[0] for c in eng.calls].count("upload") == 1
     assert [c[0] for c in eng.calls[-2:]] == ["finish", "patch"]
 
@@ -180,7 +180,7 @@ def test_errors():
     inc2 = IncrementalCycle(RecordingEngine(), [3], slots=4)
     inc2.assigned("b")
     with pytest.raises(AggregationError):
-        inc2.close(b"")
+        inc2.close(b"", framing="template")
 
 
 def test_malformed_diff_is_refused_to_its_sender_only():
@@ -195,7 +195,7 @@ def test_malformed_diff_is_refused_to_its_sender_only():
     inc.reported(1, b"1")
     inc.reported(0, b"0")  # the worker may retry with a good diff
     inc.reported(3, b"3")
-    inc.close(b"ck")
+    inc.close(b"ck", framing="template")
     assert folded(eng) == [b"0", b"1", b"3"]
 
 
@@ -215,7 +215,7 @@ def test_malformed_diff_is_refused_when_it_would_park():
     assert inc.n_parked == 1
     inc.reported(0, good)
     inc.reported(1, good)
-    inc.close(ck)
+    inc.close(ck, framing="template")
     assert len(folded(eng)) == 4
 
 
@@ -236,9 +236,9 @@ def test_reports_from_many_threads_and_a_late_one():
         t.start()
     for t in threads:
         t.join()
-    inc.close(b"ck")
+    inc.close(b"ck", framing="template")
     assert folded(eng) == [mk(k) for k in range(64)]
     with pytest.raises(AggregationError):
         inc.reported(0, b"late")
     with pytest.raises(AggregationError):
-        inc.close(b"ck")
+        inc.close(b"ck", framing="template")
