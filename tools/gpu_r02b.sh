@@ -1,0 +1,9 @@
+set -o pipefail
+mkdir -p gpurun_out/r02b
+O=gpurun_out/r02b
+timeout -k 10 120 python -u tools/time_mnist_second.py 8 > $O/second_default.log 2>&1 || exit 1
+MALLOC_MMAP_THRESHOLD_=131072 timeout -k 10 120 python -u tools/time_mnist_second.py 8 > $O/second_mmap_fixed.log 2>&1 || exit 1
+PGH_PREFAULT=0 timeout -k 10 120 python -u tools/time_mnist_second.py 8 > $O/second_noprefault.log 2>&1 || exit 1
+MALLOC_TOP_PAD_=67108864 timeout -k 10 120 python -u tools/time_mnist_second.py 8 > $O/second_toppad.log 2>&1 || exit 1
+timeout -k 10 120 python -u tools/time_mnist_cold.py > $O/mnist_cold.log 2>&1 || exit 1
+for f in $O/*.log; do echo "== $f"; grep -v amdgpu.ids $f | head -12; done
