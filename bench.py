@@ -290,10 +290,21 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def kernels_sha256() -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ("pygrid_amd/csrc/pgh_kernels.hip", "pygrid_amd/csrc/pgh_kernels.h"):
+        h.update((ROOT / f).read_bytes())
+    return h.hexdigest()
+
+
 def load_traffic(workload: str, variant: int, alg_bytes: float):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/pmc_traffic.json).
     When this launch's algorithmic bytes differ from the profiled launch's (e.g. a range-split
-    fold at N > 1), the measured traffic/algorithmic ratio is applied and the source says so."""
+    fold at N > 1), the measured traffic/algorithmic ratio is applied and the source says so.  A
+    summary measured on other kernel sources (kernels_sha256 differs) is not quoted: traffic is
+    then null and the source says it is stale."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
         return None, None
@@ -301,6 +312,8 @@ def load_traffic(workload: str, variant: int, alg_bytes: float):
         e = json.loads(f.read_text()).get(workload, {}).get(str(variant))
         if e is None:
             return None, None
+        if e.get("kernels_sha256") != kernels_sha256():
+            return None, f"stale: {e.get('source')} was measured on other kernel sources (re-run tools/profile_round.sh)"
         if abs(float(e.get("alg_bytes_per_launch", alg_bytes)) - alg_bytes) <= 1e-6 * alg_bytes:
             return float(e["hbm_bytes_per_launch"]), e.get("source")
         return float(e["ratio"]) * alg_bytes, f"{e.get('source')}; ratio {e['ratio']:.6f} applied to this launch"

@@ -18,7 +18,18 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 KERNEL = {"resnet18-fedavg": "k_fedavg", "resnet18-iterative": "k_fedavg", "resnet18-weighted": "k_fedavg",
-          "resnet18-secagg": "k_secagg"}
+          "resnet18-secagg": "k_secagg", "resnet18-report": "k_fedavg_rows"}
+
+
+def kernels_sha256() -> str:
+    """Hash of the kernel sources the counters were measured on (bench.py refuses to quote stale
+    traffic once they change)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ("pygrid_amd/csrc/pgh_kernels.hip", "pygrid_amd/csrc/pgh_kernels.h"):
+        h.update((ROOT / f).read_bytes())
+    return h.hexdigest()
 
 
 def per_launch(tree: Path, counter: str, kernel: str):
@@ -62,9 +73,12 @@ def main():
                       "formula": "(2*FETCH_SIZE + WRITE_SIZE)*1024",
                       "source": f"{dst}/pmc_summary.json (rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, "
                                 f"separate passes)"}
+    sha = kernels_sha256()
+    for e in summary.values():
+        e["kernels_sha256"] = sha
     (dst / "pmc_summary.json").write_text(json.dumps(summary, indent=1) + "\n")
     traffic = {w: {str(e["variant"]): {kk: e[kk] for kk in ("hbm_bytes_per_launch", "alg_bytes_per_launch", "ratio",
-                                                           "kernel", "layout", "source")}}
+                                                           "kernel", "layout", "source", "kernels_sha256")}}
                for w, e in summary.items()}
     (ROOT / "profiles" / "pmc_traffic.json").write_text(json.dumps(traffic, indent=1) + "\n")
     for w, e in summary.items():
