@@ -38,7 +38,8 @@ def per_launch(tree: Path, counter: str, kernel: str):
     for f in glob.glob(str(tree / "**" / "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if row.get("Counter_Name") != counter or kernel not in row.get("Kernel_Name", ""):
+                # "k_secagg<" / "k_fedavg<": not k_secagg_decode (pgh_create's warm-up) or k_fedavg_rows
+                if row.get("Counter_Name") != counter or (kernel + "<") not in row.get("Kernel_Name", ""):
                     continue
                 vals[(f, row.get("Dispatch_Id"))] += float(row["Counter_Value"])
                 name = row["Kernel_Name"]
