@@ -256,6 +256,16 @@ int pgh_state_scan(const uint8_t* pb, size_t n, int cap, int64_t* offsets, int64
  * has n bytes; out == tmpl patches in place. */
 int pgh_state_patch(const uint8_t* tmpl, size_t n, const float* values, int64_t n_values, uint8_t* out);
 
+/* Framing of the new checkpoint as serialize_model_params emits it (model_manager.py:79-92:
+ * State(state_placeholders=[PlaceHolder().instantiate(p) for p in params]) of plain tensors): per
+ * tensor of `tmpl` (State order, its shapes) a Placeholder{id = ids[2k]} and a
+ * StateTensor.torch_tensor{id = ids[2k + 1], serializer, contents_data{shape, "float32", payload}};
+ * no tags.  *needed = message bytes; with out (cap >= *needed) the framing is written and every
+ * payload span left for pgh_ckpt_patch_state(ctx, out, n, out) (in place) or the caller.  n_ids must
+ * be 2 x the tensors of tmpl. */
+int pgh_state_fresh(const uint8_t* tmpl, size_t n, const int64_t* ids, int n_ids, uint8_t* out, size_t cap,
+                    size_t* needed);
+
 /* Secure-aggregation shares as State bytes: every tensor a TensorData.contents_int64 (packed
  * varint; build-owned schema restatement, field 10).  Per tensor: payload byte offset, payload
  * bytes and the number of int64 values, validated as protobuf's parser would (varints of at most

@@ -110,6 +110,7 @@ SIGNATURES = {
     "pgh_state_scan": (_i, [C.c_char_p, _sz, _i, _P64, _P64, C.POINTER(C.c_int)]),
     "pgh_state_scan_i64": (_i, [C.c_char_p, _sz, _i, _P64, _P64, _P64, C.POINTER(C.c_int)]),
     "pgh_state_patch": (_i, [C.c_char_p, _sz, _vp, _i64, _vp]),
+    "pgh_state_fresh": (_i, [C.c_char_p, _sz, _P64, _i, _vp, _sz, C.POINTER(_sz)]),
     "pgh_b64_decoded_cap": (_sz, [_sz]),
     "pgh_b64_decode": (_i, [C.c_char_p, _sz, _vp, C.POINTER(_sz), _i]),
 }

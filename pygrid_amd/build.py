@@ -58,7 +58,8 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     tmp = LIB.with_suffix(".so.tmp")
     # -ldl: librccl.so.1 is dlopen'ed at the first multi-GPU collective (no link-time RCCL)
     cmd = [hipcc(), "-shared", "-fPIC", *objs, "-o", str(tmp), f"--offload-arch={ARCH}",
-           "-Wl,-soname,libpygrid_hip.so", "-ldl"]
+           "-Wl,-soname,libpygrid_hip.so", "-ldl",
+           "-Wl,-z,now"]  # bind every symbol at load: the node's first cycle close pays no lazy PLT lookups
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -410,3 +410,106 @@ int pgh_state_patch(const uint8_t* tmpl, size_t n, const float* values, int64_t 
 }
 
 }  // extern "C"
+
+// ---- fresh checkpoint framing (serialize_model_params, model_manager.py:79-92) -----------------------
+namespace {
+void put_varint(std::string* o, uint64_t v) {
+    while (v >= 0x80) {
+        o->push_back((char)(uint8_t)(v | 0x80));
+        v >>= 7;
+    }
+    o->push_back((char)(uint8_t)v);
+}
+void put_key(std::string* o, uint32_t field, uint32_t wt) { put_varint(o, ((uint64_t)field << 3) | wt); }
+void put_bytes(std::string* o, uint32_t field, const std::string& b) {
+    put_key(o, field, 2);
+    put_varint(o, b.size());
+    o->append(b);
+}
+std::string id_msg(int64_t id) {  // Id{id_int = 2}; proto3 omits a zero id
+    std::string m;
+    if (id) {
+        put_key(&m, 2, 0);
+        put_varint(&m, (uint64_t)id);
+    }
+    return m;
+}
+size_t varint_len(uint64_t v) {
+    size_t n = 1;
+    while (v >= 0x80) { v >>= 7; ++n; }
+    return n;
+}
+constexpr int SERIALIZER_ALL = 4;  // TorchTensor.serializer as state_schema.SERIALIZER_ALL
+}  // namespace
+
+extern "C" int pgh_state_fresh(const uint8_t* tmpl, size_t n, const int64_t* ids, int n_ids, uint8_t* out, size_t cap,
+                               size_t* needed) {
+    if (!needed || (!tmpl && n)) return PGH_E_ARG;
+    std::vector<pgh_state::Span> spans;
+    std::string msg;
+    int rc = pgh_state::scan(tmpl, n, &spans, &msg);
+    if (rc) return rc;
+    const size_t T = spans.size();
+    if (n_ids != (int)(2 * T) || (T && !ids)) return PGH_E_ARG;
+    // State.placeholders: Placeholder{id} per tensor (PlaceHolder().instantiate(p): no tags)
+    std::string head;
+    for (size_t k = 0; k < T; ++k) {
+        std::string ph;
+        put_bytes(&ph, 1, id_msg(ids[2 * k]));
+        put_bytes(&head, 1, ph);
+    }
+    // State.tensors: StateTensor.torch_tensor{id, serializer, contents_data{shape, dtype, f32}}; the
+    // payload is the last field of every enclosing message, so each tensor is prefix + payload
+    std::vector<std::string> prefix(T);
+    size_t total = head.size();
+    for (size_t k = 0; k < T; ++k) {
+        const auto& sp = spans[k];
+        std::vector<int64_t> dims = sp.shape;
+        int64_t numel = 1;
+        for (auto d : dims) numel *= d;
+        if (dims.empty() && sp.count != 1) dims.push_back(sp.count), numel = sp.count;  // no Size: 1-D
+        if (numel != sp.count) return PGH_E_PARSE;
+        const uint64_t pay = 4 * (uint64_t)sp.count;
+        std::string size_msg, td_head;
+        std::string packed;
+        for (auto d : dims) put_varint(&packed, (uint64_t)(uint32_t)(int32_t)d);
+        if (!packed.empty()) put_bytes(&size_msg, 1, packed);
+        put_bytes(&td_head, 1, size_msg);
+        put_bytes(&td_head, 2, "float32");
+        std::string td_pay;
+        if (pay) {
+            put_key(&td_pay, 12, 2);
+            put_varint(&td_pay, pay);
+        }
+        const uint64_t td_len = td_head.size() + td_pay.size() + pay;
+        std::string tt_head;
+        put_bytes(&tt_head, 1, id_msg(ids[2 * k + 1]));
+        put_key(&tt_head, 2, 0);
+        put_varint(&tt_head, SERIALIZER_ALL);
+        put_key(&tt_head, 4, 2);
+        put_varint(&tt_head, td_len);
+        const uint64_t tt_len = tt_head.size() + td_len;
+        const uint64_t st_len = 1 + varint_len(tt_len) + tt_len;
+        std::string& pf = prefix[k];
+        put_key(&pf, 2, 2);
+        put_varint(&pf, st_len);
+        put_key(&pf, 1, 2);
+        put_varint(&pf, tt_len);
+        pf += tt_head;
+        pf += td_head;
+        pf += td_pay;
+        total += pf.size() + pay;
+    }
+    *needed = total;
+    if (!out) return PGH_OK;
+    if (cap < total) return PGH_E_ARG;
+    size_t pos = 0;
+    std::memcpy(out, head.data(), head.size());
+    pos = head.size();
+    for (size_t k = 0; k < T; ++k) {  // the payload bytes are left for the caller (pgh_ckpt_patch_state)
+        std::memcpy(out + pos, prefix[k].data(), prefix[k].size());
+        pos += prefix[k].size() + 4 * (size_t)spans[k].count;
+    }
+    return PGH_OK;
+}
+

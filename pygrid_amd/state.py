@@ -89,20 +89,36 @@ def serialize_model_params(template: bytes, values: np.ndarray) -> bytes:
     return out
 
 
-def fresh_checkpoint(engine, template: bytes, ids=None) -> bytes:
-    """The new checkpoint as ``serialize_model_params`` emits it (model_manager.py:79-92): a fresh
-    State whose framing is built here from the template's tensor shapes and fresh ids
-    (``state_schema.fresh_frame``) and whose payloads the engine writes in place from the resident
-    checkpoint in HBM (``pgh_ckpt_patch_state`` with out == tmpl)."""
+def fresh_frame_bytes(template: bytes, ids=None):
+    """(uninitialised-payload bytes of the fresh checkpoint framed by ``pgh_state_fresh``, its host
+    address).  ``ids``: 2 per tensor (placeholder, tensor), syft's id space by default."""
     from . import state_schema
 
-    shapes = state_schema.tensor_shapes(template)
-    ids = list(ids) if ids is not None else state_schema.syft_ids(2 * len(shapes))
-    total, pieces, _ = state_schema.fresh_frame(shapes, ids)
-    out, ptr = _lib.fresh_bytes(total)
-    for off, b in pieces:  # framing; the payload bytes are all written by the engine below
-        C.memmove(ptr + off, b, len(b))
-    engine.ckpt_patch_into(ptr, total)
+    lib = _lib.load()
+    n = C.c_int(0)
+    rc = lib.pgh_state_scan(template, len(template), 0, None, None, C.byref(n))
+    if rc != 0:
+        raise StateParseError(f"malformed checkpoint State ({_lib.STATUS_NAMES.get(rc, rc)})", status=rc)
+    ids = list(ids) if ids is not None else state_schema.syft_ids(2 * n.value)
+    arr = (C.c_int64 * max(len(ids), 1))(*ids)
+    need = C.c_size_t(0)
+    rc = lib.pgh_state_fresh(template, len(template), arr, len(ids), None, 0, C.byref(need))
+    if rc != 0:
+        raise StateParseError(f"cannot frame a fresh checkpoint ({_lib.STATUS_NAMES.get(rc, rc)})", status=rc)
+    out, ptr = _lib.fresh_bytes(need.value)
+    rc = lib.pgh_state_fresh(template, len(template), arr, len(ids), ptr, need.value, C.byref(need))
+    if rc != 0:
+        raise StateParseError(f"cannot frame a fresh checkpoint ({_lib.STATUS_NAMES.get(rc, rc)})", status=rc)
+    return out, ptr
+
+
+def fresh_checkpoint(engine, template: bytes, ids=None) -> bytes:
+    """The new checkpoint as ``serialize_model_params`` emits it (model_manager.py:79-92): a fresh
+    State whose framing ``pgh_state_fresh`` builds from the template's tensor shapes and fresh ids
+    (restated in ``state_schema.fresh_frame``) and whose payloads the engine writes in place from
+    the resident checkpoint in HBM (``pgh_ckpt_patch_state`` with out == tmpl)."""
+    out, ptr = fresh_frame_bytes(template, ids)
+    engine.ckpt_patch_into(ptr, len(out))
     return out
 
 

@@ -333,13 +333,21 @@ def tensor_shapes(pb: bytes):
     return shapes
 
 
+_ID_RNG = None
+
+
 def syft_ids(n: int, rng=None):
     """n fresh object ids from syft 0.2.9's id space (random ints below 10e10,
     ``create_random_id``), as PlaceHolder().instantiate(...) and new tensors get them."""
+    global _ID_RNG
+    import os
     import random
 
-    r = rng or random.SystemRandom()
-    return [int(10e10 * r.random()) for _ in range(n)]
+    if rng is None:
+        if _ID_RNG is None:
+            _ID_RNG = random.Random(int.from_bytes(os.urandom(16), "little"))
+        rng = _ID_RNG
+    return [int(10e10 * rng.random()) for _ in range(n)]
 
 
 def fresh_frame(shapes, ids):

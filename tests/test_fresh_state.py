@@ -63,3 +63,33 @@ def test_tensor_shapes_rejects_truncated_framing():
 def test_syft_id_space():
     ids = S.syft_ids(1000)
     assert all(0 <= i < 10e10 for i in ids) and len(set(ids)) > 990
+
+
+@pytest.mark.parametrize("shapes", [MNIST_SHAPES, RESNET18_SHAPES, [(3,), (0,), (2, 0), (1,), (5, 1, 2)]])
+def test_native_fresh_frame_matches_the_restatement(shapes):
+    """pgh_state_fresh (C++, the product path) == state_schema.fresh_frame (Python restatement)."""
+    import ctypes as C
+
+    from pygrid_amd.state import fresh_frame_bytes
+
+    rng = np.random.default_rng(5)
+    arrs = [rng.standard_normal(s).astype(F) for s in shapes]
+    tmpl = S.build_state(arrs, as_param=True)  # the template's own framing differs (Parameters, tags)
+    ids = S.syft_ids(2 * len(shapes))
+    out, ptr = fresh_frame_bytes(tmpl, ids)
+    total, pieces, spans = S.fresh_frame(shapes, ids)
+    assert len(out) == total
+    for (off, n), a in zip(spans, arrs):  # fill the payloads as the engine would
+        C.memmove(ptr + off, a.astype("<f4").tobytes(), n)
+    assert out == reference_message(arrs, ids)
+
+
+def test_native_fresh_frame_rejects_bad_ids():
+    from pygrid_amd import _lib
+
+    import ctypes as C
+    lib = _lib.load()
+    tmpl = S.build_state_fast([np.zeros(3, F)])
+    need = C.c_size_t(0)
+    arr = (C.c_int64 * 1)(5)
+    assert lib.pgh_state_fresh(tmpl, len(tmpl), arr, 1, None, 0, C.byref(need)) == -1  # 2 ids per tensor
