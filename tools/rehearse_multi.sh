@@ -1,9 +1,9 @@
 #!/bin/bash
-# r02a: default bench (kernel line + e2e close), group bench at 1 GPU (RCCL) and a 2-child
+# default bench (kernel line + e2e close), group bench at 1 GPU (RCCL) and a 2-child
 # group rehearsal on GPU 0, the spawned 2-rank bench rehearsal (gloo on GPU 0).
 set -o pipefail
-mkdir -p gpurun_out/r02a
-O=gpurun_out/r02a
+mkdir -p gpurun_out/${1:-multi}
+O=gpurun_out/${1:-multi}
 run() { local name=$1; shift; echo "== $name"; timeout -k 10 400 "$@" > $O/$name.log 2>&1; local rc=$?; tail -1 $O/$name.log | cut -c1-2000; return $rc; }
 run default python -u bench.py --no-cpu-baseline || exit 1
 run group1 python -u bench.py --group --gpus 1 --no-cpu-baseline --steps 10 || exit 1
