@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Where the report-time close goes (bench.py --workload resnet18-report: ResNet-18, 100 assigned,
+~83 report in shuffled order, worker 0 never): every Engine call and codec step inside
+IncrementalCycle.close timed, per cycle.
+
+    python tools/time_report_close.py [cycles]
+"""
+import functools
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import numpy as np  # noqa: E402
+
+from pygrid_amd import Engine, _lib  # noqa: E402
+from pygrid_amd import state as st  # noqa: E402
+from pygrid_amd.incremental import IncrementalCycle  # noqa: E402
+from pygrid_amd.state_schema import build_state_fast  # noqa: E402
+from pygrid_amd.workloads import RESNET18_SHAPES  # noqa: E402
+
+rng = np.random.default_rng(1234)
+numel = [int(np.prod(s)) for s in RESNET18_SHAPES]
+ck = build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in RESNET18_SHAPES])
+distinct = [build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2) for s in RESNET18_SHAPES])
+            for _ in range(4)]
+N = 100
+reporters = [w for w in range(N) if w != 0 and rng.random() >= 0.2]
+arrival = [int(w) for w in rng.permutation(reporters)]
+eng = Engine(0)
+T = {}
+
+
+def wrap(obj, name, key=None):
+    f = getattr(obj, name)
+
+    @functools.wraps(f)
+    def g(*a, **k):
+        t0 = time.perf_counter()
+        r = f(*a, **k)
+        T[key or name] = round(T.get(key or name, 0) + (time.perf_counter() - t0) * 1e3, 3)
+        return r
+    setattr(obj, name, g)
+
+
+for n in ("fold_slots", "fold_slots_finish_resident", "ckpt_patch_into", "ckpt_upload_state"):
+    wrap(eng, n)
+wrap(st, "fresh_frame_bytes")
+wrap(_lib, "fresh_bytes")
+for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
+    inc = IncrementalCycle(eng, numel, slots=N, fold_batch=8, checkpoint=ck)
+    for w in range(N):
+        inc.assigned(w)
+    for w in arrival:
+        inc.reported(w, distinct[w % 4])
+    eng.sync()
+    T.clear()
+    t0 = time.perf_counter()
+    inc.close(ck)
+    print(it, round((time.perf_counter() - t0) * 1e3, 3), T, flush=True)
