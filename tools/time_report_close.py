@@ -43,8 +43,10 @@ def wrap(obj, name, key=None):
     setattr(obj, name, g)
 
 
-for n in ("fold_slots", "fold_slots_finish_resident", "ckpt_patch_into", "ckpt_upload_state"):
+for n in ("fold_slots", "fold_slots_finish_resident", "ckpt_patch_into", "ckpt_upload_state", "set_weights"):
     wrap(eng, n)
+wrap(IncrementalCycle, "_advance")
+wrap(IncrementalCycle, "_fold_ready")
 wrap(st, "fresh_frame_bytes")
 wrap(_lib, "fresh_bytes")
 for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
@@ -55,6 +57,20 @@ for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
         inc.reported(w, distinct[w % 4])
     eng.sync()
     T.clear()
-    t0 = time.perf_counter()
-    inc.close(ck)
-    print(it, round((time.perf_counter() - t0) * 1e3, 3), T, flush=True)
+    import gc
+    gc0 = gc.get_count()
+    if "--profile" in sys.argv and it == 3:
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        t0 = time.perf_counter()
+        pr.enable()
+        inc.close(ck)
+        pr.disable()
+        el = time.perf_counter() - t0
+        pstats.Stats(pr).sort_stats("cumulative").print_stats(25)
+    else:
+        t0 = time.perf_counter()
+        inc.close(ck)
+        el = time.perf_counter() - t0
+    print(it, round(el * 1e3, 3), T, "gc", gc0, gc.get_count(), flush=True)
