@@ -49,6 +49,7 @@ wrap(IncrementalCycle, "_advance")
 wrap(IncrementalCycle, "_fold_ready")
 wrap(st, "fresh_frame_bytes")
 wrap(_lib, "fresh_bytes")
+new = None  # the previous close's bytes stay alive until the next close returns (as in a node)
 for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
     inc = IncrementalCycle(eng, numel, slots=N, fold_batch=8, checkpoint=ck)
     for w in range(N):
@@ -65,12 +66,13 @@ for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
         pr = cProfile.Profile()
         t0 = time.perf_counter()
         pr.enable()
-        inc.close(ck)
+        out = inc.close(ck)
         pr.disable()
         el = time.perf_counter() - t0
         pstats.Stats(pr).sort_stats("cumulative").print_stats(25)
     else:
         t0 = time.perf_counter()
-        inc.close(ck)
+        out = inc.close(ck)
         el = time.perf_counter() - t0
+    new = out
     print(it, round(el * 1e3, 3), T, "gc", gc0, gc.get_count(), flush=True)
