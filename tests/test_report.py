@@ -95,3 +95,36 @@ def test_state_diff_roundtrip():
     rng = np.random.default_rng(2)
     pb = build_state_fast([rng.standard_normal(s).astype(np.float32) for s in MNIST_SHAPES])
     assert b64decode(base64.b64encode(pb).decode()) == pb
+
+
+@pytest.mark.parametrize("size", [300, 90_000, 1_200_001])
+def test_every_byte_value_inside_a_clean_string(size):
+    """The AVX2 fast path (fixed quad positions, pshufb range check) must hand every character
+    outside the alphabet to the general path: each of the 256 byte values planted in a clean
+    string, at a SIMD-block edge and mid-block, single- and multi-threaded."""
+    rng = np.random.default_rng(size)
+    enc = base64.b64encode(rng.integers(0, 256, size, dtype=np.uint8).tobytes()).rstrip(b"=")
+    for pos in (31, 32, 45, len(enc) // 2, len(enc) - 5):
+        for b in range(256):
+            s = enc[:pos] + bytes([b]) + enc[pos:]
+            try:
+                want = base64.b64decode(s)
+            except binascii.Error:
+                want = None
+            for th in ((1, 7) if size > 1_000_000 else (1,)):
+                try:
+                    got = b64decode(s, threads=th)
+                except binascii.Error:
+                    got = None
+                assert got == want, (pos, b, th)
+
+
+def test_fast_and_general_paths_agree(monkeypatch):
+    rng = np.random.default_rng(11)
+    for n in (0, 1, 2, 3, 23, 24, 25, 47, 48, 49, 196_607, 196_608, 196_609, 1_000_000):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        enc = base64.b64encode(data)
+        assert b64decode(enc) == data
+        monkeypatch.setenv("PGH_B64_GENERAL", "1")
+        assert b64decode(enc) == data
+        monkeypatch.delenv("PGH_B64_GENERAL")
