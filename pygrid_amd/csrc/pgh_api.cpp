@@ -1962,7 +1962,7 @@ int pgh_stream_finish_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, f
 int pgh_set_variant(pgh_ctx* c, int variant) {
     if (c && c->grp) return pgh_group_api::set_variant(c, variant);
     if (!c) return PGH_E_ARG;
-    if (variant < -1 || variant > 22) return fail(c, PGH_E_ARG, "variant %d outside [-1,22]", variant);
+    if (variant < -1 || variant > 23) return fail(c, PGH_E_ARG, "variant %d outside [-1,23]", variant);
     c->variant = variant;
     return PGH_OK;
 }

@@ -291,6 +291,8 @@ int ensure_backend(pgh_ctx* c, int n) {
             const ncclResult_t e = r->comm_init_all(g->comms.data(), n, devs.data());
             if (e != ncclSuccess) {
                 g->comms.clear();
+                g->backend = -1;  // not silently peer copies: the next collective tries RCCL again (and fails loudly)
+                g->comm_n = 0;
                 return fail(c, PGH_E_HIP, "ncclCommInitAll over %d GPUs failed: %s", n, r->error_string(e));
             }
             g->backend = 1;
@@ -841,7 +843,7 @@ int stream_finish_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float
 }
 
 int set_variant(pgh_ctx* c, int variant) {
-    if (variant < -1 || variant > 22) return fail(c, PGH_E_ARG, "variant %d outside [-1,22]", variant);
+    if (variant < -1 || variant > 23) return fail(c, PGH_E_ARG, "variant %d outside [-1,23]", variant);
     return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_set_variant(k, variant); }, (int)G(c)->kids.size());
 }
 

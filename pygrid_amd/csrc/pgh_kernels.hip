@@ -308,11 +308,21 @@ __global__ __launch_bounds__(TB) void k_fedavg_pipe(FedavgArgs a, int64_t ncol) 
         fedavg_columns_pipe<MODE, U, NT, VEC>(a, q);
 }
 
+// Workgroup -> tile order.  Workgroups are dealt round robin over the 8 XCDs (wg % 8); XMAP gives
+// each XCD a contiguous eighth of the tiles instead (A/B variant 23: does DRAM page locality
+// across XCDs matter for a read-once stream?).
+template <bool XMAP>
+__device__ __forceinline__ int64_t tile_of_wg() {
+    if constexpr (!XMAP) return blockIdx.x;
+    const int64_t g = gridDim.x, per = g / 8, b = blockIdx.x;
+    return b < per * 8 ? (b % 8) * per + b / 8 : b;
+}
+
 // Grid-stride over tiles of TB x W columns; a partial last tile goes one column per lane.
-template <int MODE, int U, int W, bool NT, int TB, int VEC, bool IDX>
+template <int MODE, int U, int W, bool NT, int TB, int VEC, bool IDX, bool XMAP = false>
 __device__ __forceinline__ void fedavg_tiles(const FedavgArgs& a, const RowTab* tab, int64_t ncol) {
     const int64_t tile = (int64_t)TB * W;
-    for (int64_t t0 = (int64_t)blockIdx.x * tile; t0 < ncol; t0 += (int64_t)gridDim.x * tile) {
+    for (int64_t t0 = tile_of_wg<XMAP>() * tile; t0 < ncol; t0 += (int64_t)gridDim.x * tile) {
         const int64_t q0 = t0 + threadIdx.x;
         if (t0 + tile <= ncol) {
             fedavg_columns<MODE, U, W, NT, VEC, IDX>(a, tab, q0, TB);
@@ -323,9 +333,9 @@ __device__ __forceinline__ void fedavg_tiles(const FedavgArgs& a, const RowTab* 
     }
 }
 
-template <int MODE, int U, int W, bool NT, int TB, int VEC>
+template <int MODE, int U, int W, bool NT, int TB, int VEC, bool XMAP = false>
 __global__ __launch_bounds__(TB) void k_fedavg(FedavgArgs a, int64_t ncol) {
-    fedavg_tiles<MODE, U, W, NT, TB, VEC, false>(a, nullptr, ncol);
+    fedavg_tiles<MODE, U, W, NT, TB, VEC, false, XMAP>(a, nullptr, ncol);
 }
 
 // The same fold over the slab rows listed in `tab` (report-time aggregation, pgh_fold_slots).
@@ -583,10 +593,11 @@ int cu_count() {
 //   20  nt     8                   1              1024   4                 one lane per column
 //   21  nt     8 (+8 next batch)   1              256    4                 one lane per column, pipelined
 //   22  nt     4 (+4 next batch)   1              256    4                 one lane per column, pipelined
+//   23  nt     8                   1              256    4                 as 0, each XCD a contiguous eighth
 // nt loads won 2-5 % on the once-read diff stream (r01c).  Small shards are bound by lanes / CU
 // balance, not by the loads: the auto choice (variant -1) picks by shard size and mode
 // (auto_variant below, r01l measurements on the column-blocked slab).
-constexpr int N_VARIANTS = 23;
+constexpr int N_VARIANTS = 24;
 constexpr int SECAGG_AUTO_VARIANT = 14;
 
 inline unsigned grid_for(int64_t ncol, int64_t tile, bool persistent) {
@@ -596,10 +607,10 @@ inline unsigned grid_for(int64_t ncol, int64_t tile, bool persistent) {
     return (unsigned)(full < pers ? (full > 0 ? full : 1) : pers);
 }
 
-template <int MODE, int U, int W, bool NT, int TB, int VEC>
+template <int MODE, int U, int W, bool NT, int TB, int VEC, bool XMAP = false>
 hipError_t go_fedavg(const FedavgArgs& a, bool persistent, hipStream_t s) {
     const int64_t ncol = (a.p + VEC - 1) / VEC;
-    k_fedavg<MODE, U, W, NT, TB, VEC><<<grid_for(ncol, (int64_t)TB * W, persistent), TB, 0, s>>>(a, ncol);
+    k_fedavg<MODE, U, W, NT, TB, VEC, XMAP><<<grid_for(ncol, (int64_t)TB * W, persistent), TB, 0, s>>>(a, ncol);
     return hipGetLastError();
 }
 
@@ -655,6 +666,7 @@ hipError_t dispatch_fedavg(const FedavgArgs& a, int variant, hipStream_t s) {
     case 20: return go_fedavg<MODE, 8, 1, true, 1024, 4>(a, false, s);
     case 21: return go_fedavg_pipe<MODE, 8, 256, 4>(a, s);
     case 22: return go_fedavg_pipe<MODE, 4, 256, 4>(a, s);
+    case 23: return go_fedavg<MODE, 8, 1, true, 256, 4, true>(a, false, s);
     default: return hipErrorInvalidValue;
     }
 }

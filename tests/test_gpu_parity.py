@@ -50,7 +50,7 @@ def test_engine_reports_device(engine):
     assert device_count() >= 1
 
 
-@pytest.mark.parametrize("variant", list(range(-1, 23)))
+@pytest.mark.parametrize("variant", list(range(-1, 24)))
 def test_edge_fixtures_all_modes(engine, gold, variant):
     z = np.load(gold / "edge_f32.npz")
     engine.set_variant(variant)
@@ -64,7 +64,7 @@ def test_edge_fixtures_all_modes(engine, gold, variant):
         engine.set_variant(-1)
 
 
-@pytest.mark.parametrize("variant", list(range(-1, 23)))
+@pytest.mark.parametrize("variant", list(range(-1, 24)))
 def test_variants_mid_size(engine, variant):
     """Full tiles and a partial last tile for every variant (W = 2 tiles are 512 columns)."""
     rng = np.random.default_rng(variant + 1)
