@@ -278,6 +278,14 @@ size_t pgh_b64_decoded_cap(size_t n);
 /* Python base64.b64decode semantics (non-validating); threads <= 0 = auto.  PGH_E_PARSE on bad
  * padding. */
 int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int threads);
+/* Decoded size, computed from the text after the last whole quad of the '='-free prefix alone,
+ * valid IF that prefix is all alphabet characters (the common case; not checked).  PGH_E_PARSE when
+ * that tail is not clean: use pgh_b64_decode(out = NULL) for the exact size then. */
+int pgh_b64_clean_size(const char* in, size_t n, size_t* size);
+/* pgh_b64_decode into `out` of `cap` bytes: when the decoded size exceeds cap, nothing past cap is
+ * written and PGH_E_STATE returns the size needed in *written (lets a caller allocate the clean
+ * size, decode in one pass, and fall back only for unclean text). */
+int pgh_b64_decode_into(const char* in, size_t n, uint8_t* out, size_t cap, size_t* written, int threads);
 
 #ifdef __cplusplus
 }

@@ -34,7 +34,10 @@
 #include <cstdint>
 #include <cstring>
 
+#include <condition_variable>
 #include <cstdlib>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -198,12 +201,79 @@ void populate(uint8_t* p, size_t n) {
     if (b > a) (void)madvise((void*)a, b - a, MADV_POPULATE_WRITE);
 }
 
+// A persistent pool (thread creation cost ~1 ms per decode at 16 threads x 2 passes): run(t, f)
+// calls f(k) for k in [0, t), k = 0 on the caller's thread.  One decode at a time per pool.
+class Pool {
+  public:
+    void run(int t, const std::function<void(int)>& f) {
+        std::lock_guard<std::mutex> one(busy_);
+        if (t <= 1) { f(0); return; }
+        grow(t - 1);
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            fn_ = &f;
+            want_ = t - 1;
+            pending_ = t - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& w : workers_) w.join();
+    }
+
+  private:
+    void grow(int n) {
+        while ((int)workers_.size() < n) {
+            const int id = (int)workers_.size() + 1;
+            workers_.emplace_back([this, id] { loop(id); });
+        }
+    }
+    void loop(int id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* fn = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                if (id > want_) continue;  // not needed for this job
+                fn = fn_;
+            }
+            (*fn)(id);
+            std::lock_guard<std::mutex> lk(m_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::mutex busy_, m_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> workers_;
+    const std::function<void(int)>* fn_ = nullptr;
+    int want_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+Pool& pool() {
+    static Pool* p = new Pool();  // never destroyed: worker threads must not be joined at exit
+    return *p;
+}
+
 template <class F>
 void parallel(int t, F&& f) {  // f(k) for k in [0, t), k = 0 on the calling thread
-    std::vector<std::thread> th;
-    for (int k = 1; k < t; ++k) th.emplace_back(f, k);
-    f(0);
-    for (auto& x : th) x.join();
+    const std::function<void(int)> fn = f;
+    pool().run(t, fn);
 }
 
 }  // namespace
@@ -213,12 +283,29 @@ extern "C" {
 // Decoded size upper bound for an input of n characters.
 size_t pgh_b64_decoded_cap(size_t n) { return n / 4 * 3 + 3; }
 
-// Decode `in` (n chars) into `out` (capacity >= pgh_b64_decoded_cap(n)); *written = bytes.
-// out == NULL: validate only and return the exact decoded size in *written.
-// threads <= 0 picks min(16, hardware threads).  Returns PGH_OK or PGH_E_PARSE (Python's
-// "Incorrect padding" / "cannot be 1 more than a multiple of 4").
-int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int threads) {
-    if ((!in && n) || !written) return PGH_E_ARG;  // out == NULL: validate and size only
+// Decoded size of `in` IF every character before its first '=' is in the alphabet (not checked:
+// O(characters from the last whole quad of that prefix on)).  PGH_E_PARSE when that tail does not
+// decode cleanly -- the caller then takes the general route (pgh_b64_decode with out == NULL).
+int pgh_b64_clean_size(const char* in, size_t n, size_t* size) {
+    if ((!in && n) || !size) return PGH_E_ARG;
+    const unsigned char* s = (const unsigned char*)in;
+    const void* eq = n ? std::memchr(s, '=', n) : nullptr;
+    const size_t fe = eq ? (size_t)((const unsigned char*)eq - s) : n;
+    const size_t n4f = fe / 4;
+    Machine m;
+    std::vector<uint8_t> tail;
+    m.feed(s + 4 * n4f, n - 4 * n4f, &tail);
+    if (!m.done && m.quad_pos != 0) return PGH_E_PARSE;
+    *size = n4f * 3 + tail.size();
+    return PGH_OK;
+}
+
+// Decode `in` (n chars) into `out` of `cap` bytes; *written = decoded bytes.  out == NULL: validate
+// and size only.  When the decoded size exceeds cap, nothing past cap is written: PGH_E_STATE with
+// *written = the size needed.  threads <= 0 picks min(16, hardware threads).  PGH_E_PARSE is
+// Python's "Incorrect padding" / "cannot be 1 more than a multiple of 4".
+int pgh_b64_decode_into(const char* in, size_t n, uint8_t* out, size_t cap, size_t* written, int threads) {
+    if ((!in && n) || !written) return PGH_E_ARG;
     const unsigned char* s = (const unsigned char*)in;
     int t = threads > 0 ? threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     if (n < (1u << 18)) t = 1;
@@ -227,24 +314,27 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
     if (std::getenv("PGH_B64_GENERAL") == nullptr) {
         // fast path: a prefix of alphabet characters only -> fixed quad positions, one pass
         const size_t n4f = fe / 4;
-        const int tf = n4f < (1u << 16) ? 1 : t;
-        const size_t pq = (n4f + tf - 1) / tf;
-        std::atomic<bool> clean{true};
-        parallel(tf, [&](int k) {
-            const size_t g0 = std::min(n4f, pq * k), g1 = std::min(n4f, g0 + pq);
-            if (out) populate(out + 3 * g0, 3 * (g1 - g0));  // this thread's part of the fresh output
-            const bool ok = out ? decode_clean(s + 4 * g0, g1 - g0, out + 3 * g0)
-                                : all_alphabet(s + 4 * g0, 4 * (g1 - g0));
-            if (!ok) clean.store(false, std::memory_order_relaxed);
-        });
-        if (clean.load() && all_alphabet(s + 4 * n4f, fe - 4 * n4f)) {
-            Machine m;
-            std::vector<uint8_t> tail;
-            m.feed(s + 4 * n4f, n - 4 * n4f, &tail);  // the last 0-3 prefix characters, then from '='
-            if (!m.done && m.quad_pos != 0) return PGH_E_PARSE;
-            if (out && !tail.empty()) std::memcpy(out + 3 * n4f, tail.data(), tail.size());
-            *written = n4f * 3 + tail.size();
-            return PGH_OK;
+        Machine m;
+        std::vector<uint8_t> tail;
+        m.feed(s + 4 * n4f, n - 4 * n4f, &tail);  // the last 0-3 prefix characters, then from '='
+        const bool tail_ok = (m.done || m.quad_pos == 0) && all_alphabet(s + 4 * n4f, fe - 4 * n4f);
+        const size_t need = n4f * 3 + tail.size();
+        if (tail_ok && (!out || need <= cap)) {
+            const int tf = n4f < (1u << 16) ? 1 : t;
+            const size_t pq = (n4f + tf - 1) / tf;
+            std::atomic<bool> clean{true};
+            parallel(tf, [&](int k) {
+                const size_t g0 = std::min(n4f, pq * k), g1 = std::min(n4f, g0 + pq);
+                if (out) populate(out + 3 * g0, 3 * (g1 - g0));  // this thread's part of the fresh output
+                const bool ok = out ? decode_clean(s + 4 * g0, g1 - g0, out + 3 * g0)
+                                    : all_alphabet(s + 4 * g0, 4 * (g1 - g0));
+                if (!ok) clean.store(false, std::memory_order_relaxed);
+            });
+            if (clean.load()) {
+                if (out && !tail.empty()) std::memcpy(out + 3 * n4f, tail.data(), tail.size());
+                *written = need;
+                return PGH_OK;
+            }
         }
     }
     // count alphabet characters per chunk of [0, fe)
@@ -271,10 +361,9 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
     m.feed(lead, nl, &tail);
     m.feed(s + fe, n - fe, &tail);
     if (!m.done && m.quad_pos != 0) return PGH_E_PARSE;
-    if (!out) {
-        *written = n4 * 3 + tail.size();
-        return PGH_OK;
-    }
+    *written = n4 * 3 + tail.size();
+    if (!out) return PGH_OK;
+    if (*written > cap) return PGH_E_STATE;
     if (d == fe) {  // clean prefix: whole quads straight from the input
         const int td = n4 < (1u << 16) ? 1 : t;
         const size_t pq = (n4 + td - 1) / td;
@@ -301,8 +390,12 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
         });
     }
     if (!tail.empty()) std::memcpy(out + 3 * n4, tail.data(), tail.size());
-    *written = n4 * 3 + tail.size();
     return PGH_OK;
+}
+
+// Decode `in` (n chars) into `out` (capacity >= pgh_b64_decoded_cap(n)); *written = bytes.
+int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int threads) {
+    return pgh_b64_decode_into(in, n, out, pgh_b64_decoded_cap(n), written, threads);
 }
 
 }  // extern "C"

@@ -128,3 +128,28 @@ def test_fast_and_general_paths_agree(monkeypatch):
         monkeypatch.setenv("PGH_B64_GENERAL", "1")
         assert b64decode(enc) == data
         monkeypatch.delenv("PGH_B64_GENERAL")
+
+
+def test_decode_into_capacity_and_clean_size():
+    import ctypes as C
+
+    from pygrid_amd import _lib
+
+    lib = _lib.load()
+    data = np.random.default_rng(5).integers(0, 256, 100_000, dtype=np.uint8).tobytes()
+    enc = base64.b64encode(data)
+    n = C.c_size_t(0)
+    assert lib.pgh_b64_clean_size(enc, len(enc), C.byref(n)) == 0 and n.value == len(data)
+    small = (C.c_uint8 * 10)()
+    assert lib.pgh_b64_decode_into(enc, len(enc), small, 10, C.byref(n), 1) == -3  # PGH_E_STATE
+    assert n.value == len(data)
+    buf = (C.c_uint8 * len(data))()
+    assert lib.pgh_b64_decode_into(enc, len(enc), buf, len(data), C.byref(n), 4) == 0
+    assert bytes(buf) == data
+    dirty = enc[:1000] + b"**\n" + enc[1000:]  # the clean size is a guess: decode_into checks it
+    assert lib.pgh_b64_clean_size(dirty, len(dirty), C.byref(n)) == 0
+    assert b64decode(dirty) == data
+    bad_tail = enc[:-2] + b"Q"  # one character over a multiple of 4
+    assert lib.pgh_b64_clean_size(bad_tail, len(bad_tail), C.byref(n)) == -5
+    with pytest.raises(binascii.Error):
+        b64decode(bad_tail)
