@@ -282,10 +282,10 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
  * valid IF that prefix is all alphabet characters (the common case; not checked).  PGH_E_PARSE when
  * that tail is not clean: use pgh_b64_decode(out = NULL) for the exact size then. */
 int pgh_b64_clean_size(const char* in, size_t n, size_t* size);
-/* pgh_b64_decode into `out` of `cap` bytes: when the decoded size exceeds cap, nothing past cap is
- * written and PGH_E_STATE returns the size needed in *written (lets a caller allocate the clean
- * size, decode in one pass, and fall back only for unclean text). */
-int pgh_b64_decode_into(const char* in, size_t n, uint8_t* out, size_t cap, size_t* written, int threads);
+/* One pass for a clean string (every character before the first '=' in the alphabet): `out` holds
+ * `cap` = pgh_b64_clean_size bytes.  PGH_E_STATE when the text is not clean (or decodes to more than
+ * cap): take pgh_b64_decode then. */
+int pgh_b64_decode_clean(const char* in, size_t n, uint8_t* out, size_t cap, size_t* written, int threads);
 
 #ifdef __cplusplus
 }

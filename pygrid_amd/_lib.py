@@ -114,7 +114,7 @@ SIGNATURES = {
     "pgh_b64_decoded_cap": (_sz, [_sz]),
     "pgh_b64_decode": (_i, [C.c_char_p, _sz, _vp, C.POINTER(_sz), _i]),
     "pgh_b64_clean_size": (_i, [C.c_char_p, _sz, C.POINTER(_sz)]),
-    "pgh_b64_decode_into": (_i, [C.c_char_p, _sz, _vp, _sz, C.POINTER(_sz), _i]),
+    "pgh_b64_decode_clean": (_i, [C.c_char_p, _sz, _vp, _sz, C.POINTER(_sz), _i]),
 }
 
 ABI_VERSION = 4  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)

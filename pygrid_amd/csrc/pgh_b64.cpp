@@ -134,6 +134,7 @@ __attribute__((target("avx2"))) bool all_alphabet_avx2(const unsigned char* in, 
         const __m256i hi = _mm256_and_si256(_mm256_srli_epi32(v, 4), nib);
         bad = _mm256_or_si256(bad, _mm256_and_si256(_mm256_shuffle_epi8(lut_lo, _mm256_and_si256(v, nib)),
                                                     _mm256_shuffle_epi8(lut_hi, hi)));
+        if ((i & 2047) == 2016 && !_mm256_testz_si256(bad, bad)) return false;  // every 2 KiB: stop early
     }
     if (!_mm256_testz_si256(bad, bad)) return false;
     for (; i < n; ++i)
@@ -278,6 +279,47 @@ void parallel(int t, F&& f) {  // f(k) for k in [0, t), k = 0 on the calling thr
 
 }  // namespace
 
+namespace {
+// The fast path: every character before the first '=' in the alphabet.  Returns PGH_OK (decoded,
+// *written set), PGH_E_PARSE (clean text, bad padding) or PGH_E_STATE (not clean, or more than
+// cap bytes: nothing usable written).
+int decode_fast(const unsigned char* s, size_t n, size_t fe, uint8_t* out, size_t cap, size_t* written, int t) {
+    const size_t n4f = fe / 4;
+    Machine m;
+    std::vector<uint8_t> tail;
+    m.feed(s + 4 * n4f, n - 4 * n4f, &tail);  // the last 0-3 prefix characters, then from '='
+    if (!all_alphabet(s + 4 * n4f, fe - 4 * n4f)) return PGH_E_STATE;
+    const bool padded = m.done || m.quad_pos == 0;
+    const size_t need = n4f * 3 + tail.size();
+    if (padded && out && need > cap) return PGH_E_STATE;
+    const int tf = n4f < (1u << 16) ? 1 : t;
+    const size_t pq = (n4f + tf - 1) / tf;
+    std::atomic<bool> clean{true};
+    parallel(tf, [&](int k) {
+        const size_t g0 = std::min(n4f, pq * k), g1 = std::min(n4f, g0 + pq);
+        const bool dec = out && padded;
+        if (dec) populate(out + 3 * g0, 3 * (g1 - g0));  // this thread's part of the fresh output
+        const bool ok = dec ? decode_clean(s + 4 * g0, g1 - g0, out + 3 * g0) : all_alphabet(s + 4 * g0, 4 * (g1 - g0));
+        if (!ok) clean.store(false, std::memory_order_relaxed);
+    });
+    if (!clean.load()) return PGH_E_STATE;
+    if (!padded) return PGH_E_PARSE;  // a clean prefix: the machine's verdict is final
+    if (out && !tail.empty()) std::memcpy(out + 3 * n4f, tail.data(), tail.size());
+    *written = need;
+    return PGH_OK;
+}
+
+int threads_for(size_t n, int threads) {
+    const int t = threads > 0 ? threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    return n < (1u << 18) ? 1 : t;
+}
+
+size_t first_eq(const unsigned char* s, size_t n) {
+    const void* eq = n ? std::memchr(s, '=', n) : nullptr;
+    return eq ? (size_t)((const unsigned char*)eq - s) : n;
+}
+}  // namespace
+
 extern "C" {
 
 // Decoded size upper bound for an input of n characters.
@@ -300,42 +342,27 @@ int pgh_b64_clean_size(const char* in, size_t n, size_t* size) {
     return PGH_OK;
 }
 
-// Decode `in` (n chars) into `out` of `cap` bytes; *written = decoded bytes.  out == NULL: validate
-// and size only.  When the decoded size exceeds cap, nothing past cap is written: PGH_E_STATE with
-// *written = the size needed.  threads <= 0 picks min(16, hardware threads).  PGH_E_PARSE is
-// Python's "Incorrect padding" / "cannot be 1 more than a multiple of 4".
-int pgh_b64_decode_into(const char* in, size_t n, uint8_t* out, size_t cap, size_t* written, int threads) {
+
+// One pass for a clean string: `out` holds cap bytes (pgh_b64_clean_size's value); PGH_E_STATE
+// when the text is not all alphabet before its first '=' (or decodes to more than cap): then take
+// the general route, pgh_b64_decode.
+int pgh_b64_decode_clean(const char* in, size_t n, uint8_t* out, size_t cap, size_t* written, int threads) {
+    if ((!in && n) || !written || !out) return PGH_E_ARG;
+    const unsigned char* s = (const unsigned char*)in;
+    return decode_fast(s, n, first_eq(s, n), out, cap, written, threads_for(n, threads));
+}
+
+// Decode `in` (n chars) into `out` (capacity >= pgh_b64_decoded_cap(n)); *written = bytes.
+// out == NULL: validate and size only.  threads <= 0 picks min(16, hardware threads).  Returns
+// PGH_OK or PGH_E_PARSE (Python's "Incorrect padding" / "cannot be 1 more than a multiple of 4").
+int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int threads) {
     if ((!in && n) || !written) return PGH_E_ARG;
     const unsigned char* s = (const unsigned char*)in;
-    int t = threads > 0 ? threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    if (n < (1u << 18)) t = 1;
-    const void* eq = n ? std::memchr(s, '=', n) : nullptr;
-    const size_t fe = eq ? (size_t)((const unsigned char*)eq - s) : n;  // the machine's fast prefix
+    const int t = threads_for(n, threads);
+    const size_t fe = first_eq(s, n);  // the machine's fast prefix
     if (std::getenv("PGH_B64_GENERAL") == nullptr) {
-        // fast path: a prefix of alphabet characters only -> fixed quad positions, one pass
-        const size_t n4f = fe / 4;
-        Machine m;
-        std::vector<uint8_t> tail;
-        m.feed(s + 4 * n4f, n - 4 * n4f, &tail);  // the last 0-3 prefix characters, then from '='
-        const bool tail_ok = (m.done || m.quad_pos == 0) && all_alphabet(s + 4 * n4f, fe - 4 * n4f);
-        const size_t need = n4f * 3 + tail.size();
-        if (tail_ok && (!out || need <= cap)) {
-            const int tf = n4f < (1u << 16) ? 1 : t;
-            const size_t pq = (n4f + tf - 1) / tf;
-            std::atomic<bool> clean{true};
-            parallel(tf, [&](int k) {
-                const size_t g0 = std::min(n4f, pq * k), g1 = std::min(n4f, g0 + pq);
-                if (out) populate(out + 3 * g0, 3 * (g1 - g0));  // this thread's part of the fresh output
-                const bool ok = out ? decode_clean(s + 4 * g0, g1 - g0, out + 3 * g0)
-                                    : all_alphabet(s + 4 * g0, 4 * (g1 - g0));
-                if (!ok) clean.store(false, std::memory_order_relaxed);
-            });
-            if (clean.load()) {
-                if (out && !tail.empty()) std::memcpy(out + 3 * n4f, tail.data(), tail.size());
-                *written = need;
-                return PGH_OK;
-            }
-        }
+        const int rc = decode_fast(s, n, fe, out, pgh_b64_decoded_cap(n), written, t);
+        if (rc != PGH_E_STATE) return rc;  // clean text: decoded, or a padding error
     }
     // count alphabet characters per chunk of [0, fe)
     const size_t per = (fe + t - 1) / t;
@@ -363,7 +390,6 @@ int pgh_b64_decode_into(const char* in, size_t n, uint8_t* out, size_t cap, size
     if (!m.done && m.quad_pos != 0) return PGH_E_PARSE;
     *written = n4 * 3 + tail.size();
     if (!out) return PGH_OK;
-    if (*written > cap) return PGH_E_STATE;
     if (d == fe) {  // clean prefix: whole quads straight from the input
         const int td = n4 < (1u << 16) ? 1 : t;
         const size_t pq = (n4 + td - 1) / td;
@@ -393,9 +419,5 @@ int pgh_b64_decode_into(const char* in, size_t n, uint8_t* out, size_t cap, size
     return PGH_OK;
 }
 
-// Decode `in` (n chars) into `out` (capacity >= pgh_b64_decoded_cap(n)); *written = bytes.
-int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int threads) {
-    return pgh_b64_decode_into(in, n, out, pgh_b64_decoded_cap(n), written, threads);
-}
 
 }  // extern "C"

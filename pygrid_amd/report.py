@@ -22,14 +22,13 @@ def b64decode(s, threads: int = 0) -> bytes:
     n = C.c_size_t(0)
     # one pass for a clean string: allocate the size its tail implies, decode (which checks the rest)
     if len(s) >= (1 << 16) and lib.pgh_b64_clean_size(s, len(s), C.byref(n)) == 0:
-        want = n.value
-        out, dst = _lib.fresh_bytes(want)
-        rc = lib.pgh_b64_decode_into(s, len(s), dst, want, C.byref(n), int(threads))
+        out, dst = _lib.fresh_bytes(n.value)
+        rc = lib.pgh_b64_decode_clean(s, len(s), dst, n.value, C.byref(n), int(threads))
         if rc == 0:
-            return out if n.value == want else out[:n.value]  # junk characters: shorter (rare)
+            return out
         if rc == -5:
             raise binascii.Error("Incorrect padding")
-        # PGH_E_STATE: junk made the text decode to more than its tail implied -- general route
+        # PGH_E_STATE: not clean (junk, line breaks): the general route
     if lib.pgh_b64_decode(s, len(s), None, C.byref(n), int(threads)) != 0:  # validate + exact size
         raise binascii.Error("Incorrect padding")
     out, dst = _lib.fresh_bytes(n.value)  # fresh, unshared bytes object: decoded into in place

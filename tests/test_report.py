@@ -141,11 +141,12 @@ def test_decode_into_capacity_and_clean_size():
     n = C.c_size_t(0)
     assert lib.pgh_b64_clean_size(enc, len(enc), C.byref(n)) == 0 and n.value == len(data)
     small = (C.c_uint8 * 10)()
-    assert lib.pgh_b64_decode_into(enc, len(enc), small, 10, C.byref(n), 1) == -3  # PGH_E_STATE
-    assert n.value == len(data)
+    assert lib.pgh_b64_decode_clean(enc, len(enc), small, 10, C.byref(n), 1) == -3  # PGH_E_STATE: too small
     buf = (C.c_uint8 * len(data))()
-    assert lib.pgh_b64_decode_into(enc, len(enc), buf, len(data), C.byref(n), 4) == 0
-    assert bytes(buf) == data
+    assert lib.pgh_b64_decode_clean(enc, len(enc), buf, len(data), C.byref(n), 4) == 0
+    assert bytes(buf) == data and n.value == len(data)
+    mime = base64.encodebytes(data)
+    assert lib.pgh_b64_decode_clean(mime, len(mime), buf, len(data), C.byref(n), 4) == -3  # not clean
     for junk in (b"**\n", b"*\n\r*"):  # the clean size is only a guess: decode_into checks it
         dirty = enc[:1000] + junk + enc[1000:]
         assert b64decode(dirty) == data
