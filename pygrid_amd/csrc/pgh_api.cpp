@@ -26,6 +26,8 @@
 // Python shim raises a PyGridError subclass, as tasks/cycle.py:33-37 expects).
 #include <emmintrin.h>
 #include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <unistd.h>
 
@@ -39,6 +41,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <fstream>
 #include <functional>
 #include <string>
 #include <thread>
@@ -80,6 +83,45 @@ void copy_stream(uint8_t* dst, const uint8_t* src, size_t n) {
     _mm_sfence();
 }
 
+// Bind the calling thread to `cpus` (no-op when empty or refused).
+void bind_thread(const std::vector<int>& cpus) {
+    if (cpus.empty()) return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (int c : cpus)
+        if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
+    (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+}
+
+// CPUs on the GPU's own socket (its PCI device's local_cpulist) that this process may run on; empty
+// when unknown.  Staging copies and pinned buffers there keep the host side of every H2D / D2H off
+// the socket interconnect (a 2-socket node: GPUs 0-3 on one socket, 4-7 on the other).
+std::vector<int> gpu_local_cpus(int device) {
+    std::vector<int> out;
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) { (void)hipGetLastError(); return out; }
+    std::string id(bus);
+    for (auto& ch : id) ch = (char)std::tolower((unsigned char)ch);
+    std::ifstream f("/sys/bus/pci/devices/" + id + "/local_cpulist");
+    std::string list;
+    if (!f || !std::getline(f, list)) return out;
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return out;
+    size_t pos = 0;
+    while (pos < list.size()) {
+        size_t end = list.find(',', pos);
+        if (end == std::string::npos) end = list.size();
+        const std::string r = list.substr(pos, end - pos);
+        const size_t dash = r.find('-');
+        const int a = std::atoi(r.c_str()), b = dash == std::string::npos ? a : std::atoi(r.c_str() + dash + 1);
+        for (int cpu = a; cpu <= b && cpu < CPU_SETSIZE; ++cpu)
+            if (cpu >= 0 && CPU_ISSET(cpu, &allowed)) out.push_back(cpu);
+        pos = end + 1;
+    }
+    return out;
+}
+
 class CopyPool {
   public:
     struct Seg {
@@ -87,8 +129,12 @@ class CopyPool {
         const uint8_t* src;
         size_t n;
     };
-    explicit CopyPool(int threads) : nthreads_(std::max(1, threads)) {
-        for (int t = 1; t < nthreads_; ++t) workers_.emplace_back([this, t] { loop(t); });
+    explicit CopyPool(int threads, std::vector<int> cpus = {}) : nthreads_(std::max(1, threads)) {
+        for (int t = 1; t < nthreads_; ++t)
+            workers_.emplace_back([this, t, cpus] {
+                bind_thread(cpus);
+                loop(t);
+            });
     }
     ~CopyPool() {
         {
@@ -246,6 +292,7 @@ struct pgh_ctx {
     bool pin_used[2] = {false, false};
     int pin_next = 0;
     int copy_threads = 8;
+    std::vector<int> local_cpus;  // PGH_NUMA (default on): the GPU's socket, for the copy pool + pinned ring
     std::unique_ptr<CopyPool> pool_copy;
     bool register_ingest = false;  // PGH_REGISTER_INGEST=1: page-lock State messages instead of staging
 
@@ -999,7 +1046,11 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     const unsigned hw = std::thread::hardware_concurrency();
     c->copy_threads = (int)std::max(1u, std::min(16u, hw ? hw : 1u));
     if (const char* e = std::getenv("PGH_COPY_THREADS")) c->copy_threads = std::max(1, std::atoi(e));
-    c->pool_copy.reset(new CopyPool(c->copy_threads));
+    {
+        const char* nu = std::getenv("PGH_NUMA");
+        if (!nu || std::atoi(nu) != 0) c->local_cpus = gpu_local_cpus(device);
+    }
+    c->pool_copy.reset(new CopyPool(c->copy_threads, c->local_cpus));
     if (const char* e = std::getenv("PGH_REGISTER_INGEST")) c->register_ingest = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_SYNTH_WGS")) c->synth_wgs = std::max(0LL, std::atoll(e));
     if (const char* e = std::getenv("PGH_BLOCK_BYTES")) c->block_bytes = (size_t)std::max(0LL, std::atoll(e));
@@ -1018,11 +1069,27 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
               hipEventCreateWithFlags(&c->pin_ev[0], hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->pin_ev[1], hipEventDisableTiming) == hipSuccess;
     if (!ok) { pgh_destroy(c); return fail(nullptr, PGH_E_HIP, "stream/event creation failed"); }
-    for (int k = 0; k < 2; ++k)
-        if (hipHostMalloc((void**)&c->h_pin[k], c->pin_slot, hipHostMallocDefault) != hipSuccess) {
+    {
+        // the pinned ring on the GPU's socket: allocated by a thread bound there, pages placed by
+        // its (local) memory policy
+        bool pin_ok = true;
+        auto alloc = [&] {
+            bind_thread(c->local_cpus);
+            const unsigned flags = c->local_cpus.empty() ? hipHostMallocDefault : hipHostMallocNumaUser;
+            for (int k = 0; k < 2 && pin_ok; ++k)
+                if (hipHostMalloc((void**)&c->h_pin[k], c->pin_slot, flags) != hipSuccess) {
+                    (void)hipGetLastError();
+                    c->h_pin[k] = nullptr;
+                    pin_ok = false;
+                }
+        };
+        if (c->local_cpus.empty()) alloc();
+        else std::thread([&] { DeviceGuard g2(device); alloc(); }).join();
+        if (!pin_ok) {
             pgh_destroy(c);
             return fail(nullptr, PGH_E_OOM, "pinned host allocation of %zu bytes failed", c->pin_slot);
         }
+    }
     // Warm-up (PGH_WARMUP=0 skips it): the first kernel launch loads the code object and the first
     // copies set up the runtime's copy engines (the first ~1 MB H2D from the pinned ring took 8.3 ms
     // of host time, r01ao) -- ~11 ms that would otherwise land on the node's first cycle close
@@ -2053,7 +2120,7 @@ int set_copy_threads(pgh_ctx* c, int n) {
     n = std::max(1, n);
     if (n == c->copy_threads && c->pool_copy) return PGH_OK;
     c->copy_threads = n;
-    c->pool_copy.reset(new CopyPool(n));
+    c->pool_copy.reset(new CopyPool(n, c->local_cpus));
     return PGH_OK;
 }
 int set_client_base(pgh_ctx* c, int64_t base) {
