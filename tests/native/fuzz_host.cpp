@@ -144,6 +144,56 @@ int main(int argc, char** argv) {
             if (pgh_b64_decode(txt, s.size(), out.data(), &w2, 1) != PGH_OK || w2 != w) { std::printf("b64 size mismatch\n"); return 4; }
         }
         delete[] txt;
+        // long, mostly clean base64 (the AVX2 fast path: 32-character blocks) with rare junk, decoded
+        // through pgh_b64_clean_size + pgh_b64_decode_clean into an exact-size heap buffer
+        {
+            const int blen = 32 + (int)(rng() % 400);
+            std::string t;
+            for (int k = 0; k < blen; ++k) t.push_back(rng() % 97 == 0 ? alpha[rng() % 67] : alpha[rng() % 64]);
+            char* bt = new char[t.size()];
+            std::memcpy(bt, t.data(), t.size());
+            size_t want = 0, w3 = 0;
+            if (pgh_b64_clean_size(bt, t.size(), &want) == PGH_OK) {
+                uint8_t* o = new uint8_t[want ? want : 1];
+                const int rc3 = pgh_b64_decode_clean(bt, t.size(), o, want, &w3, 1 + (int)(rng() % 3));
+                if (rc3 == PGH_OK && w3 != want) { std::printf("b64 clean size mismatch\n"); return 8; }
+                delete[] o;
+            }
+            size_t w4 = 0;
+            if (pgh_b64_decode(bt, t.size(), nullptr, &w4, 2) == PGH_OK) {
+                std::vector<uint8_t> o(pgh_b64_decoded_cap(t.size()));
+                size_t w5 = 0;
+                if (pgh_b64_decode(bt, t.size(), o.data(), &w5, 2) != PGH_OK || w5 != w4) { std::printf("b64 long mismatch\n"); return 9; }
+            }
+            delete[] bt;
+        }
+        // fresh checkpoint framing of a (mutated) template into an exact-size buffer
+        {
+            std::vector<uint8_t> tp = make_state(rng, 1 + (int)(rng() % 4));
+            if (rng() % 2 && !tp.empty()) tp[rng() % tp.size()] = (uint8_t)rng();
+            uint8_t* tb = new uint8_t[tp.size() ? tp.size() : 1];
+            if (!tp.empty()) std::memcpy(tb, tp.data(), tp.size());
+            int ntt = 0;
+            if (pgh_state_scan(tb, tp.size(), 0, nullptr, nullptr, &ntt) == PGH_OK && ntt <= 8) {
+                int64_t ids[16];
+                for (int k = 0; k < 2 * ntt; ++k) ids[k] = (int64_t)(rng() % 100000000000ull);
+                size_t need = 0, need2 = 0;
+                if (pgh_state_fresh(tb, tp.size(), ids, 2 * ntt, nullptr, 0, &need) == PGH_OK) {
+                    uint8_t* fo = new uint8_t[need ? need : 1];
+                    if (pgh_state_fresh(tb, tp.size(), ids, 2 * ntt, fo, need, &need2) != PGH_OK || need2 != need) {
+                        std::printf("fresh framing failed\n");
+                        return 10;
+                    }
+                    int nf = 0;  // the fresh framing scans back with the same tensor count
+                    if (pgh_state_scan(fo, need, 0, nullptr, nullptr, &nf) != PGH_OK || nf != ntt) {
+                        std::printf("fresh framing does not scan back\n");
+                        return 11;
+                    }
+                    delete[] fo;
+                }
+            }
+            delete[] tb;
+        }
     }
     std::printf("ok parsed=%d rejected=%d\n", parsed, rejected);
     return 0;
