@@ -316,6 +316,14 @@ struct pgh_ctx {
     bool prefault = true;  // PGH_PREFAULT: pre-fault big fresh checkpoint outputs in parallel (patch)
     bool warmup_skipped = false;  // pgh_create's warm-up failed (e.g. no device memory left): skipped
     int64_t vec_min = 0;      // [P_shard] device vectors at least this long (group collectives)
+    // Pipelined close: a resident fold's FINAL pass runs as final_split param ranges, each followed by
+    // an event; a D2H of the new checkpoint (patch / download) then runs on the copy stream, piece by
+    // piece behind the range that wrote it, so the HBM -> host copy overlaps the rest of the fold
+    // (PGH_FINAL_RANGES, default 4, shards of >= 1 M params).
+    struct RangeMark { int64_t end; hipEvent_t ev; };
+    std::vector<RangeMark> final_marks;
+    std::vector<hipEvent_t> rmark_pool;
+    int final_split = 4;
     int64_t client_base = 0;  // synthetic client k is generated as global client client_base + k
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
@@ -395,6 +403,8 @@ void free_slab(pgh_ctx* c) {
     (void)hipFree(c->d_ckpt); c->d_ckpt = nullptr;
     (void)hipFree(c->d_out); c->d_out = nullptr;
     c->ckpt_valid = false;
+    for (auto& m : c->final_marks) c->rmark_pool.push_back(m.ev);
+    c->final_marks.clear();
     (void)hipFree(c->d_acc); c->d_acc = nullptr;
     (void)hipFree(c->d_uacc); c->d_uacc = nullptr;
     (void)hipFree(c->d_sum); c->d_sum = nullptr;
@@ -654,13 +664,36 @@ void prefault_parallel(uint8_t* p, size_t n, CopyPool& pool) {
     });
 }
 
+// ---- pipelined close: range marks of the last resident fold ---------------------------------------
+void clear_final_marks(pgh_ctx* c) {
+    for (auto& m : c->final_marks) c->rmark_pool.push_back(m.ev);
+    c->final_marks.clear();
+}
+
+int add_final_mark(pgh_ctx* c, hipStream_t s, int64_t end) {
+    hipEvent_t e = nullptr;
+    if (!c->rmark_pool.empty()) { e = c->rmark_pool.back(); c->rmark_pool.pop_back(); }
+    else CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    CK(c, hipEventRecord(e, s));
+    c->final_marks.push_back({end, e});
+    return PGH_OK;
+}
+
+// Ranges of a FINAL fold pass: 1, or final_split 4-aligned ranges of the shard.
+int final_ranges(const pgh_ctx* c) { return c->final_split > 1 && c->pg >= (1 << 20) ? c->final_split : 1; }
+int64_t range_edge(const pgh_ctx* c, int k, int K) { return k >= K ? c->pg : (c->pg * k / K) & ~(int64_t)3; }
+
 // HBM bytes at `src` (after the work already on stream `s`) -> host pieces, through the pinned
 // ring: the DMA of one slot overlaps the host copy-out of the previous one.  `overlap`, if given,
 // is host work run while the first DMA is in flight (the checkpoint template's framing copy).
+// marks: src is the resident checkpoint: when its last fold left range marks, the DMAs run on the
+// copy stream, each behind the range that wrote its bytes (the rest of the fold continues).
 int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>& pieces, hipStream_t s,
-                     const std::function<void()>& overlap = nullptr) {
+                     const std::function<void()>& overlap = nullptr, bool marks = false) {
     size_t total = 0;
     for (auto& p : pieces) total += p.n;
+    const bool piped = marks && !c->final_marks.empty();
+    if (piped) s = c->copy;
     size_t off = 0;
     int prev_slot = -1;
     size_t prev_off = 0, prev_len = 0;
@@ -672,6 +705,11 @@ int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>
             c->pin_next ^= 1;
             if (c->pin_used[cur_slot]) CK(c, hipEventSynchronize(c->pin_ev[cur_slot]));
             cur_len = std::min({total - off, c->pin_slot, c->d2h_piece});
+            if (piped) {  // wait for the fold range holding the piece's last element
+                const int64_t last = (int64_t)((off + cur_len + 3) / 4);
+                for (auto& m : c->final_marks)
+                    if (m.end >= last) { CK(c, hipStreamWaitEvent(s, m.ev, 0)); break; }
+            }
             CK(c, hipMemcpyAsync(c->h_pin[cur_slot], src + off, cur_len, hipMemcpyDeviceToHost, s));
             CK(c, hipEventRecord(c->pin_ev[cur_slot], s));
             c->pin_used[cur_slot] = true;
@@ -1057,6 +1095,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_SHARE_FILL_MB")) c->share_fill = (size_t)std::max(1LL, std::atoll(e)) << 20;
     if (const char* e = std::getenv("PGH_NT_COPY")) c->nt_copy = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_PREFAULT")) c->prefault = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PGH_FINAL_RANGES")) c->final_split = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("PGH_D2H_PIECE_MB")) {
         const long long mb = std::atoll(e);
         c->d2h_piece = mb > 0 ? (size_t)mb << 20 : ~(size_t)0;
@@ -1143,6 +1182,7 @@ void pgh_destroy(pgh_ctx* c) {
     for (hipEvent_t e : {c->copy_done, c->xsync})
         if (e) (void)hipEventDestroy(e);
     for (auto e : c->fold_ev_pool) (void)hipEventDestroy(e);
+    for (auto e : c->rmark_pool) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
     delete c;
@@ -1578,6 +1618,7 @@ int pgh_synth_ckpt_device(pgh_ctx* c, uint64_t seed, float* d_ckpt, void* stream
     }
     if (!c->d_ckpt) return fail(c, PGH_E_STATE, "pgh_reserve has not been called");
     c->ckpt_valid = false;  // the resident checkpoint is used as scratch here
+    clear_final_marks(c);
     hipError_t e = pgh::launch_synth_f32(c->d_ckpt, pgh::single_block(c->pvec), c->pvec, 1, c->pg, seed,
                                          pgh::STREAM_CKPT, 0, c->lo, pgh::CKPT_SCALE, s);
     if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic checkpoint failed: %s", hipGetErrorString(e));
@@ -1647,6 +1688,7 @@ int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
     const size_t bytes = sizeof(float) * (size_t)c->pg;
     RC(order_before_overwrite(c));
     c->ckpt_valid = false;
+    clear_final_marks(c);
     RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
     c->ckpt_valid = true;
     RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
@@ -1674,6 +1716,7 @@ int pgh_ckpt_upload(pgh_ctx* c, const float* ckpt, size_t nbytes) {
     RC(order_before_overwrite(c));
     const uint8_t* src = (const uint8_t*)ckpt + (nbytes == whole ? 4 * (size_t)c->lo : 0);
     c->ckpt_valid = false;
+    clear_final_marks(c);
     RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), src, shard, is_pinned(ckpt)));
     c->ckpt_valid = true;
     return PGH_OK;
@@ -1690,6 +1733,7 @@ int pgh_ckpt_upload_state(pgh_ctx* c, const uint8_t* pb, size_t n) {
     DeviceGuard g(c->device);
     RC(order_before_overwrite(c));
     c->ckpt_valid = false;
+    clear_final_marks(c);
     RC(stage_pieces_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), pieces));
     c->ckpt_valid = true;
     return PGH_OK;
@@ -1699,9 +1743,27 @@ int pgh_fedavg_resident(pgh_ctx* c, int mode) {
     if (c && c->grp) return pgh_group_api::fedavg_resident(c, mode);
     RC(check_dtype(c, PGH_F32));
     RC(check_ckpt(c, "pgh_fedavg_resident"));
+    if (!valid_mode(mode)) return fail(c, PGH_E_ARG, "unknown averaging mode %d", mode);
     DeviceGuard g(c->device);
     const double t0 = now_ms();
-    RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
+    clear_final_marks(c);
+    const int K = final_ranges(c);
+    if (K == 1) {
+        RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
+    } else {  // the same fold as K range launches, each followed by its mark (pipelined close)
+        int64_t n = 0;
+        RC(resident_count(c, &n));
+        FinalArgs fa;
+        fa.ckpt = c->d_ckpt;
+        fa.out = c->d_out;
+        RC(fedavg_divisor(c, mode, n, &fa.divisor));
+        for (int k = 0; k < K; ++k) {
+            fa.off = range_edge(c, k, K);
+            fa.len = range_edge(c, k + 1, K) - fa.off;
+            RC(fold_run(c, mode, 0, n, true, fa, c->stream));
+            RC(add_final_mark(c, c->stream, fa.off + fa.len));
+        }
+    }
     std::swap(c->d_ckpt, c->d_out);  // the new checkpoint is the next cycle's input
     c->st.close_ms_last = now_ms() - t0;
     return PGH_OK;
@@ -1719,7 +1781,7 @@ int pgh_ckpt_download(pgh_ctx* c, float* out) {
         CK(c, hipMemcpyAsync(out, c->d_ckpt, bytes, hipMemcpyDeviceToHost, c->stream));
         CK(c, hipStreamSynchronize(c->stream));
     } else {
-        RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, {OutPiece{(uint8_t*)out, bytes}}, c->stream));
+        RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, {OutPiece{(uint8_t*)out, bytes}}, c->stream, nullptr, true));
     }
     return collect_timings(c);
 }
@@ -1756,7 +1818,7 @@ int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out
         if (c->prefault) prefault_parallel(out, n, *c->pool_copy);
         else prefault_small(out, n);
         if (!gaps.empty()) c->pool_copy->run(gaps);
-    }));
+    }, true));
     return collect_timings(c);
 }
 
@@ -1854,7 +1916,6 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
         RC(sync_weights(c, s));
     }
     if (mode == PGH_ITERATIVE_MEAN && n > 0) RC(ensure_recips(c, total, s));
-    const uint64_t pg = (uint64_t)c->pg;
     int done = 0;
     do {
         const int m = std::min(n - done, pgh::ROWTAB_MAX);
@@ -1876,8 +1937,22 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
         a.flags = (first ? pgh::FL_FIRST : 0) | (final && last ? pgh::FL_FINAL : 0);
         a.mode = mode;
         a.variant = c->variant;
-        const uint64_t bytes = 4ull * (uint64_t)m * pg + (first ? 0 : 4 * pg) + ((a.flags & pgh::FL_FINAL) ? 8 * pg : 4 * pg);
-        RC(timed_launch(c, s, bytes, [&] { return pgh::launch_fedavg_rows(a, tab, s); }));
+        // the FINAL pass as K param ranges, each followed by its mark (pipelined close)
+        const int K = (a.flags & pgh::FL_FINAL) ? final_ranges(c) : 1;
+        if (a.flags & pgh::FL_FINAL) clear_final_marks(c);
+        for (int r = 0; r < K; ++r) {
+            const int64_t lo = K == 1 ? 0 : range_edge(c, r, K), hi = K == 1 ? c->pg : range_edge(c, r + 1, K);
+            pgh::FedavgArgs ar = a;
+            ar.map.off = lo;
+            ar.p = hi - lo;
+            ar.acc = c->d_acc + lo;
+            ar.ckpt = c->d_ckpt + lo;
+            ar.out = c->d_out + lo;
+            const uint64_t rp = (uint64_t)(hi - lo);
+            const uint64_t bytes = 4ull * (uint64_t)m * rp + (first ? 0 : 4 * rp) + ((a.flags & pgh::FL_FINAL) ? 8 * rp : 4 * rp);
+            RC(timed_launch(c, s, bytes, [&] { return pgh::launch_fedavg_rows(ar, tab, s); }));
+            if (K > 1) RC(add_final_mark(c, s, hi));
+        }
         done += m;
     } while (done < n);
     RC(record_fold(c, s));
@@ -1971,6 +2046,7 @@ int pgh_stream_finish_resident(pgh_ctx* c) {
     RC(check_dtype(c, PGH_F32));
     RC(check_ckpt(c, "pgh_stream_finish_resident"));
     DeviceGuard g(c->device);
+    clear_final_marks(c);
     const double t0 = now_ms();
     RC(pgh_stream_finish_device(c, c->d_ckpt, c->d_out, c->stream));
     std::swap(c->d_ckpt, c->d_out);  // the new checkpoint is the next cycle's input
@@ -1990,6 +2066,7 @@ int pgh_stream_finish(pgh_ctx* c, const float* ckpt, float* out) {
     // pgh_ckpt_upload's last ring DMA can no longer land after this copy)
     RC(order_before_overwrite(c));
     c->ckpt_valid = false;
+    clear_final_marks(c);
     RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
     c->ckpt_valid = true;
     RC(pgh_stream_finish_device(c, c->d_ckpt, c->d_out, c->stream));
@@ -2150,7 +2227,7 @@ int patch_payloads(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out) {
             const size_t a = spans.front().first, b = spans.back().first + spans.back().second;
             if (b > a) prefault_parallel(out + a, b - a, *c->pool_copy);
         }
-    }));
+    }, true));
     return collect_timings(c);
 }
 }  // namespace pgh_int
