@@ -1115,12 +1115,17 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
         auto alloc = [&] {
             bind_thread(c->local_cpus);
             const unsigned flags = c->local_cpus.empty() ? hipHostMallocDefault : hipHostMallocNumaUser;
-            for (int k = 0; k < 2 && pin_ok; ++k)
-                if (hipHostMalloc((void**)&c->h_pin[k], c->pin_slot, flags) != hipSuccess) {
-                    (void)hipGetLastError();
-                    c->h_pin[k] = nullptr;
-                    pin_ok = false;
-                }
+            for (int k = 0; k < 2 && pin_ok; ++k) {
+                if (hipHostMalloc((void**)&c->h_pin[k], c->pin_slot, flags) == hipSuccess) continue;
+                (void)hipGetLastError();
+                // a placement the runtime refuses is not worth failing the context for
+                if (flags != hipHostMallocDefault &&
+                    hipHostMalloc((void**)&c->h_pin[k], c->pin_slot, hipHostMallocDefault) == hipSuccess)
+                    continue;
+                (void)hipGetLastError();
+                c->h_pin[k] = nullptr;
+                pin_ok = false;
+            }
         };
         if (c->local_cpus.empty()) alloc();
         else std::thread([&] { DeviceGuard g2(device); alloc(); }).join();
