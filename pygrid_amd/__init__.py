@@ -10,12 +10,13 @@ The product is ``libpygrid_hip.so`` (C ABI: ``include/pgh_api.h``; gfx950 HIP ke
 
 Nothing here computes on the CPU: without the built library and a GPU the engine raises.
 """
-from .exceptions import (AggregationError, EngineUnavailableError, PlanNotAcceleratedError, PyGridError,
-                         StateParseError)
+from .exceptions import (AggregationError, EngineUnavailableError, ModelNotAcceleratedError, PlanNotAcceleratedError,
+                         PyGridError, StateParseError)
 from .engine import F32, I64, ITERATIVE_MEAN, MEAN, STREAM_SECAGG, WEIGHTED_MEAN, Engine, PinnedBuffer, device_count
 
 __all__ = [
-    "AggregationError", "EngineUnavailableError", "PlanNotAcceleratedError", "PyGridError", "StateParseError",
+    "AggregationError", "EngineUnavailableError", "ModelNotAcceleratedError", "PlanNotAcceleratedError", "PyGridError",
+    "StateParseError",
     "Engine", "PinnedBuffer", "device_count", "STREAM_SECAGG", "MEAN", "ITERATIVE_MEAN", "WEIGHTED_MEAN", "F32", "I64",
 ]
 __version__ = "0.1.0"

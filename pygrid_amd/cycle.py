@@ -23,7 +23,7 @@ import numpy as np
 
 from . import state as state_codec
 from .engine import ITERATIVE_MEAN, MEAN, WEIGHTED_MEAN, F32, I64, Engine
-from .exceptions import AggregationError, PlanNotAcceleratedError
+from .exceptions import AggregationError, ModelNotAcceleratedError, PlanNotAcceleratedError, StateParseError
 
 
 def ready_to_average(server_config: dict, received_diffs: int, cycle_end=None, now=None) -> bool:
@@ -138,6 +138,21 @@ def select_mode(server_config: dict, avg_plan: Optional[Callable] = None, weight
     return ITERATIVE_MEAN
 
 
+def _decline_non_float32(pb: bytes, what: str):
+    """After the State walker refused ``pb``: well-formed bytes holding non-float32 tensors are a
+    model the engine does not implement (``ModelNotAcceleratedError``: the node averages it with
+    its own code, cycle_manager.py:240-303, torch type promotion included); anything else is
+    malformed and the caller re-raises the parse error."""
+    from . import state_schema
+
+    try:
+        bad = state_schema.non_float32_tensors(pb)
+    except ValueError:
+        return
+    if bad:
+        raise ModelNotAcceleratedError(f"{what} holds non-float32 tensors {bad[:8]} (the engine is fp32-only)")
+
+
 class CycleAggregator:
     """Owns one Engine across cycles; the slab is re-used while it fits.  ``devices=[0, ..., 7]``
     gives the node's single process every GPU of the node (``pgh_create_group``: parameter shards,
@@ -179,12 +194,20 @@ class CycleAggregator:
         if len(diffs) == 0:
             raise AggregationError("no diffs to average")
         mode = select_mode(server_config, avg_plan, weights)
-        numel = state_codec.tensor_numels(checkpoint)  # :240
+        try:
+            numel = state_codec.tensor_numels(checkpoint)  # :240
+        except StateParseError:
+            _decline_non_float32(checkpoint, "the checkpoint")
+            raise
         self._prepare(numel, len(diffs))
         if checkpoint is not self._resident or self.engine.ckpt_owner is not self:
             self.engine.ckpt_upload_state(checkpoint)  # else: the last cycle's output is still in HBM
         for i, d in enumerate(diffs):  # :247-250
-            self.engine.ingest_state(i, d)
+            try:
+                self.engine.ingest_state(i, d)
+            except StateParseError:
+                _decline_non_float32(d, f"diff {i}")
+                raise
         if mode == WEIGHTED_MEAN:
             self.engine.set_weights(weights)
         # From the fold on, HBM holds the NEW checkpoint: until its bytes exist, nobody may take the

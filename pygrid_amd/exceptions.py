@@ -33,3 +33,10 @@ class PlanNotAcceleratedError(PyGridError):
     """The hosted avg plan is not one the engine implements (user-defined non-iterative plan,
     or an iterative plan that does not match ``(avg * num + item) / (num + 1)``).  The caller
     keeps running the reference's own CPU path for it."""
+
+
+class ModelNotAcceleratedError(PlanNotAcceleratedError):
+    """The checkpoint or a diff holds well-formed tensors that are not float32 (another dtype, or a
+    serializer other than syft's "all").  The reference averages them with torch's type promotion;
+    the engine is fp32-only, so the caller runs the reference path for this cycle, as for an
+    unaccelerated plan (malformed bytes still raise ``StateParseError``)."""

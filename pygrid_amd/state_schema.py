@@ -333,6 +333,51 @@ def tensor_shapes(pb: bytes):
     return shapes
 
 
+def tensor_dtypes(pb: bytes):
+    """Per tensor of a State message, State order: the TensorData dtype string and the numbers of the
+    contents fields present (10 int64, 12 float32, 13 float64; 3 = TorchTensor.contents_bin, a
+    serializer other than "all"), from the framing alone.  ValueError on bytes that are not a
+    State."""
+    b = memoryview(pb)
+    out = []
+    for num, wt, v in _fields(b, 0, len(b)):
+        if num != 2 or wt != 2:  # State.tensors
+            continue
+        tt = None
+        for n2, w2, v2 in _fields(b, *v):
+            if n2 == 1 and w2 == 2:
+                tt = v2
+            elif n2 == 2 and w2 == 2:
+                for n3, w3, v3 in _fields(b, *v2):
+                    if n3 == 2 and w3 == 2:
+                        tt = v3
+        dtype, contents = "", set()
+        if tt is not None:
+            for n3, w3, v3 in _fields(b, *tt):
+                if n3 == 3 and w3 == 2:  # TorchTensor.contents_bin
+                    contents.add(3)
+                elif n3 == 4 and w3 == 2:  # TorchTensor.contents_data -> TensorData
+                    for n4, w4, v4 in _fields(b, *v3):
+                        if n4 == 2 and w4 == 2:
+                            dtype = bytes(b[v4[0]:v4[1]]).decode("utf-8", "replace")
+                        elif n4 in (10, 12, 13):
+                            contents.add(n4)
+        out.append((dtype, frozenset(contents)))
+    return out
+
+
+def non_float32_tensors(pb: bytes):
+    """Indices of the tensors of a State message that are well-formed but not float32 (another
+    dtype, float64 / int64 contents, or a non-"all" serializer's binary blob): the reference
+    averages those with torch's type promotion, the engine does not.  ValueError on bytes that are
+    not a State."""
+    bad = []
+    for k, (dtype, contents) in enumerate(tensor_dtypes(pb)):
+        if dtype not in ("", "float32", "torch.float32") or not contents <= {12}:
+            bad.append(k)
+    return bad
+
+
 _ID_RNG = None
 
 

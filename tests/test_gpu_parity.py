@@ -793,3 +793,35 @@ def test_non_iterative_mean_plan_is_accelerated(engine):
     with pytest.raises(PlanNotAcceleratedError):
         agg.average_plan_diffs({}, build_state_fast(ckpt), [build_state_fast(d) for d in diffs],
                                avg_plan=lambda ds: [th.stack(list(col)).mean(0) for col in zip(*ds)])
+
+
+def test_float64_diff_declines_and_leaves_the_aggregator_usable(engine):
+    """A diff holding a float64 tensor (well-formed: the reference would average it with torch's
+    type promotion) is declined mid-ingest (ModelNotAcceleratedError: the node runs its own code
+    for the cycle); the same aggregator then closes a float32 cycle bit-exactly, its resident
+    checkpoint untouched by the declined one."""
+    from pygrid_amd import ModelNotAcceleratedError
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.state_schema import build_state_fast, classes, parse_state
+
+    rng = np.random.default_rng(13)
+    shapes = [(300, 7), (7,)]
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for _ in range(4)]
+    st = classes()["State"]()
+    st.ParseFromString(build_state_fast(diffs[2]))
+    td = st.tensors[1].torch_tensor.contents_data
+    vals = list(td.contents_float32)
+    td.ClearField("contents_float32")
+    td.dtype = "float64"
+    td.contents_float64.extend(vals)
+    bad = st.SerializeToString()
+    agg = CycleAggregator(engine)
+    ck_pb = build_state_fast(ckpt)
+    first = agg.average_plan_diffs({}, ck_pb, [build_state_fast(d) for d in diffs])  # resident now
+    with pytest.raises(ModelNotAcceleratedError):
+        agg.average_plan_diffs({}, first, [build_state_fast(diffs[0]), build_state_fast(diffs[1]), bad])
+    new = agg.average_plan_diffs({}, first, [build_state_fast(d) for d in diffs])
+    want = O.fedavg_mean(O.fedavg_mean(ckpt, diffs), diffs)
+    for got, w in zip(parse_state(new), want):
+        assert same(got, w)

@@ -176,6 +176,78 @@ def test_wiring_iterative_plan_accelerated_and_fl_done():
     assert agg.calls[0][2] is canonical_plan and saved == [(7, b"NEW")] and created == []
 
 
+def _state_with(kinds):
+    """State bytes via google.protobuf with one tensor per entry of ``kinds``: "f32", "f64", "i64",
+    "bin" (TorchTensor.contents_bin), "f32-as-param"."""
+    st = classes()["State"]()
+    for k, kind in enumerate(kinds):
+        st.placeholders.add().id.id_int = 10 + k
+        stt = st.tensors.add()
+        tt = stt.torch_param.tensor if kind == "f32-as-param" else stt.torch_tensor
+        tt.id.id_int = 10 + k
+        tt.serializer = 4
+        if kind == "bin":
+            tt.contents_bin = b"\x80\x02torch-blob"
+            continue
+        tt.contents_data.shape.dims.extend([3])
+        if kind in ("f32", "f32-as-param"):
+            tt.contents_data.dtype = "float32"
+            tt.contents_data.contents_float32.extend([1.0, -2.0, 0.5])
+        elif kind == "f64":
+            tt.contents_data.dtype = "float64"
+            tt.contents_data.contents_float64.extend([1.0, -2.0, 0.5])
+        else:
+            tt.contents_data.dtype = "int64"
+            tt.contents_data.contents_int64.extend([1, -2, 5])
+    return st.SerializeToString()
+
+
+@pytest.mark.parametrize("kinds,bad", [(["f32", "f32-as-param"], []), (["f32", "f64"], [1]), (["i64", "f32"], [0]),
+                                       (["bin"], [0]), (["f64", "i64", "bin"], [0, 1, 2])])
+def test_non_float32_tensors_found_from_framing(kinds, bad):
+    from pygrid_amd import state_schema
+
+    pb = _state_with(kinds)
+    assert state_schema.non_float32_tensors(pb) == bad
+    if bad:  # the walker the engine uses refuses them
+        with pytest.raises(StateParseError):
+            state.scan(pb)
+    with pytest.raises(ValueError):
+        state_schema.non_float32_tensors(pb[:-2])  # cut-off bytes are malformed, not "another dtype"
+
+
+class _NoEngine:
+    """Engine stand-in for dispatch tests that must decline before any engine call."""
+    ckpt_owner = None
+
+    def __getattr__(self, name):
+        raise AssertionError(f"engine.{name} touched")
+
+
+def test_non_float32_checkpoint_declined_before_the_engine():
+    from pygrid_amd import ModelNotAcceleratedError
+
+    agg = cycle.CycleAggregator(engine=_NoEngine())
+    with pytest.raises(ModelNotAcceleratedError):
+        agg.average_plan_diffs({}, _state_with(["f32", "f64"]), [_state_with(["f32", "f32"])])
+    with pytest.raises(StateParseError):  # malformed bytes still raise the parse error
+        agg.average_plan_diffs({}, _state_with(["f32", "f32"])[:-3], [_state_with(["f32", "f32"])])
+
+
+def test_wiring_declines_non_float32_models_to_the_reference():
+    from pygrid_amd import ModelNotAcceleratedError
+
+    class Refusing(FakeAggregator):
+        def average_plan_diffs(self, *a, **k):
+            raise ModelNotAcceleratedError("float64 model")
+
+    mm, pm, plm, self_, cyc, saved, created = _fake_node()
+    ran = []
+    fn = cycle.make_average_plan_diffs(Refusing(), mm, pm, plm, original=lambda s, cfg, c: ran.append(c))
+    fn(self_, {}, cyc)
+    assert ran == [cyc] and saved == [] and not cyc.is_completed
+
+
 # ---- State codec (host-only C++) -----------------------------------------------------------------
 SHAPES = [(392, 784), (392,), (10, 392), (10,)]
 
