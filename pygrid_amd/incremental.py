@@ -28,7 +28,10 @@ thread (``tasks/cycle.py``), so every method holds the cycle's lock (the engine 
 single-owner).  A report that arrives after ``close`` started raises ``AggregationError`` -- the
 reference likewise averages only the diffs its query saw (``cycle_manager.py:243-245``).  A
 malformed diff is rejected in its own ``reported`` call (``StateParseError``, nothing recorded),
-so one bad client cannot break the cycle for the others.
+so one bad client cannot break the cycle for the others.  A well-formed diff holding non-float32
+tensors is accepted (the reference would average it with torch's type promotion): the cycle is
+then declined as a whole -- later reports are only recorded, and ``close`` raises
+``ModelNotAcceleratedError`` so the node averages the cycle with its own code, from its DB.
 
 The checkpoint can be handed over when the cycle starts (``checkpoint=``): its payloads are then
 uploaded into HBM while clients report, and ``close`` touches only the rows not folded yet.
@@ -40,7 +43,7 @@ from typing import Dict, List, Optional
 
 from . import state as state_codec
 from .engine import F32, MEAN, Engine
-from .exceptions import AggregationError, StateParseError
+from .exceptions import AggregationError, ModelNotAcceleratedError, StateParseError
 
 DEFAULT_HBM_BUDGET = 64 << 30  # bytes of diffs kept in HBM per cycle when `slots` is not given
 MAX_DEFAULT_SLOTS = 4096
@@ -74,6 +77,7 @@ class IncrementalCycle:
         self.folded_early = 0
         self._lock = threading.Lock()
         self._closed = False
+        self._declined: Optional[str] = None  # why the engine cannot average this cycle
         # keep the engine's slab when a cycle of the same model follows (no re-allocation)
         if tuple(getattr(engine, "numel", ())) != self._numel or getattr(engine, "max_clients", 0) != self.slots \
                 or getattr(engine, "dtype", None) != F32:
@@ -84,7 +88,11 @@ class IncrementalCycle:
         self._ckpt: Optional[bytes] = None  # checkpoint bytes whose payloads are resident in HBM
         if checkpoint is not None:
             engine.ckpt_owner = None
-            engine.ckpt_upload_state(checkpoint)
+            try:
+                engine.ckpt_upload_state(checkpoint)
+            except StateParseError:
+                _raise_if_not_float32(checkpoint, "the checkpoint")
+                raise
             engine.ckpt_owner = self
             self._ckpt = checkpoint
 
@@ -103,13 +111,26 @@ class IncrementalCycle:
                 raise AggregationError(f"worker {worker!r} reported without being assigned to the cycle")
             if worker in self._reported:
                 raise AggregationError(f"worker {worker!r} reported twice")
+            if self._declined:
+                self._reported.add(worker)  # the node averages this cycle itself
+                return
             front = self._pos[worker] == self._front
-            # a diff that cannot fold yet leaves one slot free for the fold front
-            if self._free and (front or len(self._free) > 1):
-                self._to_hbm(worker, diff)  # raises StateParseError on a malformed diff: nothing recorded
-            else:
-                self._check_layout(worker, diff)
-                self._parked[worker] = diff
+            try:
+                # a diff that cannot fold yet leaves one slot free for the fold front
+                if self._free and (front or len(self._free) > 1):
+                    self._to_hbm(worker, diff)  # raises StateParseError on a malformed diff: nothing recorded
+                else:
+                    self._check_layout(worker, diff)
+                    self._parked[worker] = diff
+            except StateParseError:
+                try:
+                    _raise_if_not_float32(diff, f"worker {worker!r}'s diff")
+                except ModelNotAcceleratedError as e:
+                    self._declined = str(e)
+                    self._parked.clear()
+                    self._reported.add(worker)
+                    return
+                raise
             self._reported.add(worker)
             self._advance(final=False)
 
@@ -164,6 +185,8 @@ class IncrementalCycle:
             if self._closed:
                 raise AggregationError("cycle already closed")
             self._closed = True
+            if self._declined:
+                raise ModelNotAcceleratedError(self._declined)
             self._advance(final=True)
             if self._n_folded + len(self._ready) == 0:
                 raise AggregationError("no diffs to average")
@@ -180,6 +203,12 @@ class IncrementalCycle:
             return new
 
     @property
+    def declined(self) -> Optional[str]:
+        """Why the engine will not average this cycle (``close`` raises ``ModelNotAcceleratedError``),
+        or None."""
+        return self._declined
+
+    @property
     def n_folded(self) -> int:
         return self._n_folded
 
@@ -187,3 +216,9 @@ class IncrementalCycle:
     def n_parked(self) -> int:
         """Reported diffs waiting on the host because every HBM slot was taken."""
         return len(self._parked)
+
+
+def _raise_if_not_float32(pb: bytes, what: str):
+    from .cycle import _decline_non_float32
+
+    _decline_non_float32(pb, what)

@@ -242,3 +242,63 @@ def test_reports_from_many_threads_and_a_late_one():
         inc.reported(0, b"late")
     with pytest.raises(AggregationError):
         inc.close(b"ck", framing="template")
+
+
+class ScanningEngine(RecordingEngine):
+    """ingest_state / ckpt_upload_state refuse what the real State walker refuses."""
+
+    def ingest_state(self, k, pb):
+        from pygrid_amd import state
+
+        state.scan(pb)
+        super().ingest_state(k, pb)
+
+    def ckpt_upload_state(self, pb):
+        from pygrid_amd import state
+
+        state.scan(pb)
+        super().ckpt_upload_state(pb)
+
+
+def _f64_diff():
+    from pygrid_amd.state_schema import classes
+
+    st = classes()["State"]()
+    st.ParseFromString(mk(9))
+    td = st.tensors[0].torch_tensor.contents_data
+    td.ClearField("contents_float32")
+    td.dtype = "float64"
+    td.contents_float64.extend([9.0, 9.0, 9.0])
+    return st.SerializeToString()
+
+
+@pytest.mark.parametrize("parked", [False, True])
+def test_float64_diff_declines_the_cycle_not_the_worker(parked):
+    """A well-formed float64 diff (the reference averages it with torch's type promotion) is
+    accepted; the cycle is declined as a whole, later reports are only recorded, and close raises
+    ModelNotAcceleratedError so the node averages the cycle itself.  A truncated diff is still
+    refused to its sender."""
+    from pygrid_amd import ModelNotAcceleratedError
+
+    eng = ScanningEngine()
+    inc = IncrementalCycle(eng, [3], slots=2 if parked else 8, fold_batch=1)
+    for w in range(5):
+        inc.assigned(w)
+    with pytest.raises(StateParseError):
+        inc.reported(0, mk(0)[:-2])
+    if parked:  # worker 3's diff waits on the host (no free slot for a non-front diff): scanned there
+        inc.reported(2, mk(2))
+    inc.reported(3, _f64_diff())
+    assert inc.declined and "non-float32" in inc.declined
+    n_ingests = sum(c[0] == "ingest" for c in eng.calls)
+    inc.reported(4, mk(4))
+    assert sum(c[0] == "ingest" for c in eng.calls) == n_ingests  # recorded, not ingested
+    with pytest.raises(ModelNotAcceleratedError):
+        inc.close(mk(7), framing="template")
+
+
+def test_float64_checkpoint_declined_at_cycle_start():
+    from pygrid_amd import ModelNotAcceleratedError
+
+    with pytest.raises(ModelNotAcceleratedError):
+        IncrementalCycle(ScanningEngine(), [3], slots=4, checkpoint=_f64_diff())
