@@ -543,7 +543,8 @@ def run_secagg_clients(ctx, args, eng, N, S, P):
 
 def run_c4(ctx, args, eng, N, pg, P):
     """Config 4 shard: N clients streamed through an R-slot ring; each chunk generated on the GPU
-    (stand-in for arriving data), folded in client order while the next chunk is generated."""
+    (stand-in for arriving data) and folded in client order, generator and fold alternating on one
+    stream (PGH_SYNTH_SERIAL=0 runs the generator beside the fold instead)."""
     torch = ctx.torch
     from pygrid_amd.sharding import gather_flat
 
@@ -574,8 +575,8 @@ def run_c4(ctx, args, eng, N, pg, P):
            "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
            "kernel_variant": eng.effective_variant()}
     extra = {"fold_kernel_client_diff_GBps_aggregated": round(kern_gbs, 1),
-             "note": "value includes on-device generation of every chunk (writes 4 B/param/client) "
-                     "competing for HBM with the fold; the fold kernels alone are fold_kernel_*"}
+             "note": "value includes on-device generation of every chunk (writes 4 B/param/client, "
+                     "alternating with the fold); the fold kernels alone are fold_kernel_*"}
     rec = record(ctx, args, "c4-stream", value, el, "f32", cfg,
                  roofline_of(st, "c4-stream", cfg["kernel_variant"], "k_fedavg"), extra)
     return attach_cpu_baseline(ctx, args, rec, "mean", pg, n=8,

@@ -265,6 +265,11 @@ struct pgh_ctx {
     size_t block_bytes = 256u << 10;  // PGH_BLOCK_BYTES; 0 = one block (plain row-major rows)
     int synth_kind = 0;        // pgh_set_synth_kind: generator of synthetic diffs (0 Irwin-Hall, 1 fast)
     int64_t synth_wgs = 8192;  // PGH_SYNTH_WGS: STREAM synthetic fill grid cap (0 = a grid row per row; r01t)
+    // STREAM synthetic fills run on the fold stream, generator and fold alternating with the whole
+    // GPU each (PGH_SYNTH_SERIAL=0: beside the fold on the copy stream; the write-heavy fill and the
+    // read-only fold then share HBM 13 % worse, r02p), with non-temporal stores (PGH_SYNTH_NT)
+    bool synth_serial = true;
+    bool synth_nt = true;
 
     int slots = 0, dtype = PGH_F32, parties = 1;
     void* d_slab = nullptr;
@@ -1091,6 +1096,8 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     c->pool_copy.reset(new CopyPool(c->copy_threads, c->local_cpus));
     if (const char* e = std::getenv("PGH_REGISTER_INGEST")) c->register_ingest = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_SYNTH_WGS")) c->synth_wgs = std::max(0LL, std::atoll(e));
+    if (const char* e = std::getenv("PGH_SYNTH_SERIAL")) c->synth_serial = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PGH_SYNTH_NT")) c->synth_nt = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_BLOCK_BYTES")) c->block_bytes = (size_t)std::max(0LL, std::atoll(e));
     if (const char* e = std::getenv("PGH_SHARE_FILL_MB")) c->share_fill = (size_t)std::max(1LL, std::atoll(e)) << 20;
     if (const char* e = std::getenv("PGH_NT_COPY")) c->nt_copy = std::atoi(e) != 0;
@@ -1572,13 +1579,14 @@ int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
         }
         if (c->streaming && run > 1) RC(order_stream_overwrite(c, client + run - 1));
         hipError_t e;
+        const hipStream_t gs = c->streaming && c->synth_serial ? c->stream : c->copy;
         if (c->dtype == PGH_F32)
             e = pgh::launch_synth_f32((float*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->pg, seed,
-                                      pgh::STREAM_DIFF, c->client_base + client, c->lo, pgh::DIFF_SCALE, c->copy,
-                                      c->streaming ? c->synth_wgs : 0, c->synth_kind);
+                                      pgh::STREAM_DIFF, c->client_base + client, c->lo, pgh::DIFF_SCALE, gs,
+                                      c->streaming ? c->synth_wgs : 0, c->synth_kind, c->synth_nt);
         else
             e = pgh::launch_synth_shares((int64_t*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->parties,
-                                         c->pg, seed, c->client_base + client, c->lo, 1000.0f, c->copy);
+                                         c->pg, seed, c->client_base + client, c->lo, 1000.0f, gs);
         if (e != hipSuccess) return fail(c, PGH_E_HIP, "synthetic fill failed: %s", hipGetErrorString(e));
         for (int j = 0; j < run; ++j) {
             if (c->slot_client[(size_t)(slot + j)] != client + j) c->st.n_clients += 1;

@@ -81,7 +81,8 @@ int auto_variant(int64_t p, int mode);
 hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_rows, int64_t p, uint64_t seed,
                             uint64_t stream_id, int64_t row0, int64_t idx0, float scale, hipStream_t s,
                             int64_t max_wgs = 0,  // > 0: cap the grid at max_wgs workgroups
-                            int kind = 0);        // 0 Irwin-Hall per param, 1 fast (4 params per word)
+                            int kind = 0,         // 0 Irwin-Hall per param, 1 fast (4 params per word)
+                            bool nt = false);     // non-temporal stores
 // dec[i] = float32(int64 sum[i]) / divisor for i < n (decode after a cross-rank share-sum reduction).
 hipError_t launch_secagg_decode(const int64_t* sum, float* dec, int64_t n, float divisor, hipStream_t s);
 hipError_t launch_synth_shares(int64_t* out, const SlabMap& m, int64_t ncols, int n_clients, int n_parties,

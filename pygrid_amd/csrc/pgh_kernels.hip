@@ -426,7 +426,9 @@ __global__ __launch_bounds__(BLOCK) void k_secagg_decode(const int64_t* sum, flo
 // on-device data source): one word per 4 consecutive params (global index g >> 2), param g takes
 // u16 number g & 3 of it, centred, times 2 * scale (same sigma ~ 1e-2): a quarter of the integer
 // work, so the fill is bound by its HBM writes instead of the 64-bit multiplies (r01af).
-template <int KIND>
+// NT: non-temporal stores (the rows are read back by a fold only after the whole chunk is written:
+// nothing to keep in L2 / MALL).
+template <int KIND, bool NT>
 __global__ __launch_bounds__(BLOCK) void k_synth_f32(float* out, SlabMap m, int64_t ncols, int n_rows, int64_t p,
                                                      uint64_t seed, uint64_t stream_id, int64_t row0, int64_t idx0,
                                                      float scale) {
@@ -462,7 +464,9 @@ __global__ __launch_bounds__(BLOCK) void k_synth_f32(float* out, SlabMap m, int6
                     }
                 }
             }
-            *reinterpret_cast<f32x4*>(row + m.at(4 * q)) = v;  // 4 params never straddle a block
+            f32x4* dst = reinterpret_cast<f32x4*>(row + m.at(4 * q));  // 4 params never straddle a block
+            if constexpr (NT) __builtin_nontemporal_store(v, dst);
+            else *dst = v;
         }
     }
 }
@@ -791,7 +795,7 @@ hipError_t launch_secagg(const SecaggArgs& a, hipStream_t s) {
 
 hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_rows, int64_t p, uint64_t seed,
                             uint64_t stream_id, int64_t row0, int64_t idx0, float scale, hipStream_t s,
-                            int64_t max_wgs, int kind) {
+                            int64_t max_wgs, int kind, bool nt) {
     if (!out || n_rows < 0 || n_rows > 65535 || ncols < p || (ncols & 3) || m.off != 0 || !valid_map(m, 0) ||
         (kind != 0 && kind != 1) ||
         (m.bshift == 62 && ncols > m.ld) || (reinterpret_cast<uintptr_t>(out) & 15))
@@ -804,12 +808,15 @@ hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_r
         if (gx > max_wgs) gx = max_wgs;
         gy = std::max<int64_t>(1, std::min<int64_t>(n_rows, max_wgs / gx));
     }
-    if (kind == 1)
-        k_synth_f32<1><<<dim3((unsigned)gx, (unsigned)gy), BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id,
-                                                                         row0, idx0, scale);
+    const dim3 grid((unsigned)gx, (unsigned)gy);
+    if (kind == 1 && nt)
+        k_synth_f32<1, true><<<grid, BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id, row0, idx0, scale);
+    else if (kind == 1)
+        k_synth_f32<1, false><<<grid, BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id, row0, idx0, scale);
+    else if (nt)
+        k_synth_f32<0, true><<<grid, BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id, row0, idx0, scale);
     else
-        k_synth_f32<0><<<dim3((unsigned)gx, (unsigned)gy), BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id,
-                                                                         row0, idx0, scale);
+        k_synth_f32<0, false><<<grid, BLOCK, 0, s>>>(out, m, ncols, n_rows, p, seed, stream_id, row0, idx0, scale);
     return hipGetLastError();
 }
 
