@@ -243,6 +243,8 @@ struct pgh_ctx {
     hipStream_t copy = nullptr;    // ingest H2D and on-device synthetic fill
     hipEvent_t copy_done = nullptr;
     hipEvent_t xsync = nullptr;    // caller-stream <-> context-stream ordering
+    hipStream_t aux = nullptr;     // second reduction stream: alternate ranges of a split FINAL pass
+    hipEvent_t aux_ev = nullptr;
     // The last fold issued on each stream (folds may run on several caller streams at once, e.g.
     // the param ranges of the multi-GPU overlap): the copy stream waits on all before it
     // overwrites slots, and then forgets them (later copies are ordered after those waits).
@@ -269,6 +271,7 @@ struct pgh_ctx {
     // GPU each (PGH_SYNTH_SERIAL=0: beside the fold on the copy stream; the write-heavy fill and the
     // read-only fold then share HBM 13 % worse, r02p), with non-temporal stores (PGH_SYNTH_NT)
     bool synth_serial = true;
+    int final_streams = 2;         // PGH_FINAL_STREAMS: 1 = the split FINAL pass on one stream
     bool synth_nt = true;
 
     int slots = 0, dtype = PGH_F32, parties = 1;
@@ -328,7 +331,11 @@ struct pgh_ctx {
     struct RangeMark { int64_t end; hipEvent_t ev; };
     std::vector<RangeMark> final_marks;
     std::vector<hipEvent_t> rmark_pool;
-    int final_split = 4;
+    // PGH_FINAL_RANGES (opt-in): split the FINAL pass of resident folds into this many param ranges
+    // with marks, so a following D2H starts behind the first range.  Off by default: each extra
+    // launch costs its drain (ResNet-18 fold 7.45 ms as 4 ranges on two streams vs 6.91 ms as one,
+    // r02r), about what the earlier D2H start saves in a close (report closes within noise, r02l/r02r).
+    int final_split = 1;
     int64_t client_base = 0;  // synthetic client k is generated as global client client_base + k
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
@@ -681,6 +688,26 @@ int add_final_mark(pgh_ctx* c, hipStream_t s, int64_t end) {
     else CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     CK(c, hipEventRecord(e, s));
     c->final_marks.push_back({end, e});
+    return PGH_OK;
+}
+
+// The ranges of a split FINAL pass alternate over `s` and the aux stream (final_streams == 2), so
+// range k + 1 starts while range k drains its last workgroups instead of after (one stream costs
+// the drain once per range: r02n group line, 4 launches 7.38 ms vs one 6.80 ms).  fork: aux after
+// everything issued on s; join: s after everything issued on aux.
+hipStream_t range_stream(const pgh_ctx* c, hipStream_t s, int k) {
+    return (c->final_streams > 1 && (k & 1)) ? c->aux : s;
+}
+int fork_aux(pgh_ctx* c, hipStream_t s) {
+    if (c->final_streams < 2) return PGH_OK;
+    CK(c, hipEventRecord(c->aux_ev, s));
+    CK(c, hipStreamWaitEvent(c->aux, c->aux_ev, 0));
+    return PGH_OK;
+}
+int join_aux(pgh_ctx* c, hipStream_t s) {
+    if (c->final_streams < 2) return PGH_OK;
+    CK(c, hipEventRecord(c->aux_ev, c->aux));
+    CK(c, hipStreamWaitEvent(s, c->aux_ev, 0));
     return PGH_OK;
 }
 
@@ -1103,6 +1130,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_NT_COPY")) c->nt_copy = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_PREFAULT")) c->prefault = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_FINAL_RANGES")) c->final_split = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("PGH_FINAL_STREAMS")) c->final_streams = std::atoi(e) > 1 ? 2 : 1;
     if (const char* e = std::getenv("PGH_D2H_PIECE_MB")) {
         const long long mb = std::atoll(e);
         c->d2h_piece = mb > 0 ? (size_t)mb << 20 : ~(size_t)0;
@@ -1112,6 +1140,8 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->xsync, hipEventDisableTiming) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->pin_ev[0], hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->pin_ev[1], hipEventDisableTiming) == hipSuccess;
     if (!ok) { pgh_destroy(c); return fail(nullptr, PGH_E_HIP, "stream/event creation failed"); }
@@ -1191,12 +1221,13 @@ void pgh_destroy(pgh_ctx* c) {
         if (c->h_pin[k]) (void)hipHostFree(c->h_pin[k]);
         if (c->pin_ev[k]) (void)hipEventDestroy(c->pin_ev[k]);
     }
-    for (hipEvent_t e : {c->copy_done, c->xsync})
+    for (hipEvent_t e : {c->copy_done, c->xsync, c->aux_ev})
         if (e) (void)hipEventDestroy(e);
     for (auto e : c->fold_ev_pool) (void)hipEventDestroy(e);
     for (auto e : c->rmark_pool) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     delete c;
 }
 
@@ -1770,12 +1801,15 @@ int pgh_fedavg_resident(pgh_ctx* c, int mode) {
         fa.ckpt = c->d_ckpt;
         fa.out = c->d_out;
         RC(fedavg_divisor(c, mode, n, &fa.divisor));
+        RC(fork_aux(c, c->stream));
         for (int k = 0; k < K; ++k) {
             fa.off = range_edge(c, k, K);
             fa.len = range_edge(c, k + 1, K) - fa.off;
-            RC(fold_run(c, mode, 0, n, true, fa, c->stream));
-            RC(add_final_mark(c, c->stream, fa.off + fa.len));
+            const hipStream_t rs = range_stream(c, c->stream, k);
+            RC(fold_run(c, mode, 0, n, true, fa, rs));
+            RC(add_final_mark(c, rs, fa.off + fa.len));
         }
+        RC(join_aux(c, c->stream));
     }
     std::swap(c->d_ckpt, c->d_out);  // the new checkpoint is the next cycle's input
     c->st.close_ms_last = now_ms() - t0;
@@ -1953,7 +1987,9 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
         // the FINAL pass as K param ranges, each followed by its mark (pipelined close)
         const int K = (a.flags & pgh::FL_FINAL) ? final_ranges(c) : 1;
         if (a.flags & pgh::FL_FINAL) clear_final_marks(c);
+        if (K > 1) RC(fork_aux(c, s));
         for (int r = 0; r < K; ++r) {
+            const hipStream_t rs = K > 1 ? range_stream(c, s, r) : s;
             const int64_t lo = K == 1 ? 0 : range_edge(c, r, K), hi = K == 1 ? c->pg : range_edge(c, r + 1, K);
             pgh::FedavgArgs ar = a;
             ar.map.off = lo;
@@ -1963,9 +1999,10 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
             ar.out = c->d_out + lo;
             const uint64_t rp = (uint64_t)(hi - lo);
             const uint64_t bytes = 4ull * (uint64_t)m * rp + (first ? 0 : 4 * rp) + ((a.flags & pgh::FL_FINAL) ? 8 * rp : 4 * rp);
-            RC(timed_launch(c, s, bytes, [&] { return pgh::launch_fedavg_rows(ar, tab, s); }));
-            if (K > 1) RC(add_final_mark(c, s, hi));
+            RC(timed_launch(c, rs, bytes, [&] { return pgh::launch_fedavg_rows(ar, tab, rs); }));
+            if (K > 1) RC(add_final_mark(c, rs, hi));
         }
+        if (K > 1) RC(join_aux(c, s));
         done += m;
     } while (done < n);
     RC(record_fold(c, s));

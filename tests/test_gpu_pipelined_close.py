@@ -1,6 +1,7 @@
-"""GPU: the pipelined close (shards of >= 1 M params): the resident fold's FINAL pass runs as 4
-param ranges with an event after each, and the new checkpoint's D2H (patch / download) runs on the
-copy stream piece by piece behind the range that wrote it.  The bytes must be exactly what the
+"""GPU: the pipelined close (opt-in, PGH_FINAL_RANGES=4; shards of >= 1 M params): the resident
+fold's FINAL pass runs as 4 param ranges alternating over two streams with an event after each,
+and the new checkpoint's D2H (patch / download) runs on the copy stream piece by piece behind the
+range that wrote it.  The bytes must be exactly what the
 one-launch fold gives -- checked against the oracle for every mode, through fedavg_resident,
 slot folds (report-time), downloads, template and fresh patches, and chained cycles."""
 import numpy as np
@@ -13,12 +14,33 @@ pytestmark = pytest.mark.gpu
 F = np.float32
 
 
+@pytest.fixture(scope="module")
+def piped():
+    """A context created with the pipelined close on (PGH_FINAL_RANGES=4, read at pgh_create)."""
+    import os
+
+    from pygrid_amd import Engine
+
+    old = os.environ.get("PGH_FINAL_RANGES")
+    os.environ["PGH_FINAL_RANGES"] = "4"
+    try:
+        eng = Engine(int(os.environ.get("PGH_DEVICE", "0")))
+    finally:
+        if old is None:
+            del os.environ["PGH_FINAL_RANGES"]
+        else:
+            os.environ["PGH_FINAL_RANGES"] = old
+    yield eng
+    eng.close()
+
+
 def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_resident_fold_ranges_download_and_patch(engine, mode):
+def test_resident_fold_ranges_download_and_patch(piped, mode):
+    engine = piped
     from pygrid_amd.state_schema import build_state_fast, parse_state
 
     rng = np.random.default_rng(400 + mode)
@@ -45,7 +67,8 @@ def test_resident_fold_ranges_download_and_patch(engine, mode):
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_report_time_close_ranges(engine, mode):
+def test_report_time_close_ranges(piped, mode):
+    engine = piped
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast, parse_state
 
@@ -77,9 +100,14 @@ def test_report_time_close_ranges(engine, mode):
             assert np.array_equal(bits(g), bits(w_)), cyc
 
 
-def test_group_pipelined_close(engine):
-    """Two children on GPU 0, each shard >= 1 M params: every child pipelines its own slice."""
+@pytest.mark.parametrize("streams", ["1", "2"])
+def test_group_pipelined_close(monkeypatch, streams):
+    """Two children on GPU 0, each shard >= 1 M params: every child pipelines its own slice (ranges
+    on one stream or alternating over two)."""
     from pygrid_amd import Engine
+
+    monkeypatch.setenv("PGH_FINAL_RANGES", "4")
+    monkeypatch.setenv("PGH_FINAL_STREAMS", streams)
     from pygrid_amd.cycle import CycleAggregator
     from pygrid_amd.state_schema import build_state_fast, parse_state
 
