@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""The bench's N > 1 step (sharding.OverlappedGather: 8 range folds over two streams, async RCCL
+"""The bench's N > 1 step (sharding.OverlappedGather: range folds over two streams, async RCCL
 all-gather per range, per-range placement) at world size 1 over RCCL, against one whole fold:
-what the multi-GPU step costs a rank besides the xGMI transfer itself."""
+what the multi-GPU step costs a rank besides the xGMI transfer itself.
+
+    python tools/ab_overlap_world1.py [chunks:tail ...]     (default 2:0 4:0 6:0 8:0 8:3 4:2)
+"""
 import json
 import os
 import socket
@@ -37,21 +40,22 @@ def main():
     out = torch.empty_like(ck)
     eng.synth_ckpt_device(1, ck.data_ptr(), sp)
     res = {}
-    ogs = {k: OverlappedGather(P, 1, 0, chunks=k) for k in (2, 4, 6, 8)}
+    plans = [tuple(int(x) for x in a.split(":")) for a in sys.argv[1:]] or [(2, 0), (4, 0), (6, 0), (8, 0), (8, 3), (4, 2)]
+    ogs = {pl: OverlappedGather(P, 1, 0, chunks=pl[0], tail=pl[1]) for pl in plans}
 
     def whole():
         eng.fedavg_device(0, ck.data_ptr(), out.data_ptr(), sp)
 
-    def overlapped(k, coll):
-        og = ogs[k]
+    def overlapped(pl, coll):
+        og = ogs[pl]
         lp = og.local.data_ptr()
         og.run(lambda off, n, st: eng.fedavg_device_range(0, off, n, ck.data_ptr(), lp, st), force_collective=coll)
         og.assemble()
 
     cases = {"whole": whole}
-    for k in (2, 4, 6, 8):
-        cases[f"ranges{k}_rccl"] = (lambda k=k: overlapped(k, True))
-        cases[f"ranges{k}_copy"] = (lambda k=k: overlapped(k, False))
+    for pl in plans:
+        cases[f"ranges{pl[0]}t{pl[1]}_rccl"] = (lambda pl=pl: overlapped(pl, True))
+        cases[f"ranges{pl[0]}t{pl[1]}_copy"] = (lambda pl=pl: overlapped(pl, False))
     for f in cases.values():
         f()
     torch.cuda.synchronize()
