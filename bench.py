@@ -43,6 +43,12 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+from pygrid_amd import hipenv  # noqa: E402
+
+# before anything touches HIP (the ranks this script spawns inherit it): >= 16 hardware queues,
+# so the N > 1 step's RCCL all-gather does not share a queue with the next range's fold
+HW_QUEUES = hipenv.prepare()
+
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
 METRIC = "client-diff GB/s aggregated (% of HBM peak) at 1/2/4/8 MI355X; cycle close ms"
 RESNET18_P = 11_689_512
@@ -409,6 +415,7 @@ def record(ctx, args, name, value, el, dt, config, roofline, extra=None, step_is
         "pct_hbm_peak_per_gpu": round(100 * value / ctx.n_gpus / HBM_PEAK_GBS, 2),
         ("kernel_ms" if step_is == "kernel" else "cycle_close_ms"): round(el / args.steps * 1e3, 4),
         "roofline": roofline, "cpu_baseline": None,
+        "hip_hw_queues": HW_QUEUES,
     }
     if extra:
         rec.update(extra)

@@ -9,7 +9,12 @@ The product is ``libpygrid_hip.so`` (C ABI: ``include/pgh_api.h``; gfx950 HIP ke
 * ``sharding``            -- parameter-axis shards + RCCL all-gather across GPUs
 
 Nothing here computes on the CPU: without the built library and a GPU the engine raises.
+Importing the package raises HIP's hardware-queue count (``hipenv``) when HIP is not yet up.
 """
+from . import hipenv
+
+hipenv.prepare()
+
 from .exceptions import (AggregationError, EngineUnavailableError, ModelNotAcceleratedError, PlanNotAcceleratedError,
                          PyGridError, StateParseError)
 from .engine import F32, I64, ITERATIVE_MEAN, MEAN, STREAM_SECAGG, WEIGHTED_MEAN, Engine, PinnedBuffer, device_count
