@@ -252,9 +252,20 @@ float fixed_point_divisor(int base, int prec) {
     return (float)(int64_t)scale;
 }
 
+struct DevSel {  // select a device for this thread, restore the previous one after
+    int prev = -1;
+    explicit DevSel(int d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(d);
+    }
+    ~DevSel() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 int free_exchange(pgh_group* g) {
     for (size_t i = 0; i < g->kids.size(); ++i) {
-        (void)hipSetDevice(g->devs[i]);
+        DevSel d(g->devs[i]);
         if (i < g->d_full.size()) (void)hipFree(g->d_full[i]);
         if (i < g->d_rs.size()) (void)hipFree(g->d_rs[i]);
         if (i < g->d_stage.size()) (void)hipFree(g->d_stage[i]);
@@ -288,6 +299,9 @@ int ensure_backend(pgh_ctx* c, int n) {
         if (r) {
             g->rccl = r;
             g->comms.assign((size_t)n, nullptr);
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            DevSel keep(cur);  // the caller's current device survives the communicator setup
             const ncclResult_t e = r->comm_init_all(g->comms.data(), n, devs.data());
             if (e != ncclSuccess) {
                 g->comms.clear();
@@ -305,13 +319,13 @@ int grow(pgh_ctx* c, std::vector<void*>* bufs, int64_t* cap, int64_t bytes) {
     pgh_group* g = G(c);
     if ((int64_t)bufs->size() == (int64_t)g->kids.size() && *cap >= bytes) return PGH_OK;
     for (size_t i = 0; i < bufs->size(); ++i) {
-        (void)hipSetDevice(g->devs[i]);
+        DevSel d(g->devs[i]);
         (void)hipFree((*bufs)[i]);
     }
     bufs->assign(g->kids.size(), nullptr);
     *cap = 0;
     for (size_t i = 0; i < g->kids.size(); ++i) {
-        (void)hipSetDevice(g->devs[i]);
+        DevSel d(g->devs[i]);
         if (hipMalloc(&(*bufs)[i], (size_t)bytes) != hipSuccess) {
             (void)hipGetLastError();
             return fail(c, PGH_E_OOM, "gpu %zu: exchange buffer of %lld bytes failed", i, (long long)bytes);
@@ -324,17 +338,6 @@ int grow(pgh_ctx* c, std::vector<void*>* bufs, int64_t* cap, int64_t bytes) {
 int sync_all(pgh_ctx* c, int n) {
     return fan(c, [](int, pgh_ctx* k) -> int { return pgh_sync(k); }, n);
 }
-
-struct DevSel {  // select a device for this thread, restore the previous one after
-    int prev = -1;
-    explicit DevSel(int d) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        (void)hipSetDevice(d);
-    }
-    ~DevSel() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
 
 // Client-sharded secure aggregation: per-GPU share sums -> reduce-scatter -> per-GPU decode ->
 // host slices.
