@@ -498,35 +498,75 @@ __global__ __launch_bounds__(BLOCK) void k_synth_shares(int64_t* out, SlabMap m,
 
 // Packed varints -> int64 (TensorData.contents_int64 of secagg share States).  One workgroup per
 // 64 KiB chunk, walked in 4 KiB windows staged in LDS with the 16 bytes before them (a varint is
-// at most 10 bytes, so its start is always in view).  Lane t owns bytes [16t, 16t + 16) of a
-// window: the terminators among them (bit 7 clear) end its values; a wave prefix sum (shuffles)
-// plus the per-wave totals in LDS give each value's flat index.  Byte-level work on a stream
-// PCIe fills at ~55 GB/s: the kernel only has to keep up, HBM traffic is ~2 bytes per byte in.
+// at most 10 bytes, so a value ending in the window starts at offset >= -9).  Per window:
+//   1. lane t owns bytes [16t, 16t + 16): its terminators (bit 7 clear) come from its 16-byte load
+//      in registers; a wave prefix sum (shuffles) + the per-wave totals give each value's rank;
+//   2. every lane writes the window offsets of its value ends into LDS by rank (a compacted list);
+//   3. the workgroup decodes the list rank by rank, lane = rank mod 256: value r spans
+//      (end[r - 1], end[r]] (end[-1] = the last end of the previous window, or of the 16 bytes
+//      before the chunk), its <= 10 bytes are independent LDS reads and the 7-bit groups are
+//      shifted in under a length mask -- no data-dependent loop, no divergence past the last rank;
+//      value r goes to flat index first + rank, so consecutive lanes store consecutive int64s.
+// The next window's 16-byte load is issued before the current one is decoded.  Byte-level work on
+// a stream PCIe fills at ~55 GB/s; HBM traffic is ~2 bytes per byte in.
+constexpr int VWIN = 4096;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t pack7x4(uint32_t w) {  // the low 7 bits of 4 bytes -> 28 bits
+    w &= 0x7F7F7F7Fu;
+    w = (w & 0x007F007Fu) | ((w & 0x7F007F00u) >> 1);
+    return (w & 0x00003FFFu) | ((w & 0x3FFF0000u) >> 2);
+}
+
+__device__ __forceinline__ uint32_t term_mask16(const u32x4& v) {  // bit k: byte k has bit 7 clear
+    uint32_t tm = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t nt = ~v[w] & 0x80808080u;
+        tm |= (((nt >> 7) & 1u) | ((nt >> 14) & 2u) | ((nt >> 21) & 4u) | ((nt >> 28) & 8u)) << (4 * w);
+    }
+    return tm;
+}
+
 __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, const VChunk* chunks, int64_t* row,
                                                        SlabMap m, int64_t lo, int64_t hi) {
-    __shared__ uint4 win4[1 + 256];  // [0]: the 16 bytes before the window, then the window
+    __shared__ u32x4 win4[1 + 256 + 1];  // [0]: the 16 bytes before the window; [257]: slack for reads past an end
+    __shared__ uint16_t ends[VWIN];      // window offsets of the value ends, by rank
     __shared__ int wsum[4];
-    const uint8_t* win = reinterpret_cast<const uint8_t*>(win4);
+    constexpr int NW = VARINT_CHUNK / VWIN;
+    const uint8_t* win = reinterpret_cast<const uint8_t*>(win4) + 16;  // win[-16 .. 4111]
     const VChunk ch = chunks[blockIdx.x];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int p = 16 * t;
+    const u32x4 zero = {0, 0, 0, 0};
+    // Loads are unconditional (a branch around a load makes hipcc wait for it at once, which would
+    // serialise the prefetch): an offset past the chunk is clamped to its last 16 bytes and what it
+    // reads is masked out by the chunk length.  The value end before the window, in window offsets,
+    // comes from the 16 bytes before the chunk (zero bytes at a payload's start read as
+    // terminators: the first value starts at offset 0).
+    const bool has_before = ch.off > ch.span_off;
+    const u32x4 b16 = *reinterpret_cast<const u32x4*>(bytes + (has_before ? ch.off - 16 : ch.off));
+    const int last16 = (ch.n - 1) & ~15;
+    // the next window's 16 bytes are loaded one window ahead (loading the whole chunk up front
+    // costs occupancy: 79 vs 63 us per 111 MB message, profiles/r02x/)
+    u32x4 nxt = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + ch.off + min(p, last16)));
+    const u32x4 before = has_before ? b16 : zero;
+    const uint32_t tb = term_mask16(before);
+    int carry = tb ? (31 - __clz(tb)) - 16 : -16;
+    if (t == 0) win4[257] = zero;
+    u32x4 last = before;  // lane 255: the previous window's last 16 bytes
     int64_t base = ch.first;
-    for (int w0 = 0; w0 < ch.n; w0 += 4096) {
-        const int64_t g = ch.off + w0;
-        const int p = 16 * t;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (w0 + p < ch.n) v = *reinterpret_cast<const uint4*>(bytes + g + p);
-        win4[1 + t] = v;
-        if (t == 0) {  // zero bytes read as terminators: nothing before a payload's first byte
-            uint4 b = make_uint4(0, 0, 0, 0);
-            if (g > ch.span_off) b = *reinterpret_cast<const uint4*>(bytes + g - 16);
-            win4[0] = b;
-        }
-        __syncthreads();
-        uint32_t tm = 0;
-        const int lim = ch.n - w0 - p;  // bytes of mine inside the chunk
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (k < lim && !(win[16 + p + k] & 0x80)) tm |= 1u << k;
+    for (int i = 0; i < NW; ++i) {
+        const int w0 = VWIN * i;
+        if (w0 >= ch.n) break;  // uniform over the workgroup
+        const u32x4 v = nxt;
+        nxt = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + ch.off + min(w0 + VWIN + p, last16)));
+        win4[1 + t] = v;
+        if (t == 255) win4[0] = last;
+        uint32_t tm = term_mask16(v);
+        const int lim = ch.n - w0 - p;  // bytes of mine inside the chunk
+        if (lim < 16) tm &= lim > 0 ? (1u << lim) - 1u : 0u;
         const int cnt = __popc(tm);
         int x = cnt;  // inclusive prefix over the wave
 #pragma unroll
@@ -536,27 +576,44 @@ __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, con
         }
         if (lane == 63) wsum[wave] = x;
         __syncthreads();
-        int before = 0, total = 0;
+        int rank = x - cnt, total = 0;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             const int sw = wsum[w];
-            before += w < wave ? sw : 0;
+            rank += w < wave ? sw : 0;
             total += sw;
         }
-        int64_t idx = base + before + (x - cnt);
         while (tm) {
-            const int k = __ffs(tm) - 1;
+            ends[rank++] = (uint16_t)(p + __ffs(tm) - 1);
             tm &= tm - 1;
-            const int end = 16 + p + k;
-            int st = end;
-            for (int j = 0; j < 9 && (win[st - 1] & 0x80); ++j) --st;  // st - 1 >= end - 10 >= 5
-            uint64_t val = 0;
-            for (int j = st; j <= end; ++j) val |= (uint64_t)(win[j] & 0x7F) << (7 * (j - st));
-            if (idx >= lo && idx < hi) row[m.at(idx - lo)] = (int64_t)val;
-            ++idx;
         }
+        __syncthreads();
+        for (int r = t; r < total; r += 256) {
+            const int e = ends[r];
+            // validated input: s >= e - 9 (the clamp only keeps malformed bytes inside the window)
+            const int s = max(r ? (int)ends[r - 1] + 1 : carry + 1, e - 9);
+            const int len = e - s + 1;
+            // bytes [s, s + 12) from the four aligned dwords around them (win[-16 .. 4111] are in
+            // bounds: s >= -15 and s <= 4095), then the 7-bit groups of each dword packed in
+            // 32-bit arithmetic; bytes at or past the value's length are masked out first
+            const uint32_t* wd = reinterpret_cast<const uint32_t*>(win + (s & ~3));
+            const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
+            const uint32_t sh = (uint32_t)(s & 3);
+            uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+            uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+            w0 &= len >= 4 ? 0xFFFFFFFFu : (1u << (8 * len)) - 1u;
+            w1 &= len >= 8 ? 0xFFFFFFFFu : len <= 4 ? 0u : (1u << (8 * (len - 4))) - 1u;
+            w2 &= len >= 10 ? 0xFFFFu : len == 9 ? 0xFFu : 0u;
+            const uint64_t val = (uint64_t)pack7x4(w0) | ((uint64_t)pack7x4(w1) << 28) |
+                                 ((uint64_t)(w2 & 0x7F) << 56) | ((uint64_t)((w2 >> 8) & 0x7F) << 63);
+            const int64_t idx = base + r;
+            if (idx >= lo && idx < hi) row[m.at(idx - lo)] = (int64_t)val;
+        }
+        carry = (total ? (int)ends[total - 1] : carry) - VWIN;
         base += total;
-        __syncthreads();  // win / wsum are rewritten by the next window
+        last = v;
+        __syncthreads();  // win4 / ends / wsum are rewritten by the next window
     }
 }
 

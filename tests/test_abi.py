@@ -37,7 +37,9 @@ def test_library_does_not_link_torch():
 
     out = subprocess.run(["readelf", "-d", str(ROOT / "pygrid_amd" / "libpygrid_hip.so")],
                          capture_output=True, text=True).stdout
-    assert "torch" not in out and "c10" not in out
+    # only the dependency and search-path entries (a hex address may happen to read "c10")
+    deps = [ln for ln in out.splitlines() if "(NEEDED)" in ln or "PATH)" in ln]
+    assert deps and not any("torch" in ln or "libc10" in ln for ln in deps), deps
 
 
 def test_engine_without_gpu_raises():
