@@ -114,6 +114,10 @@ class IncrementalCycle:
             if self._declined:
                 self._reported.add(worker)  # the node averages this cycle itself
                 return
+            if self._weights_by_worker is not None and worker not in self._weights_by_worker:
+                # refused to its sender now, not when a later report folds it (that would leave
+                # the fold half done and blame another worker)
+                raise AggregationError(f"worker {worker!r} reported but has no aggregation weight")
             front = self._pos[worker] == self._front
             try:
                 # a diff that cannot fold yet leaves one slot free for the fold front

@@ -168,6 +168,19 @@ def test_weights_follow_fold_order():
     assert eng.weights == [1.0, 2.0, 3.0]
 
 
+def test_weightless_report_is_refused_to_its_sender():
+    eng = RecordingEngine()
+    inc = IncrementalCycle(eng, [3], mode=2, slots=4, fold_batch=1, weights_by_worker={"x": 1.0, "z": 3.0})
+    for w in ("x", "y", "z"):
+        inc.assigned(w)
+    with pytest.raises(AggregationError):
+        inc.reported("y", b"y")  # nothing recorded: y counts as a non-reporter
+    inc.reported("z", b"z")
+    inc.reported("x", b"x")
+    inc.close(b"ck", framing="template")
+    assert folded(eng) == [b"x", b"z"] and eng.weights == [1.0, 3.0]
+
+
 def test_errors():
     eng = RecordingEngine()
     inc = IncrementalCycle(eng, [3], slots=4)
