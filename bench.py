@@ -99,6 +99,9 @@ def parse():
                          "how the node's single process uses the node's GPUs) instead of one rank per GPU")
     ap.add_argument("--e2e-distinct", type=int, default=64,
                     help="end-to-end close: distinct client State messages in host memory (re-sent as the others)")
+    ap.add_argument("--no-live-traffic", action="store_true",
+                    help="N = 1 resident lines: skip the two rocprofv3 --pmc passes that measure roofline.traffic "
+                         "in this run (the committed profiles/pmc_traffic.json is quoted instead)")
     ap.add_argument("--dry-run", action="store_true",
                     help="form the world (gloo, no GPU), print the world size on rank 0 and exit")
     return ap.parse_args()
@@ -327,6 +330,63 @@ def load_traffic(workload: str, variant: int, alg_bytes: float):
         return None, None
 
 
+PMC_KERNEL = {"resnet18-fedavg": "k_fedavg", "resnet18-iterative": "k_fedavg", "resnet18-weighted": "k_fedavg",
+              "resnet18-secagg": "k_secagg"}
+
+
+def under_profiler() -> bool:
+    return any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
+
+
+def measure_live_traffic(args, timeout_s: int = 150):
+    """roofline.traffic measured in THIS run: before the parent touches the GPU, the same workload
+    runs twice as a child under ``rocprofv3 --pmc`` (FETCH_SIZE, then WRITE_SIZE: one counter
+    block per pass, as MI355X_MICROARCH.md's HBM section prescribes), 2 steps each; HBM bytes per
+    launch of the dominant kernel = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950's FETCH_SIZE
+    counts half the bytes of wide streaming reads).  Returns (bytes per launch, the child's
+    algorithmic bytes per launch, note) or None (no profiler, a failed or timed-out pass: the
+    committed summary is quoted instead)."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    kernel = PMC_KERNEL.get(args.workload)
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if kernel is None or not Path(prof).exists():
+        return None
+    sys.path.insert(0, str(ROOT / "tools"))
+    from pmc_summarize import per_launch
+
+    tmp = Path(tempfile.mkdtemp(prefix="pgh_pmc_"))
+    child = [sys.executable, str(ROOT / "bench.py"), "--workload", args.workload, "--steps", "2", "--warmup", "1",
+             "--no-cpu-baseline", "--no-e2e", "--no-live-traffic", "--seed", str(args.seed)]
+    if args.variant is not None:
+        child += ["--variant", str(args.variant)]
+    got, alg = {}, None
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            r = subprocess.run(["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc", counter, "-d",
+                                str(tmp / counter), "-o", "run", "--output-format", "csv", "--"] + child,
+                               cwd=str(ROOT), capture_output=True, text=True)
+            if r.returncode != 0:
+                print(f"bench.py: live PMC pass {counter} failed (rc {r.returncode}); quoting the committed "
+                      f"traffic", file=sys.stderr)
+                return None
+            got[counter] = per_launch(tmp / counter, counter, kernel)
+            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            alg = json.loads(lines[-1])["roofline"]["alg_bytes_per_launch"] if lines else alg
+    except (Exception, SystemExit) as e:  # noqa: BLE001 -- evidence only: never fails the bench
+        print(f"bench.py: live PMC passes unusable ({e}); quoting the committed traffic", file=sys.stderr)
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    fetch, n, _ = got["FETCH_SIZE"]
+    write, _, _ = got["WRITE_SIZE"]
+    note = (f"live: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of this workload (2 steps each, "
+            f"{n} {kernel} launches per pass) run by bench.py before its timed run; (2*FETCH_SIZE + WRITE_SIZE)*1024")
+    return (2 * fetch + write) * 1024, alg, note
+
+
 class Ctx:
     """Per-rank setup shared by the workloads."""
 
@@ -422,9 +482,14 @@ def record(ctx, args, name, value, el, dt, config, roofline, extra=None, step_is
     return rec
 
 
+LIVE_TRAFFIC = None  # (hbm bytes per launch, algorithmic bytes per launch, note): measure_live_traffic
+
+
 def roofline_of(st, workload, variant, kernel, n_gpus=1):
     """Dominant kernel against one GPU's HBM peak.  A group's stats sum the bytes of its GPUs and
-    take the slowest GPU's times (they run concurrently): bytes are divided by n_gpus here."""
+    take the slowest GPU's times (they run concurrently): bytes are divided by n_gpus here.
+    ``traffic`` is this run's own PMC measurement when bench.py made one (LIVE_TRAFFIC), else the
+    committed summary (profiles/pmc_traffic.json), quoted only for the current kernel sources."""
     n = max(st["kernel_launches"], 1)
     ms = st["kernel_ms_total"] / n
     alg = st["kernel_bytes_total"] / n / n_gpus
@@ -436,10 +501,19 @@ def roofline_of(st, workload, variant, kernel, n_gpus=1):
     dur = busy / n if overlapped else ms
     achieved = alg / (dur / 1e3) / 1e9
     traffic, src = load_traffic(workload, variant, alg)
+    committed = traffic
+    if LIVE_TRAFFIC is not None and kernel == PMC_KERNEL.get(workload):
+        live, live_alg, note = LIVE_TRAFFIC
+        if live_alg and abs(live_alg - alg) <= 1e-6 * alg:
+            traffic, src = live, note
+        elif live_alg:
+            traffic, src = live / live_alg * alg, note + f"; ratio {live / live_alg:.6f} applied to this launch"
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
          "kernel_ms_avg": round(dur, 4), "alg_bytes_per_launch": int(alg), "launches": st["kernel_launches"],
          "traffic_source": src}
+    if traffic is not None and committed is not None and traffic is not committed:
+        r["traffic_committed"] = committed  # the last evidence pass's figure, for comparison
     if overlapped:
         r["launch_overlap"] = {"event_span_ms_avg": round(ms, 4), "busy_ms_total": round(busy, 3),
                                "note": "launches overlap on two streams: duration = busy time / launches"}
@@ -1014,6 +1088,10 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.group:
         sys.exit(spawn_ranks(args))  # no launcher: form the N-rank world here (no GPU touched yet)
+    global LIVE_TRAFFIC
+    if (args.gpus == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.group and not args.dry_run
+            and not args.no_live_traffic and args.workload in PMC_KERNEL and not under_profiler()):
+        LIVE_TRAFFIC = measure_live_traffic(args)  # child processes; this one has not touched the GPU yet
     ctx = Ctx(args)
     if args.dry_run:
         if ctx.rank == 0:

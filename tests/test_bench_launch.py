@@ -75,3 +75,30 @@ def test_group_mode_is_one_process_over_n_gpus():
     r = _run(["--gpus", "4", "--group", "--dry-run"])
     assert r.returncode == 0, r.stderr
     assert _json_line(r.stdout) == {"dry_run": True, "n_gpus": 4, "backend": "gloo", "group": True}
+
+
+def test_roofline_quotes_live_traffic_over_the_committed_file(monkeypatch):
+    """bench.py measures roofline.traffic itself (rocprofv3 --pmc passes before the timed run) and
+    quotes it instead of profiles/pmc_traffic.json; a launch of another size gets the live ratio."""
+    import importlib
+
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    bench = importlib.import_module("bench")
+    st = {"kernel_launches": 2, "kernel_ms_total": 13.0, "kernel_bytes_total": 2 * 1000, "kernel_busy_ms_total": 13.0}
+    monkeypatch.setattr(bench, "LIVE_TRAFFIC", (1001.0, 1000, "live: test"))
+    r = bench.roofline_of(st, "resnet18-fedavg", 0, "k_fedavg")
+    assert r["traffic"] == 1001.0 and r["traffic_source"] == "live: test"
+    monkeypatch.setattr(bench, "LIVE_TRAFFIC", (1001.0, 500, "live: test"))
+    r = bench.roofline_of(st, "resnet18-fedavg", 0, "k_fedavg")
+    assert abs(r["traffic"] - 2002.0) < 1e-9 and "ratio" in r["traffic_source"]
+    monkeypatch.setattr(bench, "LIVE_TRAFFIC", None)
+    assert bench.roofline_of(st, "resnet18-fedavg", 0, "k_fedavg")["traffic_source"] != "live: test"
+
+
+def test_live_traffic_is_skipped_under_a_profiler(monkeypatch):
+    import importlib
+
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    bench = importlib.import_module("bench")
+    monkeypatch.setenv("ROCPROF_COUNTERS", "FETCH_SIZE")
+    assert bench.under_profiler()

@@ -35,7 +35,7 @@ else
   done
   for w in resnet18-fedavg resnet18-iterative resnet18-weighted resnet18-secagg resnet18-report; do
     for c in FETCH_SIZE WRITE_SIZE; do
-      timeout -s KILL 200 rocprofv3 --pmc $c -d $OUT/pmc_${w}_$c -o run --output-format csv -- python3 bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $OUT/pmc_${w}_$c.log 2>&1 || exit $?
+      timeout -s KILL 200 rocprofv3 --pmc $c -d $OUT/pmc_${w}_$c -o run --output-format csv -- python3 bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-live-traffic > $OUT/pmc_${w}_$c.log 2>&1 || exit $?
     done
   done
 fi
