@@ -338,7 +338,7 @@ def under_profiler() -> bool:
     return any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
 
 
-def measure_live_traffic(args, timeout_s: int = 150):
+def measure_live_traffic(args, timeout_s: int = 90):
     """roofline.traffic measured in THIS run: before the parent touches the GPU, the same workload
     runs twice as a child under ``rocprofv3 --pmc`` (FETCH_SIZE, then WRITE_SIZE: one counter
     block per pass, as MI355X_MICROARCH.md's HBM section prescribes), 2 steps each; HBM bytes per
@@ -365,6 +365,7 @@ def measure_live_traffic(args, timeout_s: int = 150):
     got, alg = {}, None
     try:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            print(f"bench.py: live PMC pass {counter} (rocprofv3 --pmc, {timeout_s} s limit)", file=sys.stderr, flush=True)
             r = subprocess.run(["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc", counter, "-d",
                                 str(tmp / counter), "-o", "run", "--output-format", "csv", "--"] + child,
                                cwd=str(ROOT), capture_output=True, text=True)
