@@ -338,7 +338,7 @@ def under_profiler() -> bool:
     return any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
 
 
-def measure_live_traffic(args, timeout_s: int = 90):
+def measure_live_traffic(args, timeout_s=(240, 120)):
     """roofline.traffic measured in THIS run: before the parent touches the GPU, the same workload
     runs twice as a child under ``rocprofv3 --pmc`` (FETCH_SIZE, then WRITE_SIZE: one counter
     block per pass, as MI355X_MICROARCH.md's HBM section prescribes), 2 steps each; HBM bytes per
@@ -364,9 +364,10 @@ def measure_live_traffic(args, timeout_s: int = 90):
         child += ["--variant", str(args.variant)]
     got, alg = {}, None
     try:
-        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-            print(f"bench.py: live PMC pass {counter} (rocprofv3 --pmc, {timeout_s} s limit)", file=sys.stderr, flush=True)
-            r = subprocess.run(["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc", counter, "-d",
+        # the first pass may pay a fresh box's first `import torch` (1-2 minutes): a longer limit
+        for counter, limit in zip(("FETCH_SIZE", "WRITE_SIZE"), timeout_s):
+            print(f"bench.py: live PMC pass {counter} (rocprofv3 --pmc, {limit} s limit)", file=sys.stderr, flush=True)
+            r = subprocess.run(["timeout", "-s", "KILL", str(limit), prof, "--pmc", counter, "-d",
                                 str(tmp / counter), "-o", "run", "--output-format", "csv", "--"] + child,
                                cwd=str(ROOT), capture_output=True, text=True)
             if r.returncode != 0:
