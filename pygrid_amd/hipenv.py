@@ -24,7 +24,10 @@ _MAX_HW_QUEUES = 32
 
 
 def prepare() -> int | None:
-    want = int(os.environ.get("PGH_HW_QUEUES", DEFAULT_HW_QUEUES))
+    try:
+        want = int(os.environ.get("PGH_HW_QUEUES", DEFAULT_HW_QUEUES))
+    except ValueError:
+        want = DEFAULT_HW_QUEUES
     want = max(1, min(want, _MAX_HW_QUEUES))
     try:
         have = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))

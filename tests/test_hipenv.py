@@ -40,6 +40,13 @@ def test_override_and_clamp(monkeypatch):
     assert os.environ["GPU_MAX_HW_QUEUES"] == "32"
 
 
+def test_bad_override_falls_back(monkeypatch):
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "x")
+    monkeypatch.setenv("PGH_HW_QUEUES", "lots")
+    hipenv.prepare()
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "16"
+
+
 def test_bench_children_inherit():
     """bench.py sets the variable at import, before it spawns ranks or touches HIP."""
     env = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "PGH_HW_QUEUES")}
