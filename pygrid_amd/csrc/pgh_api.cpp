@@ -1113,8 +1113,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (pinned_bytes == 0) pinned_bytes = 256ull << 20;
     c->pin_slot = (pinned_bytes / 2) & ~(size_t)4095;
     if (c->pin_slot < 4096) c->pin_slot = 4096;
-    const unsigned hw = std::thread::hardware_concurrency();
-    c->copy_threads = (int)std::max(1u, std::min(16u, hw ? hw : 1u));
+    c->copy_threads = std::min(16, pgh_int::usable_cpus());
     if (const char* e = std::getenv("PGH_COPY_THREADS")) c->copy_threads = std::max(1, std::atoi(e));
     {
         const char* nu = std::getenv("PGH_NUMA");
@@ -2218,6 +2217,31 @@ int pgh_sync(pgh_ctx* c) {
 // ---- internals for the multi-GPU group driver (pgh_internal.h) ------------------------------------
 
 namespace pgh_int {
+
+int usable_cpus() {
+    static const int n = [] {
+        int cpus = 0;
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus = CPU_COUNT(&set);
+        if (cpus <= 0) cpus = (int)std::max(1u, std::thread::hardware_concurrency());
+        double quota = 0;
+        std::ifstream v2("/sys/fs/cgroup/cpu.max");
+        std::string q;
+        long long per = 0;
+        if (v2 >> q >> per) {
+            if (q != "max" && per > 0) quota = std::atof(q.c_str()) / (double)per;
+        } else {
+            std::ifstream qf("/sys/fs/cgroup/cpu/cpu.cfs_quota_us"), pf("/sys/fs/cgroup/cpu/cpu.cfs_period_us");
+            long long qq = 0, pp = 0;
+            if ((qf >> qq) && (pf >> pp) && qq > 0 && pp > 0) quota = (double)qq / (double)pp;
+        }
+        if (quota >= 1 && (int)quota < cpus) cpus = (int)quota;
+        return std::max(1, cpus);
+    }();
+    return n;
+}
+
 int fail(pgh_ctx* c, int code, const char* fmt, ...) {
     va_list ap;
     va_start(ap, fmt);

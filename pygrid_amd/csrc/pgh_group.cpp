@@ -459,8 +459,7 @@ int pgh_create_group(int n_gpus, const int* devices, size_t pinned_bytes, pgh_ct
     if (n_gpus < 1 || n_gpus > 64) return fail(nullptr, PGH_E_ARG, "n_gpus %d outside [1,64]", n_gpus);
     auto* g = new pgh_group();
     for (int i = 0; i < n_gpus; ++i) g->devs.push_back(devices ? devices[i] : i);
-    const unsigned hw = std::thread::hardware_concurrency();
-    const int threads = std::max(2, std::min(16, (int)(hw ? hw : 16) / n_gpus));
+    const int threads = std::max(2, std::min(16, pgh_int::usable_cpus() / n_gpus));
     for (int i = 0; i < n_gpus; ++i) {
         pgh_ctx* k = nullptr;
         const int rc = pgh_create(g->devs[(size_t)i], pinned_bytes, &k);

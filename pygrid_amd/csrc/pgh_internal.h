@@ -34,6 +34,10 @@ int set_copy_threads(pgh_ctx* c, int n);
 int set_client_base(pgh_ctx* c, int64_t base);
 enum Vec { V_CKPT = 0, V_SUM = 1, V_DEC = 2 };
 void* vec(pgh_ctx* c, int which);
+// CPUs this process may use: its affinity mask capped by a cgroup CPU quota (cgroup v2 cpu.max or
+// v1 cfs_quota/period) -- a GPU lease's share of a bigger machine, which hardware_concurrency()
+// (every online CPU) does not see.  Computed once.
+int usable_cpus();
 // Write only this shard's slice of every payload of `tmpl` into `out` (from the resident checkpoint);
 // the caller writes the framing.  Pre-faults the shard's own part of `out` while the first DMA flies.
 int patch_payloads(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out);
