@@ -199,17 +199,21 @@ void populate(uint8_t* p, size_t n) {
     if (!on || !p || n < (1u << 20)) return;
     static const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
     const uintptr_t a = ((uintptr_t)p + page - 1) & ~(page - 1), b = ((uintptr_t)p + n) & ~(page - 1);
-    // The 2 MiB-aligned interior on transparent huge pages (one fault per 2 MiB instead of 512):
-    // a 47 MB diff decodes in 7-9 ms instead of 11-12 (profiles/r02ad/); PGH_B64_THP=0 turns it off.
+    if (b > a) (void)madvise((void*)a, b - a, MADV_POPULATE_WRITE);
+}
+
+// The 2 MiB-aligned interior of a big fresh output on transparent huge pages (one fault per 2 MiB
+// instead of 512): a 47 MB diff decodes in 7-9 ms instead of 11-12 (profiles/r02ad/).  One call
+// over the whole output on the caller's thread, before the threads populate their parts (the
+// hint changes the mapping's flags: one writer, not one per thread).  PGH_B64_THP=0 turns it off.
+void hugepage_hint(uint8_t* p, size_t n) {
     static const bool thp = [] {
         const char* e = std::getenv("PGH_B64_THP");
         return !e || std::atoi(e) != 0;
     }();
-    if (thp) {
-        const uintptr_t h = (uintptr_t)2 << 20, ha = (a + h - 1) & ~(h - 1), hb = b & ~(h - 1);
-        if (hb > ha) (void)madvise((void*)ha, hb - ha, MADV_HUGEPAGE);
-    }
-    if (b > a) (void)madvise((void*)a, b - a, MADV_POPULATE_WRITE);
+    if (!thp || !p || n < (4u << 20)) return;
+    const uintptr_t h = (uintptr_t)2 << 20, ha = ((uintptr_t)p + h - 1) & ~(h - 1), hb = ((uintptr_t)p + n) & ~(h - 1);
+    if (hb > ha) (void)madvise((void*)ha, hb - ha, MADV_HUGEPAGE);
 }
 
 // A persistent pool (thread creation cost ~1 ms per decode at 16 threads x 2 passes): run(t, f)
@@ -305,6 +309,7 @@ int decode_fast(const unsigned char* s, size_t n, size_t fe, uint8_t* out, size_
     const int tf = n4f < (1u << 16) ? 1 : t;
     const size_t pq = (n4f + tf - 1) / tf;
     std::atomic<bool> clean{true};
+    if (out && padded) hugepage_hint(out, 3 * n4f);
     parallel(tf, [&](int k) {
         const size_t g0 = std::min(n4f, pq * k), g1 = std::min(n4f, g0 + pq);
         const bool dec = out && padded;
