@@ -327,7 +327,7 @@ struct pgh_ctx {
     // Pipelined close: a resident fold's FINAL pass runs as final_split param ranges, each followed by
     // an event; a D2H of the new checkpoint (patch / download) then runs on the copy stream, piece by
     // piece behind the range that wrote it, so the HBM -> host copy overlaps the rest of the fold
-    // (PGH_FINAL_RANGES, default 4, shards of >= 1 M params).
+    // (PGH_FINAL_RANGES, shards of >= 1 M params; opt-in, see final_split below).
     struct RangeMark { int64_t end; hipEvent_t ev; };
     std::vector<RangeMark> final_marks;
     std::vector<hipEvent_t> rmark_pool;
