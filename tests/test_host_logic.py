@@ -1,6 +1,7 @@
 """CPU: host-side logic of the drop-in -- readiness predicate, plan dispatch, the
 _average_plan_diffs wiring, and the State codec (host-only C++ in libpygrid_hip)."""
 import itertools
+from functools import reduce
 import types
 
 import numpy as np
@@ -141,10 +142,50 @@ class FakeAggregator:
     def __init__(self):
         self.calls = []
 
-    def average_plan_diffs(self, server_config, checkpoint, diffs, avg_plan=None):
-        cycle.select_mode(server_config, avg_plan)  # same dispatch as the real one
+    def average_plan_diffs(self, server_config, checkpoint, diffs, avg_plan=None, plan_key=None):
+        cycle.select_mode(server_config, avg_plan, plan_key=plan_key)  # same dispatch as the real one
         self.calls.append((checkpoint, list(diffs), avg_plan))
         return b"NEW"
+
+
+@pytest.fixture(autouse=True)
+def _fresh_plan_cache():
+    cycle._MODE_CACHE.clear()
+    yield
+    cycle._MODE_CACHE.clear()
+
+
+def test_plan_verdict_is_cached_by_plan_bytes():
+    """A node's avg plan is fixed for its FL process: probe it once per plan (its bytes), not once
+    per cycle; a declined plan stays declined; another plan (or the other iterative flag) is probed."""
+    calls = []
+
+    def mean_plan(diffs):
+        calls.append(1)
+        return [th.div(reduce(th.add, [d[j] for d in diffs]), len(diffs)) for j in range(len(diffs[0]))]
+
+    assert cycle.select_mode({}, mean_plan, plan_key=b"P1") == cycle.MEAN
+    n = len(calls)
+    assert n > 0
+    assert cycle.select_mode({}, mean_plan, plan_key=b"P1") == cycle.MEAN and len(calls) == n
+    assert cycle.cached_mode({}, b"P1") == cycle.MEAN and cycle.cached_mode({}, b"P2") is None
+    with pytest.raises(PlanNotAcceleratedError):
+        cycle.select_mode({"iterative_plan": True}, mean_plan, plan_key=b"P1")  # not the iterative form
+    with pytest.raises(PlanNotAcceleratedError):
+        cycle.cached_mode({"iterative_plan": True}, b"P1")
+    assert cycle.select_mode({}, mean_plan) == cycle.MEAN and len(calls) > n  # no key: probed
+
+
+def test_wiring_skips_deserializing_a_probed_plan():
+    mm, pm, plm, self_, cyc, saved, created = _fake_node(avg_plan_value=b"CANON")
+    loads = []
+    deser = plm.deserialize_plan
+    plm.deserialize_plan = lambda b: loads.append(b) or deser(b)
+    agg = FakeAggregator()
+    fn = cycle.make_average_plan_diffs(agg, mm, pm, plm, original=None)
+    fn(self_, {"iterative_plan": True}, cyc)
+    fn(self_, {"iterative_plan": True}, cyc)
+    assert loads == [b"CANON"] and len(agg.calls) == 2 and len(saved) == 2
 
 
 def test_wiring_hardcoded_path():
