@@ -144,3 +144,34 @@ def test_fold_slots_api_edges(engine):
     engine.fold_slots_finish_resident(0, [])
     want = O.fedavg_mean([c], [[x] for x in d[:5]])[0]
     assert np.array_equal(bits(engine.ckpt_download()), bits(want))
+
+
+@pytest.mark.parametrize("shapes", [[(1,)], [(3,)], [(64,)], [(65,)], [(1,), (2,), (61,)], [(4, 17), (3,)]])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_slot_folds_tiny_and_ragged_shapes(engine, mode, shapes):
+    """The row-table fold (K1r) at shard sizes below one lane group, around the 64-element
+    alignment and with tensors of 1-3 params, folded in batches of 1, any arrival order."""
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(90 + mode + 7 * len(shapes))
+    n_assigned = 9
+    diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in range(n_assigned)}
+    weights = {w: float(rng.uniform(0.5, 3.0)) for w in range(n_assigned)}
+    reporters = [w for w in range(n_assigned) if w not in (0, 4)]
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    ckpt_pb = build_state_fast(ckpt)
+    inc = IncrementalCycle(engine, [int(np.prod(s)) for s in shapes], mode=mode, slots=4, fold_batch=1,
+                           weights_by_worker=weights if mode == 2 else None, checkpoint=ckpt_pb)
+    for w in range(n_assigned):
+        inc.assigned(w)
+    order = list(reporters)
+    rng.shuffle(order)
+    for w in order:
+        inc.reported(w, build_state_fast(diffs[w]))
+    new = inc.close(ckpt_pb)
+    ref = [diffs[w] for w in sorted(reporters)]
+    want = (O.fedavg_mean(ckpt, ref) if mode == 0 else O.fedavg_iterative(ckpt, ref) if mode == 1 else
+            O.fedavg_weighted(ckpt, ref, np.array([weights[w] for w in sorted(reporters)], F)))
+    for got, w in zip(parse_state(new), want):
+        assert np.array_equal(bits(got), bits(w))
