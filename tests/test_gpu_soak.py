@@ -165,3 +165,40 @@ def test_overwrite_waits_for_folds_on_both_streams(engine):
     idx = np.unique(np.concatenate([rng.integers(0, P, 1000), [0, P - 1]])).astype(np.int64)
     d = np.stack([O.synth_diff(77, k, idx.astype(np.uint64)) for k in range(N)])
     assert same(out.cpu().numpy()[idx], coracle.fedavg(0, d, c[idx]))
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_report_cycles(engine, seed):
+    """Report-time aggregation under random pressure: model sizes on and off the block grid, 1-40
+    assigned workers with random non-reporters, random slot budgets (down to 2) and fold batches,
+    shuffled arrival, three chained cycles on one engine (each cycle's output is the next one's
+    checkpoint) -- every close bit-exact against the oracle's fold in WorkerCycle-id order."""
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(5000 + seed)
+    P = int(rng.choice(SIZES))
+    cut = sorted(int(x) for x in rng.choice(np.arange(1, P), size=min(2, P - 1), replace=False)) if P > 2 else []
+    numel = [b - a for a, b in zip([0] + cut, cut + [P])]
+    mode = int(rng.integers(0, 3))
+    ckpt = [(rng.standard_normal(n) * 0.05).astype(F) for n in numel]
+    for _ in range(3):
+        n = int(rng.integers(1, 41))
+        reporters = sorted(int(w) for w in rng.choice(n, size=int(rng.integers(1, n + 1)), replace=False))
+        diffs = {w: [(rng.standard_normal(k) * 1e-2).astype(F) for k in numel] for w in reporters}
+        weights = {w: float(rng.uniform(0.5, 3.0)) for w in range(n)}
+        ck_pb = build_state_fast(ckpt)
+        inc = IncrementalCycle(engine, numel, mode=mode, slots=int(rng.integers(2, n + 2)),
+                               fold_batch=int(rng.integers(1, 9)), weights_by_worker=weights if mode == 2 else None,
+                               checkpoint=ck_pb if rng.random() < 0.5 else None)
+        for w in range(n):
+            inc.assigned(w)
+        for w in rng.permutation(reporters):
+            inc.reported(int(w), build_state_fast(diffs[int(w)]))
+        got = parse_state(inc.close(ck_pb))
+        ref = [diffs[w] for w in reporters]
+        want = (O.fedavg_mean(ckpt, ref) if mode == 0 else O.fedavg_iterative(ckpt, ref) if mode == 1 else
+                O.fedavg_weighted(ckpt, ref, np.array([weights[w] for w in reporters], F)))
+        for g, w in zip(got, want):
+            assert same(g, w)
+        ckpt = [np.asarray(g, F).reshape(-1) for g in got]
