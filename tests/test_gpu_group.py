@@ -308,3 +308,52 @@ def test_device_pointer_calls_refused_on_a_group(group2):
         group2.slab()
     kid = group2.child(1)
     assert kid.slab()[0] != 0  # the child context owns a real slab
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_group_random_cycles(group2, group3, seed):
+    """Randomized chained cycles on 2- and 3-child groups: model sizes from 1 param (one active
+    child) to off-grid shards, close-time State closes and report-time cycles alternating, every
+    mode, each cycle's output feeding the next -- bit-exact against the oracle."""
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(7000 + seed)
+    eng = group2 if seed % 2 else group3
+    P = int(rng.choice([1, 5, 64, 65, 129, 191, 4_099, 70_001, 262_147]))
+    cut = sorted(int(x) for x in rng.choice(np.arange(1, P), size=min(2, P - 1), replace=False)) if P > 2 else []
+    numel = [b - a for a, b in zip([0] + cut, cut + [P])]
+    ckpt = [(rng.standard_normal(k) * 0.05).astype(F) for k in numel]
+    agg = CycleAggregator(eng)
+    for step in range(3):
+        n = int(rng.integers(1, 13))
+        mode = int(rng.integers(0, 3))
+        reporters = sorted(int(w) for w in rng.choice(n, size=int(rng.integers(1, n + 1)), replace=False))
+        diffs = {w: [(rng.standard_normal(k) * 1e-2).astype(F) for k in numel] for w in reporters}
+        weights = {w: float(rng.uniform(0.5, 3.0)) for w in range(n)}
+        ref = [diffs[w] for w in reporters]
+        wv = np.array([weights[w] for w in reporters], F)
+        ck_pb = build_state_fast(ckpt)
+        if step % 2 == 0:
+            plan = None
+            if mode == 1:
+                def plan(avg, item, num):  # 01-Create-plan.ipynb:450-454
+                    return [(a * num + i) / (num + 1) for a, i in zip(avg, item)]
+            new = agg.average_plan_diffs({"iterative_plan": mode == 1}, ck_pb, [build_state_fast(diffs[w]) for w in reporters],
+                                         plan, weights=wv if mode == 2 else None)
+        else:
+            inc = IncrementalCycle(eng, numel, mode=mode, slots=int(rng.integers(2, n + 2)),
+                                   fold_batch=int(rng.integers(1, 5)), weights_by_worker=weights if mode == 2 else None,
+                                   checkpoint=ck_pb)
+            for w in range(n):
+                inc.assigned(w)
+            for w in rng.permutation(reporters):
+                inc.reported(int(w), build_state_fast(diffs[int(w)]))
+            new = inc.close(ck_pb)
+        want = (O.fedavg_mean(ckpt, ref) if mode == 0 else O.fedavg_iterative(ckpt, ref) if mode == 1 else
+                O.fedavg_weighted(ckpt, ref, wv))
+        got = parse_state(new)
+        for g, w in zip(got, want):
+            assert np.array_equal(bits(g), bits(w))
+        ckpt = [np.asarray(g, F).reshape(-1) for g in got]
