@@ -193,3 +193,37 @@ def test_cycle_aggregator_secure_aggregate_states(engine):
     want = O.secagg_sum(sh)
     assert np.array_equal(s, want)
     assert np.array_equal(d.view(np.uint32), O.fix_prec_decode(want).view(np.uint32))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_share_state_random_value_mixes(engine, seed):
+    """k_varint_decode under random mixes: windows of only 1-byte varints (4,096 values per 4 KiB
+    window, the longest rank list), only 10-byte ones, runs of each, random tensor splits and party
+    counts -- the decoded sum bit-exact against the oracle over google.protobuf-parsed shares."""
+    rng = np.random.default_rng(900 + seed)
+    P = int(rng.choice([1, 17, 4_096, 4_097, 65_536, 70_001, 150_000]))
+    cut = sorted(int(x) for x in rng.choice(np.arange(1, P), size=min(3, P - 1), replace=False)) if P > 3 else []
+    numel = [b - a for a, b in zip([0] + cut, cut + [P])]
+    S, N = int(rng.integers(1, 4)), int(rng.integers(1, 4))
+
+    def values():
+        kind = rng.integers(0, 4)
+        if kind == 0:
+            return rng.integers(0, 128, P).astype(np.int64)             # 1-byte varints only
+        if kind == 1:
+            return -rng.integers(1, 2**62, P, dtype=np.int64)           # negative: 10 bytes each
+        if kind == 2:                                                   # runs of short and long values
+            v = rng.integers(0, 128, P).astype(np.int64)
+            for a in rng.integers(0, P, 8):
+                v[a:a + int(rng.integers(1, 5000))] = -7
+            return v
+        return every_length_values(P, rng)
+
+    sh = np.stack([np.stack([values() for _ in range(S)]) for _ in range(N)])
+    engine.set_layout(numel)
+    engine.reserve(N, 1, S)
+    ingest_all(engine, numel, sh)
+    s, d = engine.secagg(10, 3)
+    want = O.secagg_sum(sh)
+    assert np.array_equal(s, want)
+    assert np.array_equal(d.view(np.uint32), O.fix_prec_decode(want).view(np.uint32))
