@@ -202,3 +202,54 @@ def test_random_report_cycles(engine, seed):
         for g, w in zip(got, want):
             assert same(g, w)
         ckpt = [np.asarray(g, F).reshape(-1) for g in got]
+
+
+def test_many_closes_hold_device_and_host_memory_steady():
+    """A node closes cycles for as long as it runs: 300 MNIST closes (bytes path) and 100
+    report-time cycles on one engine must not grow device or host memory (no per-close leak of
+    slabs, events, pinned pieces or fresh outputs)."""
+    import ctypes as C
+    import resource
+
+    import torch
+
+    from pygrid_amd import Engine
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast
+
+    hip = C.CDLL("libamdhip64.so.7")
+
+    def dev_free():
+        free, total = C.c_size_t(0), C.c_size_t(0)
+        assert hip.hipMemGetInfo(C.byref(free), C.byref(total)) == 0
+        return free.value
+
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(77)
+    shapes = [(392, 784), (392,), (10, 392), (10,)]
+    numel = [int(np.prod(s)) for s in shapes]
+    ck = build_state_fast([(rng.standard_normal(s) * 0.05).astype(F) for s in shapes])
+    ds = [build_state_fast([(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes]) for _ in range(3)]
+    with Engine(0) as eng:
+        agg = CycleAggregator(eng)
+
+        def round_of_closes(k):
+            new = ck
+            for _ in range(k):
+                new = agg.average_plan_diffs({}, new, ds)
+            for _ in range(k // 3):
+                inc = IncrementalCycle(eng, numel, slots=3, fold_batch=1, checkpoint=new)
+                for w in range(4):
+                    inc.assigned(w)
+                for w in (2, 1, 3):
+                    inc.reported(w, ds[w - 1])
+                new = inc.close(new)
+            eng.sync()
+
+        round_of_closes(30)  # warm: allocations that persist across cycles happen here
+        free0, rss0 = dev_free(), resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+        round_of_closes(300)
+        free1, rss1 = dev_free(), resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    assert free0 - free1 < (8 << 20), f"device memory fell by {(free0 - free1) >> 20} MiB over 400 closes"
+    assert rss1 - rss0 < 64 * 1024, f"peak host RSS grew by {(rss1 - rss0) // 1024} MiB over 400 closes"
