@@ -717,7 +717,7 @@ def test_secagg_decode_device_edges(engine):
         engine.secagg_decode_device(t.data_ptr(), 4, d.data_ptr(), 1, 3)  # bad base
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 6, 11, 12, 14, 15, 17])
+@pytest.mark.parametrize("variant", [-1, 0, 6, 11, 12, 13, 14, 15, 17, 18])
 def test_iterative_division_shortcut_edges(engine, variant):
     """The iterative fold's reciprocal-multiply division (div shortcut in pgh_kernels.hip) around
     its fallback threshold |t| ~ 2^-125 * (k + 1), subnormals, zeros of both signs, overflow to
@@ -757,13 +757,25 @@ def test_iterative_division_exact_subnormal_midpoints(engine):
     d = np.zeros((N, P), F)
     d[97] = T.view(F)
     c = np.zeros(P, F)
-    for variant in (-1, 0, 14, 17):
+    for variant in (-1, 0, 13, 14, 17, 18):
         engine.set_variant(variant)
         try:
             got = run_f32(engine, d, c, 1)
         finally:
             engine.set_variant(-1)
         assert same(got, coracle.fedavg(1, d, c)), variant
+
+
+@pytest.mark.parametrize("P", [150_001, 250_000, 359_999, 400_003])
+def test_iterative_auto_variant_mid_sizes(engine, P):
+    """The auto choice for the iterative fold changes at 200 K and 360 K params (v14 / v13 / v0):
+    each side of both edges bit-exact against the scalar C oracle."""
+    rng = np.random.default_rng(P % 1000)
+    N = 12
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    engine.set_variant(-1)
+    assert same(run_f32(engine, d, c, 1), coracle.fedavg(1, d, c))
 
 
 def test_non_iterative_mean_plan_is_accelerated(engine):
