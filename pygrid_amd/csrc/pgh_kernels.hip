@@ -754,10 +754,14 @@ hipError_t dispatch_fedavg(const FedavgArgs& a, int variant, hipStream_t s) {
 int auto_variant(int64_t p, int mode) {
     if (p < 80000) return mode == MODE_ITERATIVE ? 17 : 14;
     if (p < 200000) return mode == MODE_ITERATIVE ? 14 : 11;
-    // the iterative fold between 200 K and 786 K params: one param per lane in 256-thread blocks
-    // up to ~360 K (v13: 5.9-6.6 TB/s vs v11's 4.5-5.4 at 200-311 K x 1,000), the 16-byte
-    // columns of v0 above it (6.3-6.7 vs 6.1-6.5), r02ar / r02as
-    if (p < 786432) return mode == MODE_ITERATIVE ? (p < 360000 ? 13 : 0) : 11;
+    // between 200 K and 786 K params: the iterative fold takes one param per lane in 256-thread
+    // blocks up to ~360 K (v13: 5.9-6.6 TB/s vs v11's 4.5-5.4 at 200-311 K x 1,000) and the
+    // 16-byte columns of v0 above (6.3-6.7 vs 6.1-6.5); the mean takes v13 up to ~360 K too
+    // (6.5 vs 5.9 at 200 K, equal at 250-350 K); weighted stays on v11 (mixed), r02ar-r02au
+    if (p < 786432) {
+        if (mode == MODE_ITERATIVE) return p < 360000 ? 13 : 0;
+        return mode == MODE_MEAN && p < 360000 ? 13 : 11;
+    }
     return 0;  // r01p (masked last batch): mean 6918, iterative 6910, weighted 6905 (v15 6647)
 }
 

@@ -766,16 +766,17 @@ def test_iterative_division_exact_subnormal_midpoints(engine):
         assert same(got, coracle.fedavg(1, d, c)), variant
 
 
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("P", [150_001, 250_000, 359_999, 400_003])
-def test_iterative_auto_variant_mid_sizes(engine, P):
-    """The auto choice for the iterative fold changes at 200 K and 360 K params (v14 / v13 / v0):
-    each side of both edges bit-exact against the scalar C oracle."""
-    rng = np.random.default_rng(P % 1000)
+def test_auto_variant_mid_sizes(engine, P, mode):
+    """The auto choice changes at 200 K and 360 K params (iterative v14 / v13 / v0, mean v11 / v13
+    / v11): each side of both edges bit-exact against the scalar C oracle."""
+    rng = np.random.default_rng(P % 1000 + mode)
     N = 12
     d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
     c = rng.standard_normal(P).astype(F)
     engine.set_variant(-1)
-    assert same(run_f32(engine, d, c, 1), coracle.fedavg(1, d, c))
+    assert same(run_f32(engine, d, c, mode), coracle.fedavg(mode, d, c))
 
 
 def test_non_iterative_mean_plan_is_accelerated(engine):
