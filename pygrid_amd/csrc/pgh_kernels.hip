@@ -752,7 +752,14 @@ hipError_t dispatch_fedavg(const FedavgArgs& a, int variant, hipStream_t s) {
 // blocks (CU balance); below ~200K params one param per lane (lanes), with deeper row pipelines
 // for the iterative fold of the smallest shards (few waves: latency).
 int auto_variant(int64_t p, int mode) {
-    if (p < 80000) return mode == MODE_ITERATIVE ? 17 : 14;
+    // under 80 K params (many clients per launch): the mean's 64-row walk (v17) up to ~45 K
+    // (+10-37 % over v14 at 10-40 K x 3,000), the iterative fold's 32-row walk in 128-thread blocks
+    // (v18) from ~35 K (+7-29 % over v17 at 40-65 K; below that the division chain ties them all),
+    // weighted unchanged, r02ax / r02ay
+    if (p < 80000) {
+        if (mode == MODE_ITERATIVE) return p < 35000 ? 17 : 18;
+        return mode == MODE_MEAN && p < 45000 ? 17 : 14;
+    }
     if (p < 200000) return mode == MODE_ITERATIVE ? 14 : 11;
     // between 200 K and 786 K params: the iterative fold takes one param per lane in 256-thread
     // blocks up to ~360 K (v13: 5.9-6.6 TB/s vs v11's 4.5-5.4 at 200-311 K x 1,000) and the

@@ -766,8 +766,8 @@ def test_iterative_division_exact_subnormal_midpoints(engine):
         assert same(got, coracle.fedavg(1, d, c)), variant
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("P", [150_001, 250_000, 359_999, 400_003])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("P", [30_001, 40_000, 65_000, 150_001, 250_000, 359_999, 400_003])
 def test_auto_variant_mid_sizes(engine, P, mode):
     """The auto choice changes at 200 K and 360 K params (iterative v14 / v13 / v0, mean v11 / v13
     / v11): each side of both edges bit-exact against the scalar C oracle."""
@@ -775,8 +775,9 @@ def test_auto_variant_mid_sizes(engine, P, mode):
     N = 12
     d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
     c = rng.standard_normal(P).astype(F)
+    w = rng.uniform(0.5, 2.0, N).astype(F) if mode == 2 else None
     engine.set_variant(-1)
-    assert same(run_f32(engine, d, c, mode), coracle.fedavg(mode, d, c))
+    assert same(run_f32(engine, d, c, mode, w), coracle.fedavg(mode, d, c, w))
 
 
 def test_non_iterative_mean_plan_is_accelerated(engine):
