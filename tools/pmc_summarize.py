@@ -74,6 +74,8 @@ def main():
                       "formula": "(2*FETCH_SIZE + WRITE_SIZE)*1024",
                       "source": f"{dst}/pmc_summary.json (rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, "
                                 f"separate passes)"}
+    if not summary:  # no PMC passes under src: keep the committed traffic file as it is
+        raise SystemExit(f"no pmc_<workload>_FETCH_SIZE passes under {src}; nothing written")
     sha = kernels_sha256()
     for e in summary.values():
         e["kernels_sha256"] = sha
