@@ -760,7 +760,9 @@ int auto_variant(int64_t p, int mode) {
         if (mode == MODE_ITERATIVE) return p < 35000 ? 17 : 18;
         return mode == MODE_MEAN && p < 45000 ? 17 : 14;
     }
-    if (p < 200000) return mode == MODE_ITERATIVE ? 14 : 11;
+    // 80-125 K: the weighted fold on one param per lane with 16 rows in flight (v12: +21 % at
+    // 100 K x 3,000; at 150-190 K v11 matches or beats it, r02bc / r02bd)
+    if (p < 200000) return mode == MODE_ITERATIVE ? 14 : mode == MODE_WEIGHTED && p < 125000 ? 12 : 11;
     // between 200 K and 786 K params: the iterative fold takes one param per lane in 256-thread
     // blocks up to ~360 K (v13: 5.9-6.6 TB/s vs v11's 4.5-5.4 at 200-311 K x 1,000) and the
     // 16-byte columns of v0 above (6.3-6.7 vs 6.1-6.5); the mean takes v13 up to ~360 K too

@@ -767,7 +767,7 @@ def test_iterative_division_exact_subnormal_midpoints(engine):
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
-@pytest.mark.parametrize("P", [30_001, 40_000, 65_000, 150_001, 250_000, 359_999, 400_003])
+@pytest.mark.parametrize("P", [30_001, 40_000, 65_000, 100_003, 150_001, 250_000, 359_999, 400_003])
 def test_auto_variant_mid_sizes(engine, P, mode):
     """The auto choice changes at 200 K and 360 K params (iterative v14 / v13 / v0, mean v11 / v13
     / v11): each side of both edges bit-exact against the scalar C oracle."""
