@@ -112,9 +112,10 @@ SIGNATURES = {
     "pgh_state_patch": (_i, [C.c_char_p, _sz, _vp, _i64, _vp]),
     "pgh_state_fresh": (_i, [C.c_char_p, _sz, _P64, _i, _vp, _sz, C.POINTER(_sz)]),
     "pgh_b64_decoded_cap": (_sz, [_sz]),
-    "pgh_b64_decode": (_i, [C.c_char_p, _sz, _vp, C.POINTER(_sz), _i]),
-    "pgh_b64_clean_size": (_i, [C.c_char_p, _sz, C.POINTER(_sz)]),
-    "pgh_b64_decode_clean": (_i, [C.c_char_p, _sz, _vp, _sz, C.POINTER(_sz), _i]),
+    # the text argument is a bytes object or an address (a str's own ASCII buffer: report.py)
+    "pgh_b64_decode": (_i, [_vp, _sz, _vp, C.POINTER(_sz), _i]),
+    "pgh_b64_clean_size": (_i, [_vp, _sz, C.POINTER(_sz)]),
+    "pgh_b64_decode_clean": (_i, [_vp, _sz, _vp, _sz, C.POINTER(_sz), _i]),
 }
 
 ABI_VERSION = 4  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)

@@ -154,3 +154,20 @@ def test_decode_into_capacity_and_clean_size():
     assert lib.pgh_b64_clean_size(bad_tail, len(bad_tail), C.byref(n)) == -5
     with pytest.raises(binascii.Error):
         b64decode(bad_tail)
+
+
+def test_str_text_is_decoded_in_place():
+    """The report's JSON yields a str: decoded from the str's own ASCII buffer (no encode copy),
+    same bytes as base64.b64decode; non-ASCII text raises ValueError as base64 does."""
+    import base64
+
+    from pygrid_amd.report import b64decode
+
+    data = np.random.default_rng(3).integers(0, 256, 300_001, dtype=np.uint8).tobytes()
+    text = base64.b64encode(data).decode("ascii")
+    assert b64decode(text) == base64.b64decode(text) == data
+    assert b64decode(text[:1000]) == base64.b64decode(text[:1000])
+    with pytest.raises(ValueError):
+        base64.b64decode("QUJDé")
+    with pytest.raises(ValueError):
+        b64decode("QUJDé")

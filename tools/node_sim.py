@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""What a PyGrid node sees per cycle with the engine wired in: the
+report handler's work for each client (fl_events.py:257-261: the JSON's base64 diff text ->
+bytes -> submit), here `report.b64decode` + `IncrementalCycle.reported` (the diff straight into
+an HBM slot), and the close when the cycle ends (cycle_manager.py:217).  ResNet-18, 100 workers
+assigned per cycle, ~20 % never report (routes.py:314), shuffled arrival, several cycles chained
+through the resident checkpoint.
+
+    python tools/node_sim.py [cycles]
+
+Prints one JSON line: per-report handler latency (decode, ingest, total: p50 / p99 / max) and the
+close latency per cycle.
+"""
+import base64
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import numpy as np  # noqa: E402
+
+from pygrid_amd import Engine  # noqa: E402
+from pygrid_amd.incremental import IncrementalCycle  # noqa: E402
+from pygrid_amd.report import b64decode  # noqa: E402
+from pygrid_amd.state_schema import build_state_fast  # noqa: E402
+from pygrid_amd.workloads import RESNET18_SHAPES  # noqa: E402
+
+
+def pct(xs, q):
+    return round(float(np.percentile(xs, q)), 3)
+
+
+def main():
+    cycles = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    rng = np.random.default_rng(2024)
+    numel = [int(np.prod(s)) for s in RESNET18_SHAPES]
+    ckpt = build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in RESNET18_SHAPES])
+    # the report payload as the JSON carries it: base64 text of the State diff (4 distinct diffs, re-sent)
+    texts = [base64.b64encode(build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2)
+                                                for s in RESNET18_SHAPES])).decode("ascii") for _ in range(4)]
+    eng = Engine(0)
+    phases = {}
+    if "--phases" in sys.argv:  # time the engine calls inside close (as tools/time_report_close.py)
+        import functools
+
+        from pygrid_amd import state as st
+
+        def wrap(obj, name):
+            f = getattr(obj, name)
+
+            @functools.wraps(f)
+            def g(*a, **k):
+                t0 = time.perf_counter()
+                r = f(*a, **k)
+                phases[name] = round(phases.get(name, 0) + (time.perf_counter() - t0) * 1e3, 3)
+                return r
+            setattr(obj, name, g)
+        for nm in ("fold_slots_finish_resident", "ckpt_patch_into", "fold_slots"):
+            wrap(eng, nm)
+        wrap(st, "fresh_frame_bytes")
+    dec, ing, tot, closes, close_phases = [], [], [], [], []
+    for cyc in range(cycles + 1):  # cycle 0 warms up
+        n = 100
+        reporters = [w for w in range(n) if rng.random() >= 0.2]
+        inc = IncrementalCycle(eng, numel, slots=n, fold_batch=8, checkpoint=ckpt)
+        for w in range(n):
+            inc.assigned(w)
+        for w in rng.permutation(reporters):
+            t0 = time.perf_counter()
+            diff = b64decode(texts[int(w) % 4])  # fl_events.py:257
+            t1 = time.perf_counter()
+            inc.reported(int(w), diff)           # submit_worker_diff, cycle_manager.py:151-178
+            t2 = time.perf_counter()
+            if cyc:
+                dec.append((t1 - t0) * 1e3)
+                ing.append((t2 - t1) * 1e3)
+                tot.append((t2 - t0) * 1e3)
+        time.sleep(0.05)  # the cycle ends some time after the last report (cycle.end timer)
+        phases.clear()
+        t0 = time.perf_counter()
+        ckpt = inc.close(ckpt)
+        if cyc:
+            closes.append((time.perf_counter() - t0) * 1e3)
+            close_phases.append(dict(phases, folded_before_close=inc.folded_early))
+    eng.close()
+    print(json.dumps({
+        "workload": "ResNet-18 (62 tensors), 100 assigned per cycle, ~20 % never report, shuffled arrival, "
+                    "base64 text -> report.b64decode -> IncrementalCycle.reported; close 50 ms after the last report",
+        "cycles": cycles, "reports": len(tot),
+        "report_b64decode_ms": {"p50": pct(dec, 50), "p99": pct(dec, 99), "max": round(max(dec), 3)},
+        "report_ingest_ms": {"p50": pct(ing, 50), "p99": pct(ing, 99), "max": round(max(ing), 3)},
+        "report_handler_ms": {"p50": pct(tot, 50), "p99": pct(tot, 99), "max": round(max(tot), 3)},
+        "close_ms": [round(c, 3) for c in closes], "close_phases_ms": close_phases}))
+
+
+if __name__ == "__main__":
+    main()

@@ -3,7 +3,7 @@
 ~83 report in shuffled order, worker 0 never): every Engine call and codec step inside
 IncrementalCycle.close timed, per cycle.
 
-    python tools/time_report_close.py [cycles]
+    python tools/time_report_close.py [cycles] [--idle SECONDS] [--profile]
 """
 import functools
 import sys
@@ -57,6 +57,8 @@ for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
     for w in arrival:
         inc.reported(w, distinct[w % 4])
     eng.sync()
+    if "--idle" in sys.argv:  # the cycle ends some time after the last report (cycle.end timer)
+        time.sleep(float(sys.argv[sys.argv.index("--idle") + 1]))
     T.clear()
     import gc
     gc0 = gc.get_count()
