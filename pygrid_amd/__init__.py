@@ -9,11 +9,13 @@ The product is ``libpygrid_hip.so`` (C ABI: ``include/pgh_api.h``; gfx950 HIP ke
 * ``sharding``            -- parameter-axis shards + RCCL all-gather across GPUs
 
 Nothing here computes on the CPU: without the built library and a GPU the engine raises.
-Importing the package raises HIP's hardware-queue count (``hipenv``) when HIP is not yet up.
+Importing the package raises HIP's hardware-queue count (``hipenv``) when HIP is not yet up and
+keeps big host buffers on glibc's heap (``hostmem``; ``PGH_MALLOC_TUNE=0`` opts out).
 """
-from . import hipenv
+from . import hipenv, hostmem
 
 hipenv.prepare()
+hostmem.tune()
 
 from .exceptions import (AggregationError, EngineUnavailableError, ModelNotAcceleratedError, PlanNotAcceleratedError,
                          PyGridError, StateParseError)

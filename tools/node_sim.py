@@ -79,10 +79,14 @@ def main():
         time.sleep(0.05)  # the cycle ends some time after the last report (cycle.end timer)
         phases.clear()
         t0 = time.perf_counter()
-        ckpt = inc.close(ckpt)
+        new = inc.close(ckpt)
+        t1 = time.perf_counter()
+        ckpt = new  # the previous checkpoint's bytes are freed here (the node drops them after the save)
+        t2 = time.perf_counter()
         if cyc:
-            closes.append((time.perf_counter() - t0) * 1e3)
-            close_phases.append(dict(phases, folded_before_close=inc.folded_early))
+            closes.append((t2 - t0) * 1e3)
+            close_phases.append(dict(phases, close_call=round((t1 - t0) * 1e3, 3), free_old=round((t2 - t1) * 1e3, 3),
+                                     folded_before_close=inc.folded_early))
     eng.close()
     print(json.dumps({
         "workload": "ResNet-18 (62 tensors), 100 assigned per cycle, ~20 % never report, shuffled arrival, "
