@@ -245,6 +245,44 @@ def cpu_baseline(kind: str, P: int, seed: int, budget_s: float, n: int = 32, all
             "numpy_restatement_1_thread": round(gbs_np, 3), "cpu_model": cpu_model()}
 
 
+def in_reference_allocator(fn: str, kwargs: dict, blobs=None):
+    """Run ``bench.<fn>(**kwargs)`` in a child process with glibc's default allocator
+    (PGH_MALLOC_TUNE=0): importing pygrid_amd raises glibc's mmap threshold (pygrid_amd.hostmem),
+    which would also spare the reference's torch code its per-add page faults -- the node it
+    stands for runs without that.  ``blobs`` (name -> bytes) reach the child as files.  The child
+    never touches the GPU."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    tmp = Path(tempfile.mkdtemp(prefix="pgh_cpu_"))
+    try:
+        files = {}
+        for name, data in (blobs or {}).items():
+            paths = []
+            for i, b in enumerate(data if isinstance(data, (list, tuple)) else [data]):
+                f = tmp / f"{name}_{i}.bin"
+                f.write_bytes(b)
+                paths.append(str(f))
+            files[name] = paths if isinstance(data, (list, tuple)) else paths[0]
+        code = ("import json, sys; from pathlib import Path; sys.argv = ['bench.py']; import bench\n"
+                "spec = json.loads(sys.stdin.read())\n"
+                "kw = dict(spec['kwargs'])\n"
+                "for k, v in spec['files'].items():\n"
+                "    kw[k] = [Path(p).read_bytes() for p in v] if isinstance(v, list) else Path(v).read_bytes()\n"
+                "print(json.dumps(getattr(bench, spec['fn'])(**kw)))")
+        r = subprocess.run([sys.executable, "-c", code], cwd=str(ROOT), capture_output=True, text=True,
+                           input=json.dumps({"fn": fn, "kwargs": kwargs, "files": files}),
+                           env=dict(os.environ, PGH_MALLOC_TUNE="0"), timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError(f"CPU baseline child failed: {r.stderr.strip().splitlines()[-1:]}")
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        out["allocator"] = "glibc defaults (the reference node's): measured in a child without pygrid_amd's heap thresholds"
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def cpu_baseline_state(ck_pb: bytes, d_pbs, P: int, n_target: int, budget_s: float):
     """The node's whole bytes -> bytes cycle close on the host (oracle.cycle_close_state_torch:
     State parse + per-tensor torch.tensor conversion, mean, apply, serialize; cycle_manager.py:
@@ -583,7 +621,8 @@ def attach_cpu_baseline(ctx, args, rec, kind, P, n=32, note=None):
     (cpu_baseline above), on a bounded sample of the same P-param shard."""
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
         try:
-            rec["cpu_baseline"] = cpu_baseline(kind, P, args.seed, args.cpu_seconds, n=n)
+            rec["cpu_baseline"] = in_reference_allocator(
+                "cpu_baseline", {"kind": kind, "P": P, "seed": args.seed, "budget_s": args.cpu_seconds, "n": n})
             if note:
                 rec["cpu_baseline"]["sample"] += "; " + note
         except Exception as e:  # noqa: BLE001
@@ -762,7 +801,8 @@ def run_mnist_state(ctx, args, eng):
                  {"new_checkpoint_bytes": len(new), "first_close_ms_with_plan_probe": round(first_ms, 3),
                   "note": "latency-bound: host protobuf scan, 3 H2D copies and a 0.3M-param kernel"}, step_is="close")
     if not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline_state(ck_pb, d_pb, P, 3, 4.0)
+        rec["cpu_baseline"] = in_reference_allocator("cpu_baseline_state", {"P": P, "n_target": 3, "budget_s": 4.0},
+                                                     {"ck_pb": ck_pb, "d_pbs": list(d_pb)})
     return rec
 
 
@@ -802,7 +842,8 @@ def run_resnet18_state(ctx, args, eng, N):
     rec = record(ctx, args, "resnet18-state", value, el, "f32", cfg,
                  roofline_of(st, "resnet18-state", eng.effective_variant(), "k_fedavg"), extra, step_is="close")
     if not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline_state(ck_pb, distinct[:3], P, N, 0.0)
+        rec["cpu_baseline"] = in_reference_allocator("cpu_baseline_state", {"P": P, "n_target": N, "budget_s": 0.0},
+                                                     {"ck_pb": ck_pb, "d_pbs": list(distinct[:3])})
     return rec
 
 
@@ -937,7 +978,8 @@ def run_resnet18_report(ctx, args, eng, N):
     rec = record(ctx, args, "resnet18-report", value, el, "f32", cfg,
                  roofline_of(st, "resnet18-report", eng.effective_variant(), "k_fedavg_rows"), extra, step_is="close")
     if not args.no_cpu_baseline:  # the reference decodes and folds every diff at close
-        rec["cpu_baseline"] = cpu_baseline_state(ck_pb, distinct[:3], P, nrep, 0.0)
+        rec["cpu_baseline"] = in_reference_allocator("cpu_baseline_state", {"P": P, "n_target": nrep, "budget_s": 0.0},
+                                                     {"ck_pb": ck_pb, "d_pbs": list(distinct[:3])})
     return rec
 
 
