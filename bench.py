@@ -45,9 +45,14 @@ sys.path.insert(0, str(ROOT))
 
 from pygrid_amd import hipenv  # noqa: E402
 
-# before anything touches HIP (the ranks this script spawns inherit it): >= 16 hardware queues,
-# so the N > 1 step's RCCL all-gather does not share a queue with the next range's fold
+# Before anything touches HIP (the ranks this script spawns inherit it), this harness ASKS for 16
+# hardware queues (PGH_HW_QUEUES: explicit, so hipenv applies it; an operator's own PGH_HW_QUEUES
+# wins), so the N > 1 step's RCCL all-gather does not share a queue with the next range's fold.
+# Importing pygrid_amd changes nothing by itself; the glibc thresholds are applied in main()
+# (pygrid_amd.tune_process), never in the CPU-baseline children.
+os.environ.setdefault("PGH_HW_QUEUES", str(hipenv.DEFAULT_HW_QUEUES))
 HW_QUEUES = hipenv.prepare()
+PROCESS_TUNING = {"hw_queues": HW_QUEUES, "malloc": False}
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
 METRIC = "client-diff GB/s aggregated (% of HBM peak) at 1/2/4/8 MI355X; cycle close ms"
@@ -102,6 +107,11 @@ def parse():
     ap.add_argument("--no-live-traffic", action="store_true",
                     help="N = 1 resident lines: skip the two rocprofv3 --pmc passes that measure roofline.traffic "
                          "in this run (the committed profiles/pmc_traffic.json is quoted instead)")
+    ap.add_argument("--no-group-line", action="store_true",
+                    help="N > 1 per-rank runs: skip the one-process group over the same GPUs measured after the "
+                         "ranks exit (the JSON line's `group` record)")
+    ap.add_argument("--no-tune", action="store_true",
+                    help="leave glibc's allocator thresholds alone (pygrid_amd.tune_process(malloc=...))")
     ap.add_argument("--dry-run", action="store_true",
                     help="form the world (gloo, no GPU), print the world size on rank 0 and exit")
     return ap.parse_args()
@@ -136,7 +146,9 @@ def spawn_ranks(args) -> int:
     the environment torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE,
     MASTER_ADDR=127.0.0.1, a free MASTER_PORT) and return the worst exit status.  The parent imports
     neither torch nor the engine, so it never touches a GPU; if one rank fails the others are
-    stopped (their own PIDs) instead of waiting in a collective forever."""
+    stopped (their own PIDs) instead of waiting in a collective forever.  Rank 0's result line is
+    held here; after every rank has exited, the one-process group over the same GPUs runs in a
+    fresh child (``group_line``) and its summary goes onto that line under ``group``."""
     import socket
     import subprocess
 
@@ -146,8 +158,10 @@ def spawn_ranks(args) -> int:
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
-                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   PGH_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None, text=True))
     rc = 0
     live = list(procs)
     while live:
@@ -163,7 +177,71 @@ def spawn_ranks(args) -> int:
         time.sleep(0.05)
     for p in procs:
         p.wait()
-    return rc
+    out = procs[0].stdout.read() if procs[0].stdout else ""
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    for ln in out.splitlines():
+        if not ln.startswith("{"):
+            print(ln, flush=True)
+    if rc != 0 or not lines:
+        return rc or 1
+    rec = json.loads(lines[-1])
+    if wants_group_line(args):
+        rec["group"] = group_line(args)
+    print(json.dumps(rec), flush=True)
+    return 0
+
+
+GROUP_WORKLOADS = {"resnet18-fedavg", "resnet18-iterative", "resnet18-weighted", "resnet18-secagg", "secagg-clients"}
+
+
+def wants_group_line(args) -> bool:
+    return args.gpus > 1 and not args.group and not args.no_group_line and args.workload in GROUP_WORKLOADS
+
+
+def group_line(args, limit_s: int = 900) -> dict:
+    """The path the node deploys at N > 1 (its single process drives every GPU through one library
+    context, ``pgh_create_group``), measured on the same GPUs right after
+    the per-rank world has exited: ``bench.py --group --gpus N`` in a FRESH child (no process that
+    touched a GPU re-execs), summarised for the per-rank line.  ``rccl`` says whether the group's
+    exchange ran over RCCL (distinct devices) or peer copies."""
+    import subprocess
+
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--group", "--gpus", str(args.gpus), "--workload",
+           args.workload, "--steps", str(args.steps), "--warmup", str(args.warmup), "--seed", str(args.seed),
+           "--no-cpu-baseline", "--no-live-traffic"]
+    if args.dry_run:
+        cmd.append("--dry-run")
+    if args.clients:
+        cmd += ["--clients", str(args.clients)]
+    if args.params:
+        cmd += ["--params", str(args.params)]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                        "PGH_BENCH_SPAWNED", "TORCHELASTIC_RUN_ID", "GROUP_RANK", "ROLE_RANK")}
+    print(f"bench.py: one-process group over {args.gpus} GPUs in a fresh child ({limit_s} s limit)", file=sys.stderr,
+          flush=True)
+    try:
+        r = subprocess.run(["timeout", "-k", "10", str(limit_s)] + cmd, cwd=str(ROOT), env=env, capture_output=True,
+                           text=True)
+    except OSError as e:
+        return {"error": f"group child did not start: {e}"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        tail = (r.stderr.strip().splitlines() or [""])[-1][:400]
+        return {"error": f"group child exited {r.returncode}: {tail}"}
+    g = json.loads(lines[-1])
+    if g.get("dry_run"):
+        return g
+    cfg = g.get("config", {})
+    out = {"value": g.get("value"), "unit": g.get("unit"), "n_gpus": g.get("n_gpus"),
+           "ms_per_step": g.get("ms_per_step"), "kernel_ms": g.get("kernel_ms"),
+           "pct_hbm_peak_per_gpu": g.get("pct_hbm_peak_per_gpu"),
+           "frac": (g.get("roofline") or {}).get("frac"), "rccl": cfg.get("rccl"),
+           "exchange": cfg.get("exchange"), "parallelism": cfg.get("parallelism"),
+           "devices": cfg.get("devices"), "command": " ".join(cmd[1:])}
+    if "cycle_close_e2e" in g:
+        out["cycle_close_e2e"] = g["cycle_close_e2e"]
+    return out
 
 
 def cpu_baseline(kind: str, P: int, seed: int, budget_s: float, n: int = 32, all_cores: int = 0):
@@ -462,6 +540,10 @@ class Ctx:
             formed = int(self.sum_over_ranks(1.0))
             if formed != args.gpus:
                 raise SystemExit(f"bench.py: formed a world of {formed} ranks, --gpus {args.gpus}")
+        # what the exchange really ran over: torch's "nccl" backend IS RCCL on ROCm
+        self.dist_backend = str(dist.get_backend()) if self.world > 1 else None
+        self.rccl_ranks = self.world if self.dist_backend == "nccl" else 0
+        self.coll = {"nccl": "RCCL", "gloo": "gloo (host)"}.get(self.dist_backend, self.dist_backend)
 
     def barrier(self):
         if self.world > 1:
@@ -515,7 +597,8 @@ def record(ctx, args, name, value, el, dt, config, roofline, extra=None, step_is
         "pct_hbm_peak_per_gpu": round(100 * value / ctx.n_gpus / HBM_PEAK_GBS, 2),
         ("kernel_ms" if step_is == "kernel" else "cycle_close_ms"): round(el / args.steps * 1e3, 4),
         "roofline": roofline, "cpu_baseline": None,
-        "hip_hw_queues": HW_QUEUES,
+        "hip_hw_queues": HW_QUEUES, "process_tuning": dict(PROCESS_TUNING),
+        "dist_backend": getattr(ctx, "dist_backend", None), "rccl_ranks": getattr(ctx, "rccl_ranks", 0),
     }
     if extra:
         rec.update(extra)
@@ -608,7 +691,7 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
                        + (f" x {parties} parties int64" if dtype == 1 else " fp32") + ", resident in HBM",
            "clients": N, "params_per_gpu": pg, "params_total": P,
            "parallelism": f"param-shard{ctx.world}" + (
-               f" + RCCL all-gather ({args.gather_chunks} ranges, last halved {args.gather_tail}x, overlapped with the fold)" if ctx.world > 1 else ""),
+               f" + {ctx.coll} all-gather ({args.gather_chunks} ranges, last halved {args.gather_tail}x, overlapped with the fold)" if ctx.world > 1 else ""),
            "kernel_variant": eng.effective_variant(mode if dtype == 0 else 16)}
     rec = record(ctx, args, args.workload, value, el, dt, cfg,
                  roofline_of(st, args.workload, cfg["kernel_variant"], kernel))
@@ -654,7 +737,7 @@ def run_secagg_clients(ctx, args, eng, N, S, P):
     cfg = {"workload": f"secagg-clients: {N} clients/GPU x {S} parties int64 x P={P} (ResNet-18) on every rank, "
                        "clients sharded, resident in HBM",
            "clients": N * ctx.world, "clients_per_gpu": N, "params_per_gpu": P, "params_total": P,
-           "parallelism": f"client-shard{ctx.world} + RCCL int64 reduce-scatter / decode / all-gather "
+           "parallelism": f"client-shard{ctx.world} + {ctx.coll or 'no'} int64 reduce-scatter / decode / all-gather "
                           f"({args.gather_chunks} ranges, last halved {args.gather_tail}x, overlapped with the share sum)",
            "kernel_variant": eng.effective_variant(16)}
     # roofline: the share-sum launches (k_secagg); the decode kernel (12 B/param) is not in the stats
@@ -694,7 +777,7 @@ def run_c4(ctx, args, eng, N, pg, P):
     cfg = {"workload": f"c4-stream: P_shard={pg} params/GPU x {N} clients fp32 (SURVEY 8(d) config 4 shard), "
                        f"{R}-slot HBM ring, {chunk}-client chunks generated on-device ({args.synth} generator)",
            "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R, "generator": args.synth,
-           "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
+           "parallelism": f"param-shard{ctx.world}" + (f" + {ctx.coll} all-gather" if ctx.world > 1 else ""),
            "kernel_variant": eng.effective_variant()}
     extra = {"fold_kernel_client_diff_GBps_aggregated": round(kern_gbs, 1),
              "note": "value includes on-device generation of every chunk (writes 4 B/param/client, "
@@ -742,7 +825,7 @@ def run_c5(ctx, args, eng, N, pg, P):
     cfg = {"workload": f"c5-ingest: P_shard={pg} params/GPU x {N} clients fp32 iterative plan (SURVEY 8(d) "
                        f"config 5 shard), pinned host -> HBM over PCIe, {R}-slot ring, fold batch 2",
            "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R,
-           "parallelism": f"param-shard{ctx.world}" + (" + RCCL all-gather" if ctx.world > 1 else ""),
+           "parallelism": f"param-shard{ctx.world}" + (f" + {ctx.coll} all-gather" if ctx.world > 1 else ""),
            "kernel_variant": eng.effective_variant(1)}
     extra = {"bound_by": "PCIe host->device (Gen5 x16, 63 GB/s spec per GPU)",
              "ingest_GBps_per_gpu": round(ingest_gbs, 2) if ingest_gbs else None,
@@ -770,7 +853,9 @@ def run_mnist_state(ctx, args, eng):
     ds = [[rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2) for s in MNIST_SHAPES] for _ in range(3)]
     ck_pb = build_state_fast(ck)
     d_pb = [build_state_fast(d) for d in ds]
-    agg = CycleAggregator(eng)
+    # config 1 hosts a non-iterative plan: the operator's opt-in lets the engine run it as MEAN
+    # once it probes bit-identical (pygrid_amd.cycle.mean_plan_policy; the default declines it)
+    agg = CycleAggregator(eng, mean_plans="probe")
 
     def avg_plan(diffs):  # config 1's hosted non-iterative avg plan: the plain mean (cycle_manager.py:270-271)
         import torch as th
@@ -1033,6 +1118,12 @@ def e2e_close(ctx, args, eng, n_clients: int, steps: int = 2):
                           "State bytes in host memory -> new checkpoint bytes (BASELINE.md cycle close; PCIe-inclusive)"}
 
 
+def group_exchange(eng) -> str:
+    """How a group's collective ran: RCCL (distinct devices) or the library's peer copies (repeated
+    devices, PGH_RCCL=0, or a group of one before its first collective)."""
+    return {1: "RCCL (ncclAllGather / ncclReduceScatter)", 0: "peer-copy"}.get(eng.group_backend(), "no collective")
+
+
 def run_group_resident(ctx, args, eng, mode, dtype, N, parties, Pg):
     """The resident configs on a one-process group: GPU g folds its Pg-param shard of a
     (G x Pg)-param model over all N clients (weak scaling like the per-rank runs), then the new
@@ -1069,8 +1160,9 @@ def run_group_resident(ctx, args, eng, mode, dtype, N, parties, Pg):
                        + (f" x {parties} parties int64" if dtype == 1 else " fp32") + ", resident in HBM",
            "clients": N, "params_per_gpu": Pg, "params_total": P,
            "parallelism": f"param-shard{G} in one process (pgh_create_group, one host thread per GPU)" + (
-               " + ncclAllGather of the new checkpoint" if dtype == 0 else " + host slices"),
-           "rccl": eng.group_backend() == 1, "kernel_variant": eng.effective_variant(mode if dtype == 0 else 16)}
+               f" + {group_exchange(eng)} all-gather of the new checkpoint" if dtype == 0 else " + host slices"),
+           "rccl": eng.group_backend() == 1, "exchange": group_exchange(eng), "devices": ctx.devices,
+           "kernel_variant": eng.effective_variant(mode if dtype == 0 else 16)}
     rec = record(ctx, args, args.workload, value, el, dt, cfg,
                  roofline_of(st, args.workload, cfg["kernel_variant"], kernel, G))
     for b in bufs:
@@ -1100,9 +1192,10 @@ def run_group_secagg_clients(ctx, args, eng, N, S, P):
     cfg = {"workload": f"secagg-clients: {N} clients/GPU x {S} parties int64 x P={P} (ResNet-18), clients sharded "
                        "over the GPUs of one process, resident in HBM",
            "clients": N * G, "clients_per_gpu": N, "params_per_gpu": P, "params_total": P,
-           "parallelism": f"client-shard{G} in one process (pgh_create_group) + ncclReduceScatter of the Z_2^64 sums "
-                          "+ per-GPU decode + host slices",
-           "rccl": eng.group_backend() == 1, "kernel_variant": eng.effective_variant(16)}
+           "parallelism": f"client-shard{G} in one process (pgh_create_group) + {group_exchange(eng)} reduce-scatter of "
+                          "the Z_2^64 sums + per-GPU decode + host slices",
+           "rccl": eng.group_backend() == 1, "exchange": group_exchange(eng), "devices": ctx.devices,
+           "kernel_variant": eng.effective_variant(16)}
     rec = record(ctx, args, "secagg-clients", value, el, "int64", cfg,
                  roofline_of(st, "secagg-clients", cfg["kernel_variant"], "k_secagg", G))
     for b in bufs:
@@ -1121,6 +1214,7 @@ def main_group(ctx, args):
     devices = [int(x) for x in devs.split(",")] if devs else list(range(args.gpus))
     if len(devices) != args.gpus:
         raise SystemExit(f"PGH_BENCH_DEVICES names {len(devices)} devices, --gpus {args.gpus}")
+    ctx.devices = devices
     eng = Engine(devices=devices)
     if args.variant is not None:
         eng.set_variant(args.variant)
@@ -1144,16 +1238,25 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.group:
         sys.exit(spawn_ranks(args))  # no launcher: form the N-rank world here (no GPU touched yet)
+    if not args.no_tune:
+        import pygrid_amd
+
+        # the harness opts in to the allocator thresholds a tuned node would use (the hardware
+        # queues were requested at import); cpu_baseline children run with glibc's defaults
+        PROCESS_TUNING.update(pygrid_amd.tune_process(hw_queues=False))
+        PROCESS_TUNING["hw_queues"] = HW_QUEUES
     global LIVE_TRAFFIC
     if (args.gpus == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.group and not args.dry_run
             and not args.no_live_traffic and args.workload in PMC_KERNEL and not under_profiler()):
         LIVE_TRAFFIC = measure_live_traffic(args)  # child processes; this one has not touched the GPU yet
     ctx = Ctx(args)
     if args.dry_run:
-        if ctx.rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": ctx.n_gpus, "backend": ctx.backend,
-                              "group": ctx.group}), flush=True)
+        rec = {"dry_run": True, "n_gpus": ctx.n_gpus, "backend": ctx.backend, "group": ctx.group}
         ctx.close()
+        if ctx.rank == 0:
+            if launched_elsewhere() and wants_group_line(args):
+                rec["group"] = group_line(args)
+            print(json.dumps(rec), flush=True)
         return
     if ctx.group:
         main_group(ctx, args)
@@ -1190,10 +1293,23 @@ def main():
         if args.workload == "resnet18-fedavg" and ctx.world == 1 and not args.no_e2e:
             # the bytes -> bytes close of the same config (BASELINE.md cycle close), beside the kernel line
             rec["cycle_close_e2e"] = e2e_close(ctx, args, eng, N)
-    if ctx.rank == 0:
-        print(json.dumps(rec), flush=True)
     eng.close()
+    del eng
+    if ctx.world > 1:
+        ctx.torch.cuda.synchronize()
+        ctx.torch.cuda.empty_cache()
+        ctx.barrier()  # every rank's slab is freed before the group child allocates on all GPUs
     ctx.close()
+    if ctx.rank == 0:
+        if launched_elsewhere() and wants_group_line(args):
+            rec["group"] = group_line(args)  # a fresh child: this process never re-execs
+        print(json.dumps(rec), flush=True)
+
+
+def launched_elsewhere() -> bool:
+    """True under torch.distributed.run (the driver's N > 1 launch): rank 0 runs the group line
+    itself.  Ranks this script spawned leave it to their parent (spawn_ranks)."""
+    return int(os.environ.get("WORLD_SIZE", "1")) > 1 and os.environ.get("PGH_BENCH_SPAWNED") != "1"
 
 
 if __name__ == "__main__":

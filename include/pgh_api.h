@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PGH_ABI_VERSION 4
+#define PGH_ABI_VERSION 5
 
 typedef struct pgh_ctx pgh_ctx;
 
@@ -192,6 +192,13 @@ int pgh_ckpt_patch_state(pgh_ctx* ctx, const uint8_t* tmpl, size_t n, uint8_t* o
  * same within a cycle. */
 int pgh_fold_slots(pgh_ctx* ctx, int mode, const int32_t* slots, int n);
 int pgh_fold_slots_finish_resident(pgh_ctx* ctx, int mode, const int32_t* slots, int n);
+/* Discard the running fold state of this cycle's slot folds (the diffs folded so far are gone
+ * from it; the next pgh_fold_slots starts again at fold client 0, and weights must be set again).
+ * Slots holding unfolded diffs keep them.  Used when the close-time order of the
+ * completed WorkerCycles (cycle_manager.py:243-245) differs from the order the early folds
+ * assumed, or a folded worker re-reported (submit_worker_diff overwrites its diff, :162-174):
+ * the caller then re-folds every diff in the query's order, bit-identical to the reference. */
+int pgh_fold_slots_restart(pgh_ctx* ctx);
 
 /* Z_2^64 share sum over all clients x parties, then decode float32(sum) / base**prec.
  * sum_out (int64) and dec_out (float32) are host arrays of P_shard; either may be NULL. */

@@ -87,6 +87,7 @@ SIGNATURES = {
     "pgh_fedavg_resident": (_i, [_vp, _i]),
     "pgh_fold_slots": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
     "pgh_fold_slots_finish_resident": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
+    "pgh_fold_slots_restart": (_i, [_vp]),
     "pgh_ckpt_download": (_i, [_vp, _vp]),
     "pgh_ckpt_patch_state": (_i, [_vp, C.c_char_p, _sz, _vp]),
     "pgh_secagg": (_i, [_vp, _i, _i, _vp, _vp]),
@@ -118,7 +119,7 @@ SIGNATURES = {
     "pgh_b64_decode_clean": (_i, [_vp, _sz, _vp, _sz, C.POINTER(_sz), _i]),
 }
 
-ABI_VERSION = 4  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
+ABI_VERSION = 5  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
 _LIB = None
 
 

@@ -748,10 +748,15 @@ int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>
             c->pin_next ^= 1;
             if (c->pin_used[cur_slot]) CK(c, hipEventSynchronize(c->pin_ev[cur_slot]));
             cur_len = std::min({total - off, c->pin_slot, c->d2h_piece});
-            if (piped) {  // wait for the fold range holding the piece's last element
-                const int64_t last = (int64_t)((off + cur_len + 3) / 4);
-                for (auto& m : c->final_marks)
-                    if (m.end >= last) { CK(c, hipStreamWaitEvent(s, m.ev, 0)); break; }
+            if (piped) {  // wait for EVERY fold range the piece's floats come from: the ranges
+                          // alternate over two streams, so the last one's mark orders nothing else
+                const int64_t first = (int64_t)(off / 4), last = (int64_t)((off + cur_len + 3) / 4);
+                int64_t start = 0;
+                for (auto& m : c->final_marks) {
+                    if (start >= last) break;
+                    if (m.end > first) CK(c, hipStreamWaitEvent(s, m.ev, 0));
+                    start = m.end;
+                }
             }
             CK(c, hipMemcpyAsync(c->h_pin[cur_slot], src + off, cur_len, hipMemcpyDeviceToHost, s));
             CK(c, hipEventRecord(c->pin_ev[cur_slot], s));
@@ -2041,6 +2046,21 @@ int pgh_fold_slots_finish_resident(pgh_ctx* c, int mode, const int32_t* slots, i
     const double t0 = now_ms();
     RC(slot_fold(c, mode, slots, n, true));
     c->st.close_ms_last = now_ms() - t0;
+    return PGH_OK;
+}
+
+int pgh_fold_slots_restart(pgh_ctx* c) {
+    if (c && c->grp) return pgh_group_api::fold_restart(c);
+    if (!c) return PGH_E_ARG;
+    RC(check_dtype(c, PGH_F32));
+    if (c->streaming) return fail(c, PGH_E_STATE, "context is streaming: slot folds need a RESIDENT slab");
+    // The next slot fold's FL_FIRST pass overwrites the fold state on c->stream, behind any fold
+    // still in flight there: nothing to wait for.
+    c->folded = 0;
+    c->st.n_folded = 0;
+    c->slot_mode = -1;
+    c->weights.clear();
+    c->weights_on_device = false;
     return PGH_OK;
 }
 

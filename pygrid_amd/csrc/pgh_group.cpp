@@ -798,6 +798,11 @@ int fold_slots(pgh_ctx* c, int mode, const int32_t* slots, int n, bool finish) {
     });
 }
 
+int fold_restart(pgh_ctx* c) {
+    RC(need_slab(c));
+    return fan(c, [](int, pgh_ctx* k) -> int { return pgh_fold_slots_restart(k); });
+}
+
 int secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out) {
     pgh_group* g = G(c);
     RC(need_slab(c));

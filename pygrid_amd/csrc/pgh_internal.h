@@ -64,6 +64,7 @@ int fedavg_resident(pgh_ctx* c, int mode);
 int ckpt_download(pgh_ctx* c, float* out);
 int ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out);
 int fold_slots(pgh_ctx* c, int mode, const int32_t* slots, int n, bool finish);
+int fold_restart(pgh_ctx* c);
 int secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out);
 int stream_begin(pgh_ctx* c, int kind, int fold_batch);
 int stream_flush(pgh_ctx* c);

@@ -7,8 +7,12 @@ Reference: ``CycleManager.complete_cycle`` / ``_average_plan_diffs``,
 * ``select_mode`` is the dispatch rule: no hosted plan -> hard-coded mean
   (``:273-288``); hosted plan + ``iterative_plan`` whose behaviour is the canonical
   ``(avg * num + item) / (num + 1)`` (``01-Create-plan.ipynb:450-454``) -> iterative mean
-  (``:266-269``); a hosted non-iterative plan (``:270-271``) whose output is bit-identical to
-  ``reduce(th.add) / N`` on probe inputs -> the hard-coded mean; anything else raises
+  (``:266-269``); a hosted non-iterative plan (``:270-271``) is user code the node runs itself
+  unless the operator opts in (``mean_plans="probe"`` / ``PGH_MEAN_PLANS=probe``): then a plan
+  whose output is bit-identical to ``reduce(th.add) / N`` on probe inputs -- including tensors of
+  the real model's ranks and layer count and the cycle's client count -- runs as the hard-coded
+  mean.  A probe cannot PROVE that a plan is the mean (a plan may special-case shapes or counts
+  the probe did not try), which is why it is opt-in.  Anything else raises
   ``PlanNotAcceleratedError`` so the node keeps running the reference code for it.
 * ``CycleAggregator.average_plan_diffs`` replaces the slice ``:240-303``: checkpoint bytes +
   diff bytes in, new checkpoint bytes out.  DB reads/writes and cycle bookkeeping stay with
@@ -71,10 +75,12 @@ def is_canonical_iterative_plan(avg_plan: Callable) -> bool:
     return True
 
 
-def _mean_probes():
+def _mean_probes(shapes=None, n_clients=None):
     """Probe inputs for a non-iterative plan: several client counts, values of mixed magnitude (so a
     re-associated or pairwise sum rounds differently), exact cancellations, signed zeros,
-    subnormals and an overflow to inf."""
+    subnormals and an overflow to inf.  With the real model's ``shapes``: also diffs of that many
+    tensors of the same ranks (every dimension clipped to 3, so the probe stays small), at 1, 2 and
+    3 clients and at the cycle's own client count ``n_clients``."""
     rng = np.random.default_rng(11)
     probes = []
     for n in (1, 2, 3, 7, 33):
@@ -85,6 +91,12 @@ def _mean_probes():
                                np.float32)
             diffs.append([mixed, special])
         probes.append(diffs)
+    if shapes:
+        small = [tuple(min(int(d), 3) for d in s) for s in shapes]
+        counts = sorted({1, 2, 3} | ({int(n_clients)} if n_clients and n_clients <= 4096 else set()))
+        for n in counts:
+            probes.append([[(rng.standard_normal(s) * 10.0 ** rng.integers(-4, 5, s)).astype(np.float32)
+                            for s in small] for _ in range(n)])
     return probes
 
 
@@ -97,15 +109,17 @@ def _reference_mean(diffs):
     return [th.div(reduce(th.add, col), len(diffs)).numpy() for col in cols]
 
 
-def is_mean_plan(avg_plan: Callable) -> bool:
+def is_mean_plan(avg_plan: Callable, shapes=None, n_clients=None) -> bool:
     """A hosted NON-iterative avg plan (called as ``avg_plan(diffs)``, cycle_manager.py:270-271) is
     user code; it maps to the hard-coded mean only if, on every probe, its output equals
     ``reduce(th.add) / N`` (:286-288) bit for bit (NaN-free probes; signed zeros, subnormals and
     infinities compared exactly).  Anything else -- another order of summation, a mean through a
-    pairwise reduction, a weighting, an exception -- leaves the plan to the node."""
+    pairwise reduction, a weighting, an exception -- leaves the plan to the node.  Passing the
+    model's ``shapes`` and the cycle's ``n_clients`` adds probes of that layer count, those ranks
+    and that client count."""
     import torch as th
 
-    for diffs in _mean_probes():
+    for diffs in _mean_probes(shapes, n_clients):
         try:
             res = avg_plan([[th.from_numpy(t.copy()) for t in d] for d in diffs])
             res = list(res)
@@ -124,23 +138,35 @@ def is_mean_plan(avg_plan: Callable) -> bool:
     return True
 
 
-_MODE_CACHE: dict = {}  # (sha256 of the plan's bytes, iterative flag) -> mode, or the decline message
+_MODE_CACHE: dict = {}  # (sha256 of the plan's bytes, iterative flag, mean-plan policy) -> mode, or the decline message
 _MODE_CACHE_MAX = 256
 
 
-def _plan_cache_key(server_config: dict, plan_key) -> Optional[tuple]:
+def mean_plan_policy(mean_plans: Optional[str] = None) -> str:
+    """"decline" (default: a non-iterative hosted plan runs in the node, as in the reference) or
+    "probe" (opt-in: a plan that probes bit-identical to the hard-coded mean runs as MEAN)."""
+    import os
+
+    got = mean_plans or os.environ.get("PGH_MEAN_PLANS", "decline")
+    if got not in ("decline", "probe"):
+        raise AggregationError(f"mean_plans must be 'decline' or 'probe', not {got!r}")
+    return got
+
+
+def _plan_cache_key(server_config: dict, plan_key, mean_plans: Optional[str] = None) -> Optional[tuple]:
     if plan_key is None:
         return None
     import hashlib
 
     raw = plan_key if isinstance(plan_key, (bytes, bytearray, memoryview)) else str(plan_key).encode()
-    return hashlib.sha256(raw).digest(), bool(server_config.get("iterative_plan", False))
+    iterative = bool(server_config.get("iterative_plan", False))
+    return hashlib.sha256(raw).digest(), iterative, None if iterative else mean_plan_policy(mean_plans)
 
 
-def cached_mode(server_config: dict, plan_key) -> Optional[int]:
+def cached_mode(server_config: dict, plan_key, mean_plans: Optional[str] = None) -> Optional[int]:
     """The dispatch decision already made for this hosted plan (its serialized bytes), or None.
     Raises PlanNotAcceleratedError again for a plan that was declined."""
-    key = _plan_cache_key(server_config, plan_key)
+    key = _plan_cache_key(server_config, plan_key, mean_plans)
     if key is None or key not in _MODE_CACHE:
         return None
     got = _MODE_CACHE[key]
@@ -149,28 +175,31 @@ def cached_mode(server_config: dict, plan_key) -> Optional[int]:
     return got
 
 
-def select_mode(server_config: dict, avg_plan: Optional[Callable] = None, weights=None, plan_key=None) -> int:
+def select_mode(server_config: dict, avg_plan: Optional[Callable] = None, weights=None, plan_key=None,
+                mean_plans: Optional[str] = None, shapes=None, n_clients=None) -> int:
     """Dispatch rule (module docstring).  ``plan_key`` -- the hosted plan's serialized bytes
     (``avg_plan_rec.value``, cycle_manager.py:256) -- caches the probe's verdict: a node's avg plan
     is fixed for its FL process, and probing a non-iterative plan costs ~2.6 ms of torch calls,
-    five times an MNIST close."""
+    five times an MNIST close.  ``mean_plans`` (or ``PGH_MEAN_PLANS``): see ``mean_plan_policy``;
+    ``shapes`` / ``n_clients``: the model's tensor shapes and the cycle's client count, probed too
+    (the verdict is cached for the plan's bytes, i.e. from the first cycle's shapes and count)."""
     if weights is not None:
         return WEIGHTED_MEAN
     if avg_plan is None:
         return MEAN  # "Fallback to simple hardcoded avg plan", cycle_manager.py:274
-    key = _plan_cache_key(server_config, plan_key)
+    key = _plan_cache_key(server_config, plan_key, mean_plans)
     if key is not None:
-        got = cached_mode(server_config, plan_key)
+        got = cached_mode(server_config, plan_key, mean_plans)
         if got is not None:
             return got
         try:
-            mode = _probe_mode(server_config, avg_plan)
+            mode = _probe_mode(server_config, avg_plan, mean_plans, shapes, n_clients)
         except PlanNotAcceleratedError as e:
             _remember(key, str(e))
             raise
         _remember(key, mode)
         return mode
-    return _probe_mode(server_config, avg_plan)
+    return _probe_mode(server_config, avg_plan, mean_plans, shapes, n_clients)
 
 
 def _remember(key, verdict):
@@ -179,9 +208,14 @@ def _remember(key, verdict):
     _MODE_CACHE[key] = verdict
 
 
-def _probe_mode(server_config: dict, avg_plan: Callable) -> int:
+def _probe_mode(server_config: dict, avg_plan: Callable, mean_plans=None, shapes=None, n_clients=None) -> int:
     if not server_config.get("iterative_plan", False):
-        if is_mean_plan(avg_plan):  # :270-271 with a plan that IS the hard-coded mean
+        if mean_plan_policy(mean_plans) != "probe":
+            raise PlanNotAcceleratedError("non-iterative hosted avg plan: user code, run by the node "
+                                          "(cycle_manager.py:270-271; opt in with mean_plans='probe')")
+        if callable(shapes):
+            shapes = shapes()
+        if is_mean_plan(avg_plan, shapes, n_clients):  # :270-271 with a plan that IS the hard-coded mean
             return MEAN
         raise PlanNotAcceleratedError("non-iterative hosted avg plan is not reduce(th.add) / N (cycle_manager.py:270-271)")
     if not is_canonical_iterative_plan(avg_plan):
@@ -204,15 +238,26 @@ def _decline_non_float32(pb: bytes, what: str):
         raise ModelNotAcceleratedError(f"{what} holds non-float32 tensors {bad[:8]} (the engine is fp32-only)")
 
 
+def _shapes_or_none(pb: bytes):
+    from . import state_schema
+
+    try:
+        return state_schema.tensor_shapes(pb)
+    except Exception:  # noqa: BLE001 -- malformed bytes: the engine's own parse reports them
+        return None
+
+
 class CycleAggregator:
     """Owns one Engine across cycles; the slab is re-used while it fits.  ``devices=[0, ..., 7]``
     gives the node's single process every GPU of the node (``pgh_create_group``: parameter shards,
     each GPU's slice of every diff over its own PCIe link, bit-identical results)."""
 
-    def __init__(self, engine: Optional[Engine] = None, device: int = 0, devices: Optional[Sequence[int]] = None):
+    def __init__(self, engine: Optional[Engine] = None, device: int = 0, devices: Optional[Sequence[int]] = None,
+                 mean_plans: Optional[str] = None):
         if engine is None:
             engine = Engine(devices=devices) if devices is not None else Engine(device)
         self.engine = engine
+        self.mean_plans = mean_plan_policy(mean_plans)  # non-iterative hosted plans: "decline" | "probe"
         self._numel: tuple = ()
         self._cap = 0
         self._dtype = None
@@ -246,7 +291,8 @@ class CycleAggregator:
             raise AggregationError(f"unknown checkpoint framing {framing!r}")
         if len(diffs) == 0:
             raise AggregationError("no diffs to average")
-        mode = select_mode(server_config, avg_plan, weights, plan_key=plan_key)
+        mode = select_mode(server_config, avg_plan, weights, plan_key=plan_key, mean_plans=self.mean_plans,
+                           shapes=lambda: _shapes_or_none(checkpoint), n_clients=len(diffs))
         try:
             numel = state_codec.tensor_numels(checkpoint)  # :240
         except StateParseError:
@@ -280,8 +326,9 @@ class CycleAggregator:
                        weights=None) -> List[np.ndarray]:
         if len(diffs) == 0:
             raise AggregationError("no diffs to average")
-        mode = select_mode(server_config, avg_plan, weights)
         shapes = [np.shape(p) for p in model_params]
+        mode = select_mode(server_config, avg_plan, weights, mean_plans=self.mean_plans, shapes=shapes,
+                           n_clients=len(diffs))
         numel = [int(np.prod(s)) for s in shapes]
         self._prepare(numel, len(diffs))
         for i, d in enumerate(diffs):
@@ -355,7 +402,7 @@ def make_average_plan_diffs(aggregator: CycleAggregator, model_manager, process_
             if avg_plan_rec and avg_plan_rec.value:
                 plan_key = avg_plan_rec.value
                 # a plan already probed needs no deserializing: only its verdict is used
-                if cached_mode(server_config, plan_key) is None:
+                if cached_mode(server_config, plan_key, getattr(aggregator, "mean_plans", None)) is None:
                     avg_plan = plan_manager.deserialize_plan(avg_plan_rec.value)
                 else:
                     avg_plan = _probed_plan

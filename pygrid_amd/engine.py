@@ -299,6 +299,11 @@ class Engine:
                                                              a.ctypes.data_as(C.POINTER(C.c_int32)), a.size),
                     "fold_slots_finish_resident")
 
+    def fold_restart(self):
+        """Forget the slot folds of this cycle so far (``pgh_fold_slots_restart``); unfolded slots
+        keep their diffs, weights must be set again."""
+        self._check(self._lib.pgh_fold_slots_restart(self._h), "fold_slots_restart")
+
     def ckpt_download(self) -> np.ndarray:
         out = np.empty(self.p_shard, dtype=np.float32)
         self._check(self._lib.pgh_ckpt_download(self._h, _ptr(out)), "ckpt_download")

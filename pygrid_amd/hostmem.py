@@ -7,12 +7,12 @@ Every ResNet-18 diff a report decodes, and every new checkpoint a close returns,
 -- the previous checkpoint is dropped when ``_average_plan_diffs`` returns -- and measured 3-6 ms
 per close against 1.8-2.1 ms for the close itself (``tools/node_sim.py``, ``profiles/r02bk/``).
 
-``tune()`` raises glibc's mmap threshold to 256 MiB and its trim threshold to 2 GiB
-(``mallopt``), so such buffers come from the heap and their pages are reused: the close then
-measures 1.8-2.0 ms including the free, and the report's base64 decode's p99 drops from 7-34 to
-6-7 ms.  The cost is that up to 2 GiB of freed heap stays mapped in the process.  Called when
-``pygrid_amd`` is imported; ``PGH_MALLOC_TUNE=0`` leaves the allocator alone.  Returns whether it
-applied the settings.
+``tune()`` raises glibc's mmap threshold to 256 MiB and its trim threshold to 1 GiB
+(``mallopt``), so such buffers come from the heap and their pages are reused.  The cost is that up
+to 1 GiB of freed heap stays mapped in the process.  This changes the allocator of the WHOLE host
+process (the reference node's own torch loop included), so it is never applied on import: a host
+application opts in with ``pygrid_amd.tune_process()``.  ``PGH_MALLOC_TUNE=0`` makes ``tune`` a
+no-op.  Returns whether it applied the settings.
 """
 from __future__ import annotations
 
@@ -22,7 +22,7 @@ import os
 M_TRIM_THRESHOLD = -1  # glibc malloc.h
 M_MMAP_THRESHOLD = -3
 MMAP_THRESHOLD = 256 << 20
-TRIM_THRESHOLD = 2 << 30
+TRIM_THRESHOLD = 1 << 30  # mallopt takes an int: 2 GiB would wrap to -2^31 (trimming off for good)
 
 
 def tune() -> bool:

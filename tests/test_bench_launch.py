@@ -25,11 +25,25 @@ def _json_line(out: str) -> dict:
     return json.loads(lines[0])
 
 
+GROUP_DRY = {"dry_run": True, "n_gpus": 2, "backend": "gloo", "group": True}
+
+
 def test_plain_bench_forms_two_ranks():
+    """The per-rank world's line, with the one-process group over the same GPUs (what the node
+    deploys, VERDICT r2 next #3) run after the ranks exit, in a fresh child, under `group`."""
     r = _run(["--gpus", "2", "--dry-run"])
     assert r.returncode == 0, r.stderr
     rec = _json_line(r.stdout)
-    assert rec == {"dry_run": True, "n_gpus": 2, "backend": "gloo", "group": False}
+    assert rec == {"dry_run": True, "n_gpus": 2, "backend": "gloo", "group": GROUP_DRY}
+
+
+def test_group_line_can_be_skipped_and_is_skipped_for_per_rank_only_workloads():
+    r = _run(["--gpus", "2", "--dry-run", "--no-group-line"])
+    assert r.returncode == 0, r.stderr
+    assert "group" not in {k for k, v in _json_line(r.stdout).items() if isinstance(v, dict)}
+    r = _run(["--gpus", "2", "--dry-run", "--workload", "c4-stream"])
+    assert r.returncode == 0, r.stderr
+    assert _json_line(r.stdout)["group"] is False  # no group record: c4 runs per rank only
 
 
 def test_plain_bench_forms_three_ranks():
@@ -59,7 +73,9 @@ def test_torchrun_launch_forms_two_ranks():
                         "--gpus", "2", "--dry-run"], cwd=str(ROOT), env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0, r.stderr
-    assert _json_line(r.stdout)["n_gpus"] == 2
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 2 and rec["backend"] == "gloo"
+    assert rec["group"] == GROUP_DRY  # rank 0 ran the group child itself after the world closed
 
 
 def test_usable_cores_reports_a_positive_count():

@@ -798,7 +798,10 @@ def test_non_iterative_mean_plan_is_accelerated(engine):
     shapes = [(64, 50), (50,)]
     ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
     diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for _ in range(9)]
-    agg = CycleAggregator(engine)
+    with pytest.raises(PlanNotAcceleratedError):  # the default: a user plan runs in the node
+        CycleAggregator(engine).average_plan_diffs({}, build_state_fast(ckpt), [build_state_fast(d) for d in diffs],
+                                                   avg_plan=plan)
+    agg = CycleAggregator(engine, mean_plans="probe")  # the operator's opt-in
     new = agg.average_plan_diffs({"iterative_plan": False}, build_state_fast(ckpt),
                                  [build_state_fast(d) for d in diffs], avg_plan=plan)
     avg = plan([[th.from_numpy(t) for t in d] for d in diffs])  # the node's own :270-271 + :293-296

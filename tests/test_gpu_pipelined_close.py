@@ -119,3 +119,35 @@ def test_group_pipelined_close(monkeypatch, streams):
         new = CycleAggregator(grp).average_plan_diffs({}, build_state_fast(ckpt), [build_state_fast(x) for x in diffs])
     for g, w in zip(parse_state(new), O.fedavg_mean(ckpt, diffs)):
         assert np.array_equal(bits(g), bits(w))
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_one_d2h_piece_spanning_every_range(monkeypatch, mode):
+    """with D2H pieces larger than a fold range, one piece holds floats of ranges that
+    ran on BOTH streams; its DMA must wait on every one of them, not only on the range holding its
+    last float.  Many clients make each range long enough for an unordered copy to read a
+    half-written checkpoint."""
+    from pygrid_amd import Engine
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    monkeypatch.setenv("PGH_FINAL_RANGES", "4")
+    monkeypatch.setenv("PGH_FINAL_STREAMS", "2")
+    monkeypatch.setenv("PGH_D2H_PIECE_MB", "64")  # the whole 6.2 MB checkpoint is one piece
+    rng = np.random.default_rng(430 + mode)
+    shapes = [(1024, 1500), (1500,), (7, 1024), (7,)]
+    numel = [int(np.prod(s)) for s in shapes]
+    P, N = sum(numel), 256
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    want = coracle.fedavg(mode, d, c, None)
+    tmpl = build_state_fast([np.zeros(s, F) for s in shapes])
+    with Engine(0) as eng:
+        eng.set_layout(numel)
+        eng.reserve(N)
+        for k in range(N):
+            eng.ingest(k, d[k])
+        for rep in range(3):
+            eng.ckpt_upload(c)
+            eng.fedavg_resident(mode)
+            got = np.concatenate([t.reshape(-1) for t in parse_state(eng.ckpt_patch_state(tmpl))])
+            assert np.array_equal(bits(got), bits(want)), rep

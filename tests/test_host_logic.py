@@ -9,7 +9,7 @@ import pytest
 import torch as th
 
 from oracle import oracle as O
-from pygrid_amd import ITERATIVE_MEAN, MEAN, WEIGHTED_MEAN, PlanNotAcceleratedError, StateParseError
+from pygrid_amd import ITERATIVE_MEAN, MEAN, WEIGHTED_MEAN, AggregationError, PlanNotAcceleratedError, StateParseError
 from pygrid_amd import cycle, state
 from pygrid_amd.state_schema import build_state, classes, parse_state, varint_encode
 
@@ -149,10 +149,46 @@ class FakeAggregator:
 
 
 @pytest.fixture(autouse=True)
-def _fresh_plan_cache():
+def _fresh_plan_cache(monkeypatch):
+    """The tests below exercise the opt-in probe of non-iterative plans (PGH_MEAN_PLANS=probe);
+    test_non_iterative_plans_are_declined_by_default covers the default."""
+    monkeypatch.setenv("PGH_MEAN_PLANS", "probe")
     cycle._MODE_CACHE.clear()
     yield
     cycle._MODE_CACHE.clear()
+
+
+def test_non_iterative_plans_are_declined_by_default(monkeypatch):
+    """a probe cannot prove a user plan is the mean, so by default a non-iterative
+    hosted plan runs in the node (cycle_manager.py:270-271) -- even one that IS the mean."""
+    monkeypatch.delenv("PGH_MEAN_PLANS", raising=False)
+    with pytest.raises(PlanNotAcceleratedError, match="opt in"):
+        cycle.select_mode({}, mean_plan, plan_key=b"P0")
+    assert cycle.select_mode({}, mean_plan, plan_key=b"P0", mean_plans="probe") == MEAN  # a separate verdict
+    with pytest.raises(PlanNotAcceleratedError):
+        cycle.cached_mode({}, b"P0")  # the default policy's verdict is cached too
+    assert cycle.select_mode({"iterative_plan": True}, canonical_plan) == ITERATIVE_MEAN  # unaffected
+    with pytest.raises(AggregationError):
+        cycle.mean_plan_policy("always")
+
+
+def conv_special_plan(diffs):
+    """The mean, except that 4-D (conv) tensors are halved: passes 1-D probes only."""
+    out = mean_plan(diffs)
+    return [o / 2 if o.dim() == 4 else o for o in out]
+
+
+def count_special_plan(diffs):
+    """The mean, except above 50 clients (where it trims the first one)."""
+    return mean_plan(diffs[1:] if len(diffs) > 50 else diffs)
+
+
+def test_probe_uses_the_models_ranks_and_the_cycles_client_count():
+    assert cycle.is_mean_plan(conv_special_plan)  # what the 1-D probes alone would accept
+    assert not cycle.is_mean_plan(conv_special_plan, shapes=[(64, 3, 7, 7), (64,)], n_clients=4)
+    assert cycle.is_mean_plan(count_special_plan, shapes=[(64, 3, 7, 7), (64,)], n_clients=10)
+    assert not cycle.is_mean_plan(count_special_plan, shapes=[(64, 3, 7, 7), (64,)], n_clients=100)
+    assert cycle.is_mean_plan(mean_plan, shapes=[(64, 3, 7, 7), (64,), (10, 512)], n_clients=100)
 
 
 def test_plan_verdict_is_cached_by_plan_bytes():
