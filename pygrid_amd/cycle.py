@@ -317,6 +317,7 @@ class CycleAggregator:
         new = (state_codec.fresh_checkpoint(self.engine, checkpoint) if framing == "fresh"  # :303
                else self.engine.ckpt_patch_state(checkpoint))
         self.engine.ckpt_owner = self
+        self.engine.ckpt_bytes = new  # the bytes whose params are resident (IncrementalCycle reuses them)
         self._resident = new
         return new
 
@@ -396,29 +397,39 @@ def make_average_plan_diffs(aggregator: CycleAggregator, model_manager, process_
         _model = model_manager.get(fl_process_id=cycle.fl_process_id)
         _checkpoint = model_manager.load(model_id=_model.id)
         reports = self._worker_cycles.query(cycle_id=cycle.id, is_completed=True)
-        avg_plan_rec = process_manager.get_plan(fl_process_id=cycle.fl_process_id, is_avg_plan=True)
-        avg_plan = plan_key = None
         try:
-            if avg_plan_rec and avg_plan_rec.value:
-                plan_key = avg_plan_rec.value
-                # a plan already probed needs no deserializing: only its verdict is used
-                if cached_mode(server_config, plan_key, getattr(aggregator, "mean_plans", None)) is None:
-                    avg_plan = plan_manager.deserialize_plan(avg_plan_rec.value)
-                else:
-                    avg_plan = _probed_plan
+            avg_plan, plan_key = hosted_plan(server_config, cycle, process_manager, plan_manager,
+                                             getattr(aggregator, "mean_plans", None))
             new_ckpt = aggregator.average_plan_diffs(server_config, _checkpoint.value,
                                                      [r.diff for r in reports], avg_plan, plan_key=plan_key)
         except PlanNotAcceleratedError as e:
             logging.info("engine declined (%s): running the reference averaging", e)
             return original(self, server_config, cycle)
-        model_manager.save(_model.id, new_ckpt)
-        cycle.is_completed = True
-        self._cycles.update()
-        completed = self._cycles.count(fl_process_id=cycle.fl_process_id, is_completed=True)
-        max_cycles = server_config.get("num_cycles", 0)
-        if completed < max_cycles or max_cycles == 0:
-            self.create(cycle.fl_process_id, cycle.version, server_config.get("cycle_length"))
-        else:
-            logging.info("FL is done!")
+        finish_cycle(self, server_config, cycle, model_manager, _model.id, new_ckpt)
 
     return _average_plan_diffs
+
+
+def hosted_plan(server_config: dict, cycle, process_manager, plan_manager, mean_plans=None):
+    """(avg_plan, plan_key) as ``cycle_manager.py:252-258`` looks them up; a plan whose verdict is
+    cached needs no deserializing (only its verdict is used)."""
+    avg_plan_rec = process_manager.get_plan(fl_process_id=cycle.fl_process_id, is_avg_plan=True)
+    if not (avg_plan_rec and avg_plan_rec.value):
+        return None, None
+    plan_key = avg_plan_rec.value
+    if cached_mode(server_config, plan_key, mean_plans) is None:
+        return plan_manager.deserialize_plan(avg_plan_rec.value), plan_key
+    return _probed_plan, plan_key
+
+
+def finish_cycle(cm, server_config: dict, cycle, model_manager, model_id, new_ckpt: bytes):
+    """``cycle_manager.py:303-323``: save the new checkpoint, complete the cycle, open the next."""
+    model_manager.save(model_id, new_ckpt)
+    cycle.is_completed = True
+    cm._cycles.update()
+    completed = cm._cycles.count(fl_process_id=cycle.fl_process_id, is_completed=True)
+    max_cycles = server_config.get("num_cycles", 0)
+    if completed < max_cycles or max_cycles == 0:
+        cm.create(cycle.fl_process_id, cycle.version, server_config.get("cycle_length"))
+    else:
+        logging.info("FL is done!")

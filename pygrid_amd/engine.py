@@ -125,6 +125,9 @@ class Engine:
         # Who put the current resident checkpoint in HBM (CycleAggregator / IncrementalCycle): any
         # call that overwrites it resets this, so a holder re-uploads instead of trusting stale bytes.
         self.ckpt_owner = None
+        # The bytes object the resident checkpoint was produced as (valid while ckpt_owner is set):
+        # the next cycle, handed those very bytes, skips the upload.
+        self.ckpt_bytes = None
 
     # ---- plumbing ----------------------------------------------------------------------------
     def _check(self, rc: int, what: str):

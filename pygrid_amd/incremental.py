@@ -1,52 +1,71 @@
-"""Fold diffs into HBM as they are reported.
+"""Fold diffs into HBM as they are reported, with the reference's report
+semantics.
 
-The reference stores every reported diff in the DB (``submit_worker_diff``,
-``cycle_manager.py:151-178``) and reads them all back at cycle close (``_average_plan_diffs``,
-``:243-250``) in the order of the completed-WorkerCycle query
-(``self._worker_cycles.query(cycle_id=..., is_completed=True)``: row-id order, i.e. the order in
-which workers were assigned, ``cycle_manager.assign``), skipping the workers that never reported
-(the reference expects ~20 % of them not to: ``routes.py:314``).  The fp32 fold depends on that
-order, so ``IncrementalCycle`` separates WHERE a diff lives from WHEN it is folded:
+The reference stores every reported diff in its DB (``submit_worker_diff``,
+``cycle_manager.py:151-178``: find the worker's WorkerCycle row, set ``diff``, ``is_completed``)
+and reads them all back at cycle close (``_average_plan_diffs``, ``:243-250``) in the order of the
+completed-WorkerCycle query (``self._worker_cycles.query(cycle_id=..., is_completed=True)``: a
+plain ``filter_by().all()``, no ORDER BY -- row order, in practice the order in which workers were
+assigned), skipping the workers that never reported (the reference expects ~20 % of them not to:
+``routes.py:314``).  The fp32 fold depends on that order, so ``IncrementalCycle`` separates WHERE a
+diff lives from WHEN it is folded:
 
-* ``reported(wid, diff)`` copies the diff into HBM at once, into whichever slab slot is free
+* ``reported(w, diff)`` copies the diff into HBM at once, into whichever slab slot is free
   (``pgh_ingest_state``: PCIe + host copy happen while the report is handled, in any arrival
   order);
-* the fold follows assignment order: a diff's position is certain once every worker assigned
-  before it has reported, and the certain prefix is folded from its scattered slots
-  (``pgh_fold_slots``: the kernel reads the slots through a row table), freeing them;
-* ``close(checkpoint)`` drops the workers that never reported and folds the remaining reporters'
-  slots in id order into the resident checkpoint (``pgh_fold_slots_finish_resident``), then patches
-  the new State bytes from HBM -- bit-identical to folding everything at close time.
+* the fold speculates on the assignment order (``assigned(w, key)``, ``key`` = the WorkerCycle row
+  id): a diff's position is taken as certain once every worker assigned before it has reported,
+  and the certain prefix is folded from its scattered slots (``pgh_fold_slots``: the kernel reads
+  the slots through a row table), freeing them;
+* ``close(checkpoint, order=..., fetch=...)`` takes the AUTHORITATIVE order -- the keys of the
+  completed-WorkerCycle query, as the node's DB returns them -- checks that the early-folded
+  prefix is that order's prefix, and folds the rest of the order from HBM (slots), the host
+  (parked diffs) or the DB (``fetch(w)``: diffs this process never saw, e.g. reported before a
+  restart).  When the prefix does not match (the DB returned another order, a folded worker
+  re-reported, an assignment arrived behind the fold front) the fold restarts
+  (``pgh_fold_slots_restart``) and re-folds the whole order, the folded diffs fetched from the DB:
+  bit-identical to the reference in every case, early folding is only ever a speedup.
 
-So a missing early worker no longer parks later diffs on the host: they wait in HBM, and close
-costs the fold of the not-yet-folded rows (HBM-bound, ~6.8 TB/s) plus the patch.  Only when every
-slot is taken does a diff wait on the host (``slots`` is the HBM budget in diffs); one slot is
-always kept for the fold front, so the front can never be starved by later diffs.
+Report semantics (``cycle_manager.py:162-174``, ``fl_events.py:257-263``):
+
+* **re-report** before the worker's diff was folded: the new diff replaces the old one (same slot,
+  or the parked copy); after it was folded: the early fold is stale and ``close`` re-folds from the
+  DB (the reference averages the LATEST diff at the worker's original row position);
+* **late report** (after ``close``): accepted and ignored -- the reference stores it and its
+  ``complete_cycle`` returns early for a completed cycle (``:186-188``);
+* **a report from a worker this object was not told about** (assigned before a restart):
+  kept in a slot, folded at close at the position the DB order gives it;
+* **malformed diff**: ``reported`` raises ``StateParseError`` (the caller decides what the client
+  sees; the node wiring keeps the reference's response) and any older diff of that worker is
+  dropped -- the DB now holds the malformed bytes, so ``close`` fetches them and fails the way the
+  reference's close does (its ``unserialize_model_params`` raises).
 
 Thread safety: the node calls ``reported`` from request handlers and ``close`` from its executor
 thread (``tasks/cycle.py``), so every method holds the cycle's lock (the engine context itself is
-single-owner).  A report that arrives after ``close`` started raises ``AggregationError`` -- the
-reference likewise averages only the diffs its query saw (``cycle_manager.py:243-245``).  A
-malformed diff is rejected in its own ``reported`` call (``StateParseError``, nothing recorded),
-so one bad client cannot break the cycle for the others.  A well-formed diff holding non-float32
-tensors is accepted (the reference would average it with torch's type promotion): the cycle is
-then declined as a whole -- later reports are only recorded, and ``close`` raises
-``ModelNotAcceleratedError`` so the node averages the cycle with its own code, from its DB.
+single-owner).  A well-formed diff holding non-float32 tensors is accepted (the reference would
+average it with torch's type promotion): the cycle is then declined as a whole -- later reports
+are only recorded, and ``close`` raises ``ModelNotAcceleratedError`` so the node averages the cycle
+with its own code, from its DB.
 
 The checkpoint can be handed over when the cycle starts (``checkpoint=``): its payloads are then
 uploaded into HBM while clients report, and ``close`` touches only the rows not folded yet.
 """
 from __future__ import annotations
 
+import bisect
+import itertools
+import logging
 import threading
-from typing import Dict, List, Optional
+from typing import Callable, Dict, Hashable, List, Optional, Sequence
 
 from . import state as state_codec
-from .engine import F32, MEAN, Engine
+from .engine import F32, MEAN, WEIGHTED_MEAN, Engine
 from .exceptions import AggregationError, ModelNotAcceleratedError, StateParseError
 
 DEFAULT_HBM_BUDGET = 64 << 30  # bytes of diffs kept in HBM per cycle when `slots` is not given
 MAX_DEFAULT_SLOTS = 4096
+
+log = logging.getLogger(__name__)
 
 
 def default_slots(P: int, budget: int = DEFAULT_HBM_BUDGET) -> int:
@@ -55,7 +74,8 @@ def default_slots(P: int, budget: int = DEFAULT_HBM_BUDGET) -> int:
 
 class IncrementalCycle:
     def __init__(self, engine: Engine, numel, mode: int = MEAN, slots: Optional[int] = None, fold_batch: int = 8,
-                 weights_by_worker: Optional[Dict[object, float]] = None, checkpoint: Optional[bytes] = None):
+                 weights_by_worker: Optional[Dict[object, float]] = None, checkpoint: Optional[bytes] = None,
+                 early_fold: bool = True):
         self.engine = engine
         self.mode = mode
         self._numel = tuple(int(n) for n in numel)
@@ -63,18 +83,25 @@ class IncrementalCycle:
         if self.slots < 2:
             raise AggregationError("report-time aggregation needs at least 2 HBM slots")
         self.fold_batch = max(1, int(fold_batch))
-        self._order: List[object] = []      # assigned workers, assignment order
-        self._pos: Dict[object, int] = {}
-        self._reported = set()
-        self._slot_of: Dict[object, int] = {}  # reported, in HBM, not folded
-        self._parked: Dict[object, bytes] = {}  # reported, no free slot yet (host)
+        self.early_fold = bool(early_fold)
+        self._seq = itertools.count()
+        self._order: List[object] = []      # assigned workers, sorted by assignment key
+        self._keys: List[tuple] = []        # their keys (sorted, parallel to _order)
+        self._key_of: Dict[object, tuple] = {}
+        self._reported = set()              # workers whose latest report we accepted
+        self._slot_of: Dict[object, int] = {}  # latest diff in HBM, not folded
+        self._parked: Dict[object, bytes] = {}  # latest diff on the host (no free slot yet)
+        self._bad: Dict[object, str] = {}   # latest report unusable here (malformed / failed ingest)
         self._free: List[int] = list(range(self.slots - 1, -1, -1))
-        self._ready: List[object] = []      # position certain, in HBM, not folded yet (fold order)
-        self._front = 0                     # next assigned position not yet certain
-        self._n_folded = 0
+        self._ready: List[object] = []      # position taken as certain, in HBM, not folded yet
+        self._front = 0                     # index into _order of the next position not yet certain
+        self._folded: List[object] = []     # folded early, in fold order
+        self._folded_set = set()
+        self._stale: Optional[str] = None   # why the early fold no longer matches the reports
         self._weights_by_worker = weights_by_worker
         self._weights: List[float] = []     # fold order
         self.folded_early = 0
+        self.last_close: dict = {}
         self._lock = threading.Lock()
         self._closed = False
         self._declined: Optional[str] = None  # why the engine cannot average this cycle
@@ -86,7 +113,12 @@ class IncrementalCycle:
         else:
             engine.reset()
         self._ckpt: Optional[bytes] = None  # checkpoint bytes whose payloads are resident in HBM
-        if checkpoint is not None:
+        if checkpoint is not None and getattr(engine, "ckpt_owner", None) is not None \
+                and getattr(engine, "ckpt_bytes", None) is checkpoint:
+            # the previous close left exactly these bytes' params in HBM (the cycles are chained)
+            engine.ckpt_owner = self
+            self._ckpt = checkpoint
+        elif checkpoint is not None:
             engine.ckpt_owner = None
             try:
                 engine.ckpt_upload_state(checkpoint)
@@ -96,36 +128,46 @@ class IncrementalCycle:
             engine.ckpt_owner = self
             self._ckpt = checkpoint
 
-    def assigned(self, worker):
+    # ---- assignment (cycle_manager.assign, fl_controller.py:131-132) ---------------------------
+    def assigned(self, worker, key=None):
+        """``worker`` was assigned to the cycle.  ``key`` orders the assignments (the WorkerCycle row
+        id: the order the completed-WorkerCycle query returns rows in); default: call order."""
         with self._lock:
-            if worker in self._pos:
+            if worker in self._key_of or self._closed:
                 return
-            self._pos[worker] = len(self._order)
-            self._order.append(worker)
+            k = (0, key) if key is not None else (1, next(self._seq))
+            self._key_of[worker] = k
+            i = bisect.bisect_right(self._keys, k)
+            self._keys.insert(i, k)
+            self._order.insert(i, worker)
+            if i < self._front:
+                # behind the fold front: never folded early; if it reports, close's order check
+                # sees the early prefix is not the DB's prefix and re-folds
+                self._front += 1
+            elif i == self._front and worker in self._reported and self.early_fold:
+                self._advance()
 
+    # ---- report (fl_events.py:257-261 -> submit_worker_diff, cycle_manager.py:151-178) ---------
     def reported(self, worker, diff: bytes):
+        """The worker's (latest) diff.  Raises ``StateParseError`` for a malformed diff (see the
+        module docstring); never raises for a late or repeated report."""
         with self._lock:
             if self._closed:
-                raise AggregationError(f"worker {worker!r} reported after the cycle closed")
-            if worker not in self._pos:
-                raise AggregationError(f"worker {worker!r} reported without being assigned to the cycle")
-            if worker in self._reported:
-                raise AggregationError(f"worker {worker!r} reported twice")
+                log.info("worker %r reported after the cycle closed: ignored (fl_events.py:261-263)", worker)
+                return
             if self._declined:
                 self._reported.add(worker)  # the node averages this cycle itself
                 return
             if self._weights_by_worker is not None and worker not in self._weights_by_worker:
-                # refused to its sender now, not when a later report folds it (that would leave
-                # the fold half done and blame another worker)
+                # refused to its sender now, not when a later report folds it
                 raise AggregationError(f"worker {worker!r} reported but has no aggregation weight")
-            front = self._pos[worker] == self._front
+            if worker in self._folded_set:
+                # its earlier diff is in the fold state already: the DB now holds another one
+                self._stale = f"worker {worker!r} re-reported after its diff was folded"
+                self._reported.add(worker)
+                return
             try:
-                # a diff that cannot fold yet leaves one slot free for the fold front
-                if self._free and (front or len(self._free) > 1):
-                    self._to_hbm(worker, diff)  # raises StateParseError on a malformed diff: nothing recorded
-                else:
-                    self._check_layout(worker, diff)
-                    self._parked[worker] = diff
+                self._take(worker, diff)
             except StateParseError:
                 try:
                     _raise_if_not_float32(diff, f"worker {worker!r}'s diff")
@@ -134,9 +176,43 @@ class IncrementalCycle:
                     self._parked.clear()
                     self._reported.add(worker)
                     return
+                self._forget(worker, "malformed diff")
                 raise
             self._reported.add(worker)
-            self._advance(final=False)
+            self._bad.pop(worker, None)
+            if self.early_fold:
+                self._advance()
+
+    def _take(self, worker, diff: bytes):
+        """Store ``diff`` as the worker's latest: over its old slot, in a free slot, or parked."""
+        if worker in self._slot_of:  # re-report before the fold: same slot (parse first, then DMA)
+            self.engine.ingest_state(self._slot_of[worker], diff)
+            return
+        front = self._is_front(worker)
+        # a diff that cannot fold yet leaves one slot free for the fold front
+        if self._free and (front or len(self._free) > 1):
+            self._to_hbm(worker, diff)  # raises StateParseError on a malformed diff: nothing recorded
+            self._parked.pop(worker, None)
+        else:
+            self._check_layout(worker, diff)
+            self._parked[worker] = diff
+
+    def _forget(self, worker, why: str):
+        """The worker's latest report is unusable here: drop any older copy (HBM or host)."""
+        slot = self._slot_of.pop(worker, None)
+        if slot is not None:
+            self._free.append(slot)
+        if worker in self._ready:
+            # the positions from this worker on are no longer certain: the front goes back to it
+            j = self._ready.index(worker)
+            self._front -= len(self._ready) - j
+            self._ready = self._ready[:j]
+        self._parked.pop(worker, None)
+        self._reported.discard(worker)
+        self._bad[worker] = why
+
+    def _is_front(self, worker) -> bool:
+        return self._front < len(self._order) and self._order[self._front] == worker
 
     def _check_layout(self, worker, diff: bytes):
         got = tuple(state_codec.tensor_numels(diff))
@@ -152,59 +228,162 @@ class IncrementalCycle:
             raise
         self._slot_of[worker] = slot
 
-    def _fold_ready(self, final: bool):
-        ws = self._ready
-        self._ready = []
+    def _held(self, worker) -> bool:
+        return worker in self._slot_of or worker in self._parked
+
+    # ---- early folds ---------------------------------------------------------------------------
+    def _fold(self, ws: Sequence, final: bool):
         slots = [self._slot_of.pop(w) for w in ws]
-        if self._weights_by_worker is not None and ws:
+        if self.mode == WEIGHTED_MEAN and self._weights_by_worker is not None and (ws or final):
             self._weights.extend(float(self._weights_by_worker[w]) for w in ws)
-            self.engine.set_weights(self._weights)
+            if self._weights:
+                self.engine.set_weights(self._weights)
         if final:
             self.engine.fold_slots_finish_resident(self.mode, slots)
         else:
             self.engine.fold_slots(self.mode, slots)
-            self.folded_early += len(slots)
         self._free.extend(reversed(slots))
-        self._n_folded += len(slots)
+        return slots
 
-    def _advance(self, final: bool):
+    def _fold_ready(self):
+        ws, self._ready = self._ready, []
+        self._fold(ws, final=False)
+        self._folded.extend(ws)
+        self._folded_set.update(ws)
+        self.folded_early += len(ws)
+
+    def _advance(self):
         while self._front < len(self._order):
             w = self._order[self._front]
-            if w in self._reported:
+            if w in self._reported and self._held(w):
                 if w in self._parked:  # its turn: it needs a slot now
                     if not self._free:
-                        self._fold_ready(final=False)  # frees >= 1 slot (see the invariant above)
-                    self._to_hbm(w, self._parked.pop(w))
+                        if not self._ready:
+                            break  # (cannot happen: one slot is kept for the front)
+                        self._fold_ready()
+                    try:
+                        self._to_hbm(w, self._parked[w])
+                    except Exception as e:  # noqa: BLE001 -- not this caller's report
+                        log.warning("parked diff of worker %r failed to ingest: %s", w, e)
+                        self._forget(w, f"ingest failed: {e}")
+                        break
+                    del self._parked[w]
                 self._ready.append(w)
-            elif not final:
+            else:
                 break  # an earlier worker may still report: later positions are not certain yet
-            self._front += 1  # at close, a worker that never reported is dropped
-            if not final and len(self._ready) >= self.fold_batch:
-                self._fold_ready(final=False)
+            self._front += 1
+            if len(self._ready) >= self.fold_batch:
+                self._fold_ready()
 
-    def close(self, checkpoint: bytes, framing: str = "fresh") -> bytes:
+    # ---- close (cycle_manager.py:217 -> _average_plan_diffs :240-303) ---------------------------
+    def close(self, checkpoint: bytes, framing: str = "fresh", order: Optional[Sequence[Hashable]] = None,
+              fetch: Optional[Callable[[object], bytes]] = None) -> bytes:
         """New checkpoint bytes (``cycle_manager.py:293-303``), framed like ``serialize_model_params``
-        (``framing="fresh"``) or as the old checkpoint (``"template"``; see CycleAggregator)."""
+        (``framing="fresh"``) or as the old checkpoint (``"template"``; see CycleAggregator).
+
+        ``order``: the workers of the completed-WorkerCycle query in the order the DB returned them
+        (``:243-245``); ``fetch(w)``: that row's ``diff`` bytes (read only for diffs not held here).
+        Without ``order`` the assignment order of the reporters is taken as the query's."""
         with self._lock:
             if self._closed:
                 raise AggregationError("cycle already closed")
             self._closed = True
             if self._declined:
                 raise ModelNotAcceleratedError(self._declined)
-            self._advance(final=True)
-            if self._n_folded + len(self._ready) == 0:
+            if order is None:
+                if self._stale or self._bad:
+                    what = self._stale or ", ".join(f"{w!r}: {why}" for w, why in self._bad.items())
+                    raise AggregationError(f"cannot close without the DB's rows ({what}): pass order= and fetch=")
+                order = [w for w in self._order if w in self._reported and (self._held(w) or w in self._folded_set)]
+                floating = [w for w in self._reported if w not in self._key_of and self._held(w)]
+                if floating:
+                    log.warning("close without the DB order: %d reports of unassigned workers dropped", len(floating))
+            order = list(order)
+            if len(set(order)) != len(order):
+                raise AggregationError("the completed-WorkerCycle order lists a worker twice")
+            if not order:
                 raise AggregationError("no diffs to average")
+            k = len(self._folded)
+            refold = self._stale or (order[:k] != self._folded and
+                                     f"the DB order's first {k} workers are not the {k} folded early")
+            if self._weights_by_worker is not None:
+                missing = [w for w in order if w not in self._weights_by_worker]
+                if missing:
+                    raise AggregationError(f"workers {missing[:8]!r} have no aggregation weight")
+            rest = order if refold else order[k:]
+            if fetch is None:
+                unheld = [w for w in rest if not self._held(w)]
+                if unheld:
+                    raise AggregationError(f"workers {unheld[:8]!r} in the close order have no diff here and there "
+                                           "is no fetch= to read them from the DB")
             if checkpoint is not self._ckpt or getattr(self.engine, "ckpt_owner", None) is not self:
                 self.engine.ckpt_owner = None
                 self.engine.ckpt_upload_state(checkpoint)  # scan + staged H2D of the payload spans
             # from the fold on, HBM holds the NEW checkpoint: nobody may take it for `checkpoint`
             self.engine.ckpt_owner = None
             self._ckpt = None
-            self._fold_ready(final=True)
+            if refold:  # the folded diffs are only in the fold state: discarded, re-read from the DB
+                log.info("re-folding the cycle in the DB's order: %s", refold)
+                self.engine.fold_restart()
+                self._weights = []
+            stats = self._fold_in_order(rest, fetch)
+            stats.update(refold=bool(refold), reason=refold or None, early=0 if refold else k, n=len(order))
+            self.last_close = stats
             new = (state_codec.fresh_checkpoint(self.engine, checkpoint) if framing == "fresh"
                    else self.engine.ckpt_patch_state(checkpoint))
             self.engine.ckpt_owner = self
+            self.engine.ckpt_bytes = new
             return new
+
+    def _fold_in_order(self, rest: List, fetch) -> dict:
+        """Fold ``rest`` in order and finish into the resident checkpoint, within the slot budget:
+        held slots are folded where they stand, other diffs are ingested into free slots; when none
+        is free, the pending batch is folded, or -- when the batch is empty and every slot holds a
+        later worker's diff -- the slot of the worker needed LAST is given up (its diff is fetched
+        from the DB when its turn comes)."""
+        pos = {w: i for i, w in enumerate(rest)}
+        for w in [w for w in self._slot_of if w not in pos]:  # held, but not in the DB's order
+            self._free.append(self._slot_of.pop(w))
+        self._ready = []
+        batch: List = []
+        from_hbm = from_host = from_db = 0
+        for i, w in enumerate(rest):
+            if w in self._slot_of:
+                batch.append(w)
+                from_hbm += 1
+                continue
+            diff = self._parked.get(w)
+            if diff is None:
+                if fetch is None:
+                    raise AggregationError(f"worker {w!r}: no diff held here and no fetch= to read it from the DB")
+                diff = fetch(w)
+                from_db += 1
+            else:
+                from_host += 1
+            if not self._free:
+                if batch:
+                    self._fold(batch, final=False)
+                    batch = []
+                else:
+                    later = max((x for x in self._slot_of if pos[x] > i), key=pos.__getitem__)
+                    if fetch is None:
+                        raise AggregationError(f"slot budget exhausted and no fetch= to re-read {later!r}")
+                    self._free.append(self._slot_of.pop(later))
+            self._to_hbm(w, diff)
+            self._parked.pop(w, None)
+            batch.append(w)
+        self._fold(batch, final=True)
+        return {"from_hbm": from_hbm, "from_host": from_host, "from_db": from_db}
+
+    def abandon(self):
+        """Another user takes the engine (its slab is re-laid): nothing held here survives.  Later
+        reports are ignored and ``close`` raises; the node closes this cycle from its DB rows."""
+        with self._lock:
+            self._closed = True
+            self._slot_of.clear()
+            self._parked.clear()
+            if getattr(self.engine, "ckpt_owner", None) is self:
+                self.engine.ckpt_owner = None
 
     @property
     def declined(self) -> Optional[str]:
@@ -213,8 +392,13 @@ class IncrementalCycle:
         return self._declined
 
     @property
+    def stale(self) -> Optional[str]:
+        """Why ``close`` will re-fold from the DB (a folded worker re-reported), or None."""
+        return self._stale
+
+    @property
     def n_folded(self) -> int:
-        return self._n_folded
+        return self.last_close.get("n", len(self._folded))
 
     @property
     def n_parked(self) -> int:

@@ -1,0 +1,377 @@
+"""One opt-in patch that wires the engine into a PyGrid Node.
+
+``install(cycle_manager_module, executor=...)`` replaces, on the node's own objects, the call
+sites of the cycle-close path; every endpoint keeps the response the reference gives:
+
+==========================================  ==================================================
+reference call site                         what it does after ``install``
+==========================================  ==================================================
+``CycleManager.assign``                     the DB row as before; the engine learns the row id
+(``cycle_manager.py:120-125``, called from  (``IncrementalCycle.assigned``: the fold order the
+``fl_controller.py:131-132``)               close-time query will return)
+``CycleManager.submit_worker_diff``         the DB write as before; then the diff goes into an
+(``cycle_manager.py:151-178``, from         HBM slot at once (``IncrementalCycle.reported``),
+``fl_events.py:257-261``)                   THEN the close is requested (never before its ingest)
+``run_task_once`` in ``cycle_manager.py``   unchanged by default; ``close_trigger="replay"``:
+(``tasks/cycle.py:9-25``)                   ``CycleCloseTrigger`` on the node's Flask-Executor
+                                            (replays a request that lands mid-close;
+                                            ``deadline=True`` also closes at ``cycle.end``)
+``CycleManager._average_plan_diffs``        the report-time fold finished in the DB's query
+(``cycle_manager.py:219-323``)              order (``IncrementalCycle.close(order=, fetch=)``),
+                                            or the close-time fold over the DB rows
+                                            (``CycleAggregator``), or -- for a plan or model
+                                            the engine does not implement -- the original
+``CycleManager.create`` (``:28-54``)        as before; the next cycle's report-time state is
+                                            prepared at once (its checkpoint is already in HBM)
+``ModelManager.save`` / ``load``            write-through, bounded ``CheckpointStore`` in front
+(``model_manager.py:30-60``; ``load``       of the DB: ``/get-model`` and ``/retrieve-model``
+serves ``/get-model`` ``routes.py:183``     (``routes.py:163-201, 471-516``) and the next
+and ``/retrieve-model`` ``:498``)           cycle read the newest checkpoints from memory
+==========================================  ==================================================
+
+One engine context is single-owner, so one open cycle at a time folds at report time (the first
+one prepared; the next cycle of the same FL process takes over when it closes).  Any other
+cycle closes through the close-time path over its DB rows -- bit-identical either way.  After a
+node restart the open cycle's state is rebuilt from its WorkerCycle rows: the diffs reported
+before the restart are read from the DB at close.
+
+Nothing runs at import: ``install`` is the opt-in, ``uninstall`` restores every patched name.
+"""
+from __future__ import annotations
+
+import contextlib
+import logging
+import threading
+from typing import Callable, Dict, Optional, Sequence
+
+from . import state as state_codec
+from .checkpoints import Checkpoint, CheckpointStore
+from .cycle import CycleAggregator, finish_cycle, hosted_plan, make_average_plan_diffs, select_mode
+from .exceptions import AggregationError, ModelNotAcceleratedError, PlanNotAcceleratedError, PyGridError, \
+    StateParseError
+from .incremental import IncrementalCycle
+from .trigger import CycleCloseTrigger
+
+log = logging.getLogger(__name__)
+
+_DECLINED = "declined"   # the engine does not average this cycle (plan / model): the node's code runs
+_ELSEWHERE = "elsewhere"  # report-time state not kept for this cycle: close-time path over the DB rows
+
+
+def completed_rows(cm, cycle_id):
+    """The completed WorkerCycles of the cycle in the order ``cycle_manager.py:243-245`` reads them
+    (the same ``filter_by(cycle_id=..., is_completed=True)`` query).  With SQLAlchemy the ``diff``
+    column is deferred: the blobs are read only for the diffs the engine does not already hold."""
+    return _rows(cm, cycle_id=cycle_id, is_completed=True)
+
+
+def _rows(cm, **filters):
+    wh = cm._worker_cycles
+    schema = getattr(wh, "_schema", None)
+    q = getattr(schema, "query", None)
+    if q is not None and hasattr(schema, "diff"):
+        try:
+            from sqlalchemy.orm import defer
+
+            return q.options(defer(schema.diff)).filter_by(**filters).all()
+        except ImportError:
+            pass
+    return wh.query(**filters)
+
+
+class NodeEngine:
+    """What ``install`` wires in (see the module docstring).  Attributes: ``aggregator``
+    (close-time path), ``engine``, ``store`` (checkpoint cache), ``trigger`` (or None), ``stats``."""
+
+    def __init__(self, cm_module, executor=None, engine=None, devices: Optional[Sequence[int]] = None,
+                 report_time: bool = True, close_trigger: str = "reference", deadline: bool = False,
+                 keep_checkpoints: int = 4, slots: Optional[int] = None, fold_batch: int = 8,
+                 mean_plans: Optional[str] = None, framing: str = "fresh"):
+        if close_trigger not in ("reference", "replay"):
+            raise AggregationError(f"close_trigger must be 'reference' or 'replay', not {close_trigger!r}")
+        if deadline and close_trigger != "replay":
+            raise AggregationError("deadline=True needs close_trigger='replay'")
+        self.mod = cm_module
+        self.model_manager = cm_module.model_manager
+        self.process_manager = cm_module.process_manager
+        self.plan_manager = cm_module.PlanManager
+        self.aggregator = CycleAggregator(engine, devices=devices, mean_plans=mean_plans) if engine is not None \
+            or devices is not None else CycleAggregator(mean_plans=mean_plans)
+        self.engine = self.aggregator.engine
+        self.report_time = report_time
+        self.close_trigger = close_trigger
+        self.deadline = deadline
+        self.slots = slots
+        self.fold_batch = fold_batch
+        self.framing = framing
+        self.store = CheckpointStore(keep=keep_checkpoints) if keep_checkpoints else None
+        self.trigger = CycleCloseTrigger(lambda fn, *a: fn(*a), executor=executor) if close_trigger == "replay" \
+            else None
+        self._cycles: Dict[object, object] = {}  # cycle id -> IncrementalCycle | _DECLINED | _ELSEWHERE
+        self._owner = None  # the cycle id whose IncrementalCycle holds the engine
+        self._lock = threading.RLock()
+        self._hold = threading.local()
+        self._patched: list = []
+        self.stats = {"closes_report_time": 0, "closes_close_time": 0, "closes_declined": 0, "refolds": 0,
+                      "diffs_from_db": 0, "report_errors": 0}
+
+    # ---- patching ------------------------------------------------------------------------------
+    def _patch(self, owner, name, value):
+        """Set ``owner.name`` (a class, a module or an instance), remembering what its own namespace
+        held (nothing, for an inherited or class-level attribute: uninstall then deletes ours)."""
+        self._patched.append((owner, name, vars(owner).get(name, _MISSING)))
+        setattr(owner, name, value)
+
+    def install(self):
+        CM = self.mod.CycleManager
+        node = self
+        orig = {n: getattr(CM, n) for n in ("assign", "submit_worker_diff", "_average_plan_diffs", "create")}
+        orig_run = self.mod.run_task_once
+        close_time = make_average_plan_diffs(self.aggregator, self.model_manager, self.process_manager,
+                                             self.plan_manager, original=orig["_average_plan_diffs"])
+
+        def assign(cm, worker, cycle, hash_key):
+            wc = orig["assign"](cm, worker, cycle, hash_key)
+            node.on_assign(cm, cycle, wc)
+            return wc
+
+        def submit_worker_diff(cm, worker_id, request_key, diff):
+            with node._holding_triggers() as held:
+                orig["submit_worker_diff"](cm, worker_id, request_key, diff)  # the DB write, :162-174
+                node.on_report(cm, worker_id, request_key, diff)
+            for name, func, args in held:  # :176-178, after the diff is in HBM
+                node.run_task_once(name, func, *args)
+
+        def _average_plan_diffs(cm, server_config, cycle):
+            return node.average_plan_diffs(cm, server_config, cycle, close_time, orig["_average_plan_diffs"])
+
+        def create(cm, fl_process_id, version, cycle_time):
+            cyc = orig["create"](cm, fl_process_id, version, cycle_time)
+            node.on_cycle_created(cm, cyc)
+            return cyc
+
+        def run_task_once(name, func, *args):
+            if getattr(node._hold, "queue", None) is not None:
+                node._hold.queue.append((name, func, args))
+                return None
+            return node.run_task_once(name, func, *args)
+
+        self._orig_run = orig_run
+        self._patch(CM, "_average_plan_diffs", _average_plan_diffs)
+        self._patch(CM, "submit_worker_diff", submit_worker_diff)
+        self._patch(self.mod, "run_task_once", run_task_once)
+        if self.report_time:
+            self._patch(CM, "assign", assign)
+            self._patch(CM, "create", create)
+        if self.store is not None:
+            mm = self.model_manager
+            orig_save, orig_load = mm.save, mm.load
+
+            def save(model_id, data):
+                cp = orig_save(model_id, data)
+                node.store.put(_as_checkpoint(cp, model_id, data))
+                return cp
+
+            def load(**kwargs):
+                hit = node.store.lookup(**kwargs)
+                if hit is not None:
+                    return hit
+                cp = orig_load(**kwargs)
+                if set(kwargs) <= {"model_id", "alias"} and kwargs.get("alias", "latest") == "latest":
+                    node.store.seed(_as_checkpoint(cp, kwargs["model_id"], cp.value))  # newest of the model
+                return cp
+
+            self._patch(mm, "save", save)
+            self._patch(mm, "load", load)
+        return self
+
+    def uninstall(self):
+        for owner, name, old in reversed(self._patched):
+            if old is _MISSING:
+                delattr(owner, name)
+            else:
+                setattr(owner, name, old)
+        self._patched.clear()
+        if self.trigger is not None:
+            self.trigger.shutdown()
+
+    # ---- run_task_once ---------------------------------------------------------------------------
+    @contextlib.contextmanager
+    def _holding_triggers(self):
+        """run_task_once calls made inside are queued, and dispatched by the caller afterwards."""
+        prev = getattr(self._hold, "queue", None)
+        self._hold.queue = []
+        try:
+            yield self._hold.queue
+        finally:
+            self._hold.queue = prev
+
+    def run_task_once(self, name, func, *args):
+        if self.trigger is not None and name == "complete_cycle":
+            return self.trigger.request(func, *args)
+        return self._orig_run(name, func, *args)
+
+    # ---- report-time state -------------------------------------------------------------------
+    def _cycle_state(self, cm, cycle, create: bool = True):
+        """The cycle's IncrementalCycle (made on first use, from its DB rows after a restart), or a
+        marker saying why there is none."""
+        with self._lock:
+            got = self._cycles.get(cycle.id)
+            if got is not None or not create:
+                return got
+            if not self.report_time or getattr(cycle, "is_completed", False):
+                return None
+            if self._owner is not None and self._owner != cycle.id and \
+                    isinstance(self._cycles.get(self._owner), IncrementalCycle):
+                self._cycles[cycle.id] = _ELSEWHERE  # the engine serves another open cycle
+                return _ELSEWHERE
+            try:
+                inc = self._new_cycle(cm, cycle)
+            except PlanNotAcceleratedError as e:
+                log.info("cycle %s: %s -- the node averages it", cycle.id, e)
+                self._cycles[cycle.id] = _DECLINED
+                return _DECLINED
+            self._cycles[cycle.id] = inc
+            self._owner = cycle.id
+            return inc
+
+    def _new_cycle(self, cm, cycle) -> IncrementalCycle:
+        server_config, _ = self.process_manager.get_configs(id=cycle.fl_process_id)
+        avg_plan, plan_key = hosted_plan(server_config, cycle, self.process_manager, self.plan_manager,
+                                         self.aggregator.mean_plans)
+        model = self.model_manager.get(fl_process_id=cycle.fl_process_id)
+        ckpt = self.model_manager.load(model_id=model.id).value
+        try:
+            numel = state_codec.tensor_numels(ckpt)
+        except StateParseError:
+            from .cycle import _decline_non_float32
+
+            _decline_non_float32(ckpt, "the checkpoint")
+            raise
+        mode = select_mode(server_config, avg_plan, plan_key=plan_key, mean_plans=self.aggregator.mean_plans,
+                           shapes=lambda: _shapes(ckpt))
+        self.aggregator._resident = None  # the report-time cycle takes over the engine's slab
+        inc = IncrementalCycle(self.engine, numel, mode=mode, slots=self.slots, fold_batch=self.fold_batch,
+                               checkpoint=ckpt)
+        for row in _rows(cm, cycle_id=cycle.id):  # after a restart: the rows assigned before it
+            inc.assigned(row.id, key=row.id)
+        return inc
+
+    def on_cycle_created(self, cm, cycle):
+        if self.trigger is not None and self.deadline:
+            self.trigger.schedule_deadline(cycle.id, getattr(cycle, "end", None),
+                                           args=(self._task_fn(), cm, cycle.id))
+        try:
+            self._cycle_state(cm, cycle)
+        except Exception as e:  # noqa: BLE001 -- preparing early is an optimisation only
+            log.warning("cycle %s: report-time state not prepared (%s); close-time path", cycle.id, e)
+            with self._lock:
+                self._cycles[cycle.id] = _ELSEWHERE
+
+    def _task_fn(self):
+        """The task ``submit_worker_diff`` hands to ``run_task_once`` (``tasks/cycle.py:28-37``,
+        imported into ``cycle_manager.py:18``)."""
+        return self.mod.complete_cycle
+
+    def on_assign(self, cm, cycle, wc):
+        st = self._cycle_state(cm, cycle)
+        if isinstance(st, IncrementalCycle):
+            st.assigned(wc.id, key=wc.id)
+
+    def on_report(self, cm, worker_id, request_key, diff):
+        """After the reference's DB write.  Never raises: the response stays the reference's, and a
+        diff the engine could not take is read from the DB at close."""
+        try:
+            wc = cm._worker_cycles.first(worker_id=worker_id, request_key=request_key)
+            st = self._cycles.get(wc.cycle_id)
+            if st is None and self.report_time:
+                cycle = cm._cycles.first(id=wc.cycle_id)
+                st = self._cycle_state(cm, cycle) if cycle is not None else None
+            if isinstance(st, IncrementalCycle):
+                st.reported(wc.id, diff)
+        except (PyGridError, StateParseError) as e:
+            self.stats["report_errors"] += 1
+            log.warning("report of worker %s kept for the close-time read (%s)", worker_id, e)
+        except Exception as e:  # noqa: BLE001 -- never change the report's response
+            self.stats["report_errors"] += 1
+            log.error("report of worker %s: engine error %s; the close reads it from the DB", worker_id, e)
+
+    # ---- close ---------------------------------------------------------------------------------
+    def average_plan_diffs(self, cm, server_config, cycle, close_time: Callable, original: Callable):
+        with self._lock:
+            st = self._cycles.pop(cycle.id, None)
+            if self._owner == cycle.id:
+                self._owner = None
+            if st == _DECLINED:
+                self.stats["closes_declined"] += 1
+                return original(cm, server_config, cycle)
+            if not isinstance(st, IncrementalCycle):
+                self._abandon_others()  # the close-time path re-lays the engine's slab
+                self.stats["closes_close_time"] += 1
+                return close_time(cm, server_config, cycle)
+            model = self.model_manager.get(fl_process_id=cycle.fl_process_id)
+            ckpt = self.model_manager.load(model_id=model.id)
+            rows = completed_rows(cm, cycle.id)
+            by_id = {r.id: r for r in rows}
+            try:
+                new = st.close(ckpt.value, framing=self.framing, order=[r.id for r in rows],
+                               fetch=lambda rid: by_id[rid].diff)
+            except PlanNotAcceleratedError as e:  # incl. ModelNotAcceleratedError: a non-float32 diff
+                log.info("engine declined cycle %s (%s): running the reference averaging", cycle.id, e)
+                self.stats["closes_declined"] += 1
+                return original(cm, server_config, cycle)
+            except AggregationError as e:
+                log.warning("report-time close of cycle %s failed (%s): close-time path over the DB rows",
+                            cycle.id, e)
+                self.aggregator._resident = None
+                self.stats["closes_close_time"] += 1
+                return close_time(cm, server_config, cycle)
+            self.stats["closes_report_time"] += 1
+            self.stats["refolds"] += int(st.last_close.get("refold", False))
+            self.stats["diffs_from_db"] += st.last_close.get("from_db", 0)
+            self.aggregator._resident = None
+            finish_cycle(cm, server_config, cycle, self.model_manager, model.id, new)
+
+    def _abandon_others(self):
+        for cid, st in list(self._cycles.items()):
+            if isinstance(st, IncrementalCycle):
+                st.abandon()
+                self._cycles[cid] = _ELSEWHERE
+        self._owner = None
+
+
+class _Missing:
+    pass
+
+
+_MISSING = _Missing()
+
+
+def _as_checkpoint(cp, model_id, value) -> Checkpoint:
+    return Checkpoint(id=getattr(cp, "id", 0), model_id=getattr(cp, "model_id", model_id),
+                      number=getattr(cp, "number", 0), alias=getattr(cp, "alias", "latest"), value=value)
+
+
+def _shapes(pb: bytes):
+    from .state_schema import tensor_shapes
+
+    return tensor_shapes(pb)
+
+
+def install(cycle_manager_module, executor=None, **options) -> NodeEngine:
+    """Wire the engine into the node whose ``cycle_manager`` module is given (it holds
+    ``CycleManager``, ``run_task_once``, and the ``model_manager`` / ``process_manager`` /
+    ``PlanManager`` singletons it uses).  ``executor``: the node's Flask-Executor (for
+    ``close_trigger="replay"``).  Options: see ``NodeEngine``.  Returns the NodeEngine
+    (``.uninstall()`` undoes it)."""
+    return NodeEngine(cycle_manager_module, executor=executor, **options).install()
+
+
+def install_into_node(package: str = "src.app", **options) -> NodeEngine:
+    """``install`` for the node app as shipped (``apps/node``: ``python -m src`` imports it as
+    ``src.app``)."""
+    from importlib import import_module
+
+    cm_module = import_module(f"{package}.main.model_centric.cycles.cycle_manager")
+    app = import_module(package)
+    return install(cm_module, executor=getattr(app, "executor", None), **options)

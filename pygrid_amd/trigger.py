@@ -14,7 +14,11 @@ Reference behaviour (``apps/node/src/app/main/model_centric/tasks/cycle.py:9-25`
 ``CycleCloseTrigger`` keeps the single-flight guarantee (one close at a time, as the reference
 wants: the GPU context is single-owner) and fixes both: a request that arrives during a run
 marks the run dirty and is replayed as soon as it finishes, and ``schedule_deadline`` arms a
-timer that runs the same readiness check at ``cycle.end``.
+timer that runs the same readiness check at ``cycle.end``.  Both change WHEN a cycle closes
+compared with the reference, so the node wiring uses it only on request
+(``pygrid_amd.node.install(close_trigger="replay")``; the default keeps ``run_task_once``).  The
+drain runs on the node's Flask-Executor when one is given (``executor.submit``: the node's thread
+pool and app context, ``app/__init__.py:29, 197-199``), else on a thread of its own.
 """
 from __future__ import annotations
 
@@ -26,30 +30,45 @@ from typing import Callable, Dict, Optional
 
 
 class CycleCloseTrigger:
-    def __init__(self, complete_cycle: Callable[[int], object], name: str = "complete_cycle"):
-        """``complete_cycle(cycle_id)`` is the node's readiness check + close
-        (``CycleManager.complete_cycle``, ``cycle_manager.py:180-217``)."""
+    def __init__(self, complete_cycle: Callable[..., object], name: str = "complete_cycle", executor=None):
+        """``complete_cycle(*args)`` is the node's readiness check + close
+        (``CycleManager.complete_cycle``, ``cycle_manager.py:180-217``; in the node wiring the task
+        function ``tasks.cycle.complete_cycle(cycle_manager, cycle_id)``).  ``executor``: an object
+        with ``submit(fn)`` (flask_executor.Executor, concurrent.futures.Executor)."""
         self._fn = complete_cycle
         self._name = name
+        self._executor = executor
         self._lock = threading.Lock()
         self._running = False
-        self._pending: Dict[int, None] = {}  # cycle ids requested while a run was in flight (ordered)
-        self._timers: Dict[int, threading.Timer] = {}
+        self._pending: Dict[tuple, None] = {}  # argument tuples requested while a run was in flight (ordered)
+        self._timers: Dict[tuple, threading.Timer] = {}
         self._idle = threading.Event()
         self._idle.set()
         self.runs = 0
         self.errors = 0
+        self.replayed = 0
 
     # -- the run_task_once replacement ----------------------------------------------------------
-    def request(self, cycle_id: int):
+    def request(self, *args):
         """Called where the reference calls ``run_task_once`` (``cycle_manager.py:178``)."""
         with self._lock:
-            self._pending[cycle_id] = None
+            self._pending[args] = None
             if self._running:
-                return  # replayed by the running worker when it finishes (the reference drops it)
+                self.replayed += 1
+                return  # replayed by the running drain when it finishes (the reference drops it)
             self._running = True
             self._idle.clear()
-        threading.Thread(target=self._drain, name=f"{self._name}-worker", daemon=True).start()
+        try:
+            if self._executor is not None:
+                self._executor.submit(self._drain)
+            else:
+                threading.Thread(target=self._drain, name=f"{self._name}-drain", daemon=True).start()
+        except Exception:  # the reference logs a failed submit (tasks/cycle.py:18-22)
+            logging.error("Failed to start %s: %s", self._name, traceback.format_exc())
+            with self._lock:
+                self._pending.pop(args, None)
+                self._running = False
+                self._idle.set()
 
     def _drain(self):
         while True:
@@ -58,35 +77,36 @@ class CycleCloseTrigger:
                     self._running = False
                     self._idle.set()
                     return
-                cycle_id = next(iter(self._pending))
-                del self._pending[cycle_id]
+                args = next(iter(self._pending))
+                del self._pending[args]
             try:
-                self._fn(cycle_id)
+                self._fn(*args)
             except Exception as e:  # the reference's task wrapper logs and swallows (tasks/cycle.py:33-37)
                 self.errors += 1
                 logging.error("Error in %s task: %s %s", self._name, e, traceback.format_exc())
             self.runs += 1
 
     # -- deadline ------------------------------------------------------------------------------
-    def schedule_deadline(self, cycle_id: int, end: Optional[datetime], now: Optional[datetime] = None):
+    def schedule_deadline(self, key, end: Optional[datetime], now: Optional[datetime] = None, args=None):
         """Arm a timer that requests the readiness check at ``end`` (``cycle.end``, set from
-        ``cycle_length`` when the cycle is created, ``cycle_manager.py:28-54``)."""
+        ``cycle_length`` when the cycle is created, ``cycle_manager.py:28-54``).  ``args``: the
+        request's arguments (default ``(key,)``)."""
         if end is None:
             return
         now = now or datetime.now()
         delay = max(0.0, (end - now).total_seconds())
-        t = threading.Timer(delay, self.request, args=(cycle_id,))
+        t = threading.Timer(delay, self.request, args=tuple(args) if args is not None else (key,))
         t.daemon = True
         with self._lock:
-            old = self._timers.pop(cycle_id, None)
-            self._timers[cycle_id] = t
+            old = self._timers.pop(key, None)
+            self._timers[key] = t
         if old:
             old.cancel()
         t.start()
 
-    def cancel_deadline(self, cycle_id: int):
+    def cancel_deadline(self, key):
         with self._lock:
-            t = self._timers.pop(cycle_id, None)
+            t = self._timers.pop(key, None)
         if t:
             t.cancel()
 

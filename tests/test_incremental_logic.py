@@ -36,8 +36,8 @@ class RecordingEngine:
     def ingest_state(self, k, pb):
         if self.fail_on is not None and pb == self.fail_on:
             raise StateParseError("malformed diff")
-        assert 0 <= k < self.max_slots and k not in self.slot, (k, self.slot)
-        self.slot[k] = pb
+        assert 0 <= k < self.max_slots, (k, self.slot)
+        self.slot[k] = pb  # an occupied slot is overwritten (a re-report, pgh_ingest_state RESIDENT)
         self.calls.append(("ingest", k, pb))
 
     def fold_slots(self, mode, slots):
@@ -48,6 +48,10 @@ class RecordingEngine:
         self.folds.append((True, [self.slot.pop(s) for s in slots]))
         self.calls.append(("finish",))
 
+    def fold_restart(self):
+        self.folds.append(("restart", []))
+        self.calls.append(("restart",))
+
     def ckpt_upload_state(self, pb):
         self.calls.append(("upload", pb))
 
@@ -57,7 +61,11 @@ class RecordingEngine:
 
 
 def folded(eng):
-    return [p for _, ps in eng.folds for p in ps]
+    """Payloads in the fold state, in fold order (a restart discards what came before it)."""
+    out = []
+    for kind, ps in eng.folds:
+        out = [] if kind == "restart" else out + ps
+    return out
 
 
 def mk(w: int) -> bytes:
@@ -182,18 +190,166 @@ def test_weightless_report_is_refused_to_its_sender():
 
 
 def test_errors():
-    eng = RecordingEngine()
-    inc = IncrementalCycle(eng, [3], slots=4)
-    with pytest.raises(AggregationError):
-        inc.reported("ghost", b"")
-    inc.assigned("a")
-    inc.reported("a", b"a")
-    with pytest.raises(AggregationError):
-        inc.reported("a", b"a")
     inc2 = IncrementalCycle(RecordingEngine(), [3], slots=4)
     inc2.assigned("b")
     with pytest.raises(AggregationError):
-        inc2.close(b"", framing="template")
+        inc2.close(b"", framing="template")  # nobody reported
+    inc3 = IncrementalCycle(RecordingEngine(), [3], slots=4)
+    inc3.assigned("c")
+    inc3.reported("c", b"c")
+    with pytest.raises(AggregationError):
+        inc3.close(b"ck", framing="template", order=["c", "c"])  # a row twice
+    inc4 = IncrementalCycle(RecordingEngine(), [3], slots=4)
+    with pytest.raises(AggregationError):
+        inc4.close(b"ck", framing="template", order=["x"])  # no diff here, no fetch=
+
+
+def test_re_report_before_its_fold_replaces_the_diff():
+    """cycle_manager.py:162-174: a second report overwrites the row's diff; the close folds the
+    LATEST diff at the worker's row position."""
+    eng = RecordingEngine()
+    inc = IncrementalCycle(eng, [3], slots=4, fold_batch=1)
+    for w in "abc":
+        inc.assigned(w)
+    inc.reported("b", b"b1")
+    inc.reported("b", b"b2")  # same slot, new bytes
+    inc.reported("a", b"a1")  # a, b folded now
+    assert folded(eng) == [b"a1", b"b2"]
+    inc.reported("c", b"c1")
+    inc.close(b"ck", framing="template")
+    assert folded(eng) == [b"a1", b"b2", b"c1"] and inc.last_close["refold"] is False
+
+
+def test_re_report_of_a_parked_diff_replaces_it():
+    good = {k: build_state_fast([np.full(3, k, np.float32)]) for k in range(6)}
+    eng = RecordingEngine()
+    inc = IncrementalCycle(eng, [3], slots=2, fold_batch=4)
+    for w in range(4):
+        inc.assigned(w)
+    inc.reported(2, good[2])
+    inc.reported(3, good[3])
+    assert inc.n_parked == 1
+    inc.reported(3, good[5])  # replaces the parked copy
+    for w in (0, 1):
+        inc.reported(w, good[w])
+    inc.close(b"ck", framing="template")
+    assert folded(eng) == [good[0], good[1], good[2], good[5]]
+
+
+def test_re_report_after_its_fold_refolds_from_the_db():
+    eng = RecordingEngine()
+    inc = IncrementalCycle(eng, [3], slots=4, fold_batch=1)
+    for w in "abc":
+        inc.assigned(w)
+    inc.reported("a", b"a1")
+    assert folded(eng) == [b"a1"]
+    inc.reported("a", b"a2")  # the fold holds a1, the DB a2
+    assert inc.stale
+    inc.reported("c", b"c1")
+    db = {"a": b"a2", "b": b"b1", "c": b"c1"}
+    with pytest.raises(AggregationError):
+        inc.close(b"ck", framing="template")  # no DB order: cannot re-fold
+    inc = _replay_stale(db)
+    assert folded(inc.engine) == [b"a2", b"c1"] and inc.last_close["refold"]
+
+
+def _replay_stale(db):
+    eng = RecordingEngine()
+    inc = IncrementalCycle(eng, [3], slots=4, fold_batch=1)
+    for w in "abc":
+        inc.assigned(w)
+    inc.reported("a", b"a1")
+    inc.reported("a", b"a2")
+    inc.reported("c", b"c1")
+    inc.close(b"ck", framing="template", order=["a", "c"], fetch=db.__getitem__)
+    return inc
+
+
+def test_close_follows_the_db_order_and_reads_what_it_lacks():
+    """The DB's order is the truth: an early fold that is not its prefix is redone; workers this
+    object never heard of (reported before a restart) are read with fetch."""
+    db = {w: w.encode() for w in "abcdef"}
+    eng = RecordingEngine()
+    inc = IncrementalCycle(eng, [3], slots=3, fold_batch=1)
+    for w in "abcd":
+        inc.assigned(w)
+    for w in "abd":
+        inc.reported(w, db[w])
+    assert folded(eng) == [b"a", b"b"]
+    fetched = []
+
+    def fetch(w):
+        fetched.append(w)
+        return db[w]
+    inc.close(b"ck", framing="template", order=list("badf"), fetch=fetch)
+    assert folded(eng) == [b"b", b"a", b"d", b"f"] and inc.last_close["refold"]
+    assert sorted(fetched) == ["a", "b", "f"]  # d was still in HBM
+
+
+def test_close_evicts_when_every_slot_holds_a_later_diff():
+    """Every slot held by a diff the DB order needs LATER and nothing to fold yet: the slot of the
+    diff needed last is given up and that diff is re-read from the DB when its turn comes."""
+    db = {w: mk(i) for i, w in enumerate("uxa")}
+    eng = RecordingEngine()
+    inc = IncrementalCycle(eng, [3], slots=2, fold_batch=4)
+    inc.assigned("a")
+    inc.reported("x", db["x"])  # unassigned (a restart lost it): held, never folded early
+    inc.reported("a", db["a"])  # the fold front takes the last slot, waits for a batch of 4
+    fetched = []
+
+    def fetch(w):
+        fetched.append(w)
+        return db[w]
+    inc.close(b"ck", framing="template", order=list("uxa"), fetch=fetch)
+    assert folded(eng) == [db["u"], db["x"], db["a"]]
+    assert fetched == ["u", "a"]
+
+
+def test_late_and_unknown_reports_do_not_raise():
+    eng = RecordingEngine()
+    inc = IncrementalCycle(eng, [3], slots=4)
+    inc.assigned("a")
+    inc.reported("a", b"a")
+    inc.reported("ghost", b"g")  # assigned before a restart: held, placed by the DB order at close
+    inc.close(b"ck", framing="template")  # no order: only the assigned reporters
+    assert folded(eng) == [b"a"]
+    inc.reported("a", b"late")  # fl_events.py:261-263 answers success; nothing changes
+    assert folded(eng) == [b"a"]
+
+
+def test_parked_ingest_failure_is_not_blamed_on_another_reporter():
+    """a parked diff is ingested when the front reaches it, during ANOTHER worker's
+    report; if that fails, that worker gets no error, the parked worker's diff is dropped, and the
+    close reads it from the DB."""
+    good = {k: build_state_fast([np.full(3, k, np.float32)]) for k in range(4)}
+
+    class FlakyEngine(RecordingEngine):
+        fail_once = good[3]
+
+        def ingest_state(self, k, pb):
+            if pb is self.fail_once:
+                self.fail_once = None
+                raise RuntimeError("HIP copy failed")
+            super().ingest_state(k, pb)
+
+    eng = FlakyEngine()
+    inc = IncrementalCycle(eng, [3], slots=2, fold_batch=4)
+    for w in range(4):
+        inc.assigned(w)
+    inc.reported(2, good[2])
+    inc.reported(3, good[3])  # parked
+    inc.reported(0, good[0])
+    inc.reported(1, good[1])  # the front passes 2 and reaches 3: its ingest fails -- not 1's error
+    with pytest.raises(AggregationError):
+        inc.close(b"ck", framing="template")  # no DB order: cannot invent worker 3's diff
+    inc = IncrementalCycle(FlakyEngine(), [3], slots=2, fold_batch=4)
+    inc.engine.fail_once = good[3]
+    for w in range(4):
+        inc.assigned(w)
+    for w in (2, 3, 0, 1):
+        inc.reported(w, good[w])
+    inc.close(b"ck", framing="template", order=[0, 1, 2, 3], fetch=good.__getitem__)
+    assert folded(inc.engine) == [good[k] for k in range(4)]
 
 
 def test_malformed_diff_is_refused_to_its_sender_only():
@@ -210,6 +366,33 @@ def test_malformed_diff_is_refused_to_its_sender_only():
     inc.reported(3, b"3")
     inc.close(b"ck", framing="template")
     assert folded(eng) == [b"0", b"1", b"3"]
+
+
+def test_malformed_re_report_drops_the_older_diff():
+    """The DB now holds the malformed bytes (cycle_manager.py:173): the older diff must not be
+    averaged in their place -- close reads the row from the DB (and fails the way the reference's
+    unserialize does)."""
+    eng = RecordingEngine(fail_on=b"bad")
+    inc = IncrementalCycle(eng, [3], slots=8, fold_batch=4)
+    for w in range(3):
+        inc.assigned(w)
+    inc.reported(1, b"1")
+    inc.reported(2, b"2")
+    with pytest.raises(StateParseError):
+        inc.reported(1, b"bad")
+    inc.reported(0, b"0")
+    assert folded(eng) == []  # the front stops at worker 1
+    with pytest.raises(AggregationError):
+        inc.close(b"ck", framing="template")
+    eng = RecordingEngine(fail_on=b"bad")
+    inc = IncrementalCycle(eng, [3], slots=8, fold_batch=4)
+    for w in range(3):
+        inc.assigned(w)
+    inc.reported(1, b"1")
+    with pytest.raises(StateParseError):
+        inc.reported(1, b"bad")
+    with pytest.raises(StateParseError):  # the DB's bytes for row 1, read at close
+        inc.close(b"ck", framing="template", order=[1], fetch=lambda w: b"bad")
 
 
 def test_malformed_diff_is_refused_when_it_would_park():
@@ -234,7 +417,7 @@ def test_malformed_diff_is_refused_when_it_would_park():
 
 def test_reports_from_many_threads_and_a_late_one():
     """Request threads report concurrently (the node's handlers); folds still follow assignment
-    order exactly once each, and a report after close is refused."""
+    order exactly once each, and a report after close is ignored."""
     import threading
 
     eng = RecordingEngine()
@@ -251,8 +434,7 @@ def test_reports_from_many_threads_and_a_late_one():
         t.join()
     inc.close(b"ck", framing="template")
     assert folded(eng) == [mk(k) for k in range(64)]
-    with pytest.raises(AggregationError):
-        inc.reported(0, b"late")
+    inc.reported(0, b"late")  # accepted and ignored (fl_events.py:261-263)
     with pytest.raises(AggregationError):
         inc.close(b"ck", framing="template")
 

@@ -109,3 +109,16 @@ def test_cancel_deadline():
     trig.cancel_deadline(5)
     time.sleep(0.4)
     assert fired == []
+
+
+def test_runs_on_the_given_executor_with_several_arguments():
+    """In the node the drain runs on Flask-Executor (app context, its thread pool), and the request
+    carries run_task_once's arguments (cycle_manager, cycle_id)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    seen = []
+    with ThreadPoolExecutor(2, thread_name_prefix="flask-executor") as ex:
+        trig = CycleCloseTrigger(lambda cm, cid: seen.append((cm, cid, threading.current_thread().name)), executor=ex)
+        trig.request("cm", 4)
+        assert trig.wait_idle(5)
+    assert seen[0][:2] == ("cm", 4) and seen[0][2].startswith("flask-executor")
