@@ -198,7 +198,7 @@ def wants_group_line(args) -> bool:
     return args.gpus > 1 and not args.group and not args.no_group_line and args.workload in GROUP_WORKLOADS
 
 
-def group_line(args, limit_s: int = 900) -> dict:
+def group_line(args, limit_s: int = 420) -> dict:
     """The path the node deploys at N > 1 (its single process drives every GPU through one library
     context, ``pgh_create_group``), measured on the same GPUs right after
     the per-rank world has exited: ``bench.py --group --gpus N`` in a FRESH child (no process that
@@ -220,15 +220,15 @@ def group_line(args, limit_s: int = 900) -> dict:
                         "PGH_BENCH_SPAWNED", "TORCHELASTIC_RUN_ID", "GROUP_RANK", "ROLE_RANK")}
     print(f"bench.py: one-process group over {args.gpus} GPUs in a fresh child ({limit_s} s limit)", file=sys.stderr,
           flush=True)
-    try:
-        r = subprocess.run(["timeout", "-k", "10", str(limit_s)] + cmd, cwd=str(ROOT), env=env, capture_output=True,
-                           text=True)
+    try:  # stderr passes through: the child's progress stays visible
+        r = subprocess.run(["timeout", "-k", "10", str(limit_s)] + cmd, cwd=str(ROOT), env=env,
+                           stdout=subprocess.PIPE, text=True)
     except OSError as e:
         return {"error": f"group child did not start: {e}"}
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
-        tail = (r.stderr.strip().splitlines() or [""])[-1][:400]
-        return {"error": f"group child exited {r.returncode}: {tail}"}
+        return {"error": f"group child exited {r.returncode} (limit {limit_s} s; its stderr is above)",
+                "command": " ".join(cmd[1:])}
     g = json.loads(lines[-1])
     if g.get("dry_run"):
         return g

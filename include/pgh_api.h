@@ -68,6 +68,9 @@ typedef struct {
     int32_t max_clients;       /* slab capacity (slots) */
     double kernel_busy_ms_total;/* union of the timed launches' [start, end] intervals: launches
                                  * running concurrently on several streams count once */
+    uint64_t h2d_staged_bytes_total; /* of h2d_bytes_total: bytes host threads first copied into
+                                 * the pinned staging ring (pageable sources); page-locked sources
+                                 * (pgh_host_alloc) are DMA'd as they lie and do not count */
 } pgh_stats_t;
 
 /* ---- context lifecycle ------------------------------------------------------------------ */

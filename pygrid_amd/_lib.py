@@ -34,12 +34,25 @@ class Stats(C.Structure):
         ("n_clients", C.c_int32),
         ("max_clients", C.c_int32),
         ("kernel_busy_ms_total", C.c_double),
+        ("h2d_staged_bytes_total", C.c_uint64),
     ]
 
 
 _new_bytes = C.pythonapi.PyBytes_FromStringAndSize
 _new_bytes.restype = C.py_object
 _new_bytes.argtypes = [C.c_void_p, C.c_ssize_t]
+
+
+def buf_arg(pb):
+    """(keep-alive, argument) for a ``void*`` State parameter: a ``bytes`` object is passed as is;
+    any other buffer (memoryview, bytearray, numpy) by the address of its first byte -- the
+    keep-alive holds the exporting view for the duration of the call."""
+    if isinstance(pb, bytes):
+        return pb, pb
+    import numpy as np
+
+    a = np.frombuffer(pb, dtype=np.uint8)
+    return a, (a.ctypes.data if a.size else None)
 
 
 def fresh_bytes(n: int):
@@ -73,7 +86,9 @@ SIGNATURES = {
     "pgh_reserve": (_i, [_vp, _i, _i, _i]),
     "pgh_reset": (_i, [_vp]),
     "pgh_ingest_raw": (_i, [_vp, _i, _vp, _sz, _i]),
-    "pgh_ingest_state": (_i, [_vp, _i, C.c_char_p, _sz]),
+    # State bytes: a bytes object, or the address of any buffer (buf_arg: memoryviews of page-locked
+    # report buffers, pygrid_amd.report.PinnedPool)
+    "pgh_ingest_state": (_i, [_vp, _i, _vp, _sz]),
     "pgh_set_synth_kind": (_i, [_vp, _i]),
     "pgh_ingest_state_shares": (_i, [_vp, _i, _i, C.POINTER(C.c_char_p), C.POINTER(_sz)]),
     "pgh_synth_fill": (_i, [_vp, _u64, _i]),
@@ -83,7 +98,7 @@ SIGNATURES = {
     "pgh_fedavg_device": (_i, [_vp, _i, _vp, _vp, _vp]),
     "pgh_fedavg_device_range": (_i, [_vp, _i, _i64, _i64, _vp, _vp, _vp]),
     "pgh_ckpt_upload": (_i, [_vp, _vp, _sz]),
-    "pgh_ckpt_upload_state": (_i, [_vp, C.c_char_p, _sz]),
+    "pgh_ckpt_upload_state": (_i, [_vp, _vp, _sz]),
     "pgh_fedavg_resident": (_i, [_vp, _i]),
     "pgh_fold_slots": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
     "pgh_fold_slots_finish_resident": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
@@ -108,7 +123,7 @@ SIGNATURES = {
     "pgh_stats": (_i, [_vp, C.POINTER(Stats)]),
     "pgh_reset_stats": (_i, [_vp]),
     "pgh_slab": (_i, [_vp, C.POINTER(_vp), _P64, _P64]),
-    "pgh_state_scan": (_i, [C.c_char_p, _sz, _i, _P64, _P64, C.POINTER(C.c_int)]),
+    "pgh_state_scan": (_i, [_vp, _sz, _i, _P64, _P64, C.POINTER(C.c_int)]),
     "pgh_state_scan_i64": (_i, [C.c_char_p, _sz, _i, _P64, _P64, _P64, C.POINTER(C.c_int)]),
     "pgh_state_patch": (_i, [C.c_char_p, _sz, _vp, _i64, _vp]),
     "pgh_state_fresh": (_i, [C.c_char_p, _sz, _P64, _i, _vp, _sz, C.POINTER(_sz)]),

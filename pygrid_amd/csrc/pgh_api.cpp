@@ -612,6 +612,7 @@ int stage_pieces_h2d(pgh_ctx* c, const Dest& dst, const std::vector<Piece>& piec
     }
     c->st.h2d_ms_total += now_ms() - t0;
     c->st.h2d_bytes_total += total;
+    c->st.h2d_staged_bytes_total += total;
     return PGH_OK;
 }
 
@@ -1103,7 +1104,7 @@ const char* pgh_last_error(const pgh_ctx* ctx) { return ctx ? ctx->err.c_str() :
 int pgh_host_alloc(size_t bytes, void** out) {
     if (!out || !bytes) return fail(nullptr, PGH_E_ARG, "bad pinned allocation request");
     *out = nullptr;
-    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(out, bytes, hipHostMallocPortable) != hipSuccess) {  // DMA-able by every GPU of a group
         (void)hipGetLastError();
         *out = nullptr;
         return fail(nullptr, PGH_E_OOM, "pinned host allocation of %zu bytes failed", bytes);
@@ -1380,6 +1381,22 @@ int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
     DeviceGuard g(c->device);
     int slot = 0;
     RC(claim_slot(c, client, &slot));
+    if (n && is_pinned(pb)) {
+        // Page-locked message (a report decoded straight into pgh_host_alloc memory,
+        // pygrid_amd.report.PinnedPool): the payload spans are DMA'd as they lie, no staging copy.
+        // The buffer is only borrowed for the call, so the call waits for its copies.
+        const double t0 = now_ms();
+        const Dest d = row_dest(c, slot, 0);
+        size_t off = 0;
+        for (auto& p : pieces) {
+            RC(h2d_range(c, d, (int64_t)(off / 4), p.src, (int64_t)(p.n / 4), c->copy));
+            off += p.n;
+        }
+        CK(c, hipStreamSynchronize(c->copy));
+        c->st.h2d_ms_total += now_ms() - t0;
+        c->st.h2d_bytes_total += off;
+        return mark_ingested(c, client, slot);
+    }
     if (c->register_ingest && n >= (8u << 20) &&
         hipHostRegister((void*)pb, n, hipHostRegisterDefault) == hipSuccess) {
         // page-lock the message for the duration of the call and DMA the spans directly
@@ -1527,6 +1544,7 @@ int stage_share_msg(pgh_ctx* c, ShareMsg& m) {
     }
     c->st.h2d_ms_total += now_ms() - t0;
     c->st.h2d_bytes_total += m.bytes;
+    c->st.h2d_staged_bytes_total += m.bytes;
     return PGH_OK;
 }
 

@@ -227,8 +227,12 @@ class Engine:
         self._check(self._lib.pgh_ingest_raw(self._h, int(client), _ptr(a), a.nbytes, self.dtype),
                     f"ingest client {client}")
 
-    def ingest_state(self, client: int, pb: bytes):
-        self._check(self._lib.pgh_ingest_state(self._h, int(client), pb, len(pb)), f"ingest_state client {client}")
+    def ingest_state(self, client: int, pb):
+        """``pb``: State bytes, or any buffer over them (a page-locked report buffer is DMA'd as it
+        lies: ``report.PinnedPool``)."""
+        keep, arg = _lib.buf_arg(pb)
+        self._check(self._lib.pgh_ingest_state(self._h, int(client), arg, len(keep)),
+                    f"ingest_state client {client}")
 
     def ingest_state_shares(self, client: int, messages: Sequence[bytes]):
         """One client's secure-aggregation shares, one State message per party (packed-varint
@@ -281,9 +285,10 @@ class Engine:
         self.ckpt_owner = None
         self._check(self._lib.pgh_ckpt_upload(self._h, _ptr(a), a.nbytes), "ckpt_upload")
 
-    def ckpt_upload_state(self, pb: bytes):
+    def ckpt_upload_state(self, pb):
         self.ckpt_owner = None
-        self._check(self._lib.pgh_ckpt_upload_state(self._h, pb, len(pb)), "ckpt_upload_state")
+        keep, arg = _lib.buf_arg(pb)
+        self._check(self._lib.pgh_ckpt_upload_state(self._h, arg, len(keep)), "ckpt_upload_state")
 
     def fedavg_resident(self, mode: int):
         """Fold into the resident checkpoint: afterwards it IS the new checkpoint."""

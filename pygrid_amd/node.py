@@ -27,6 +27,9 @@ reference call site                         what it does after ``install``
 (``model_manager.py:30-60``; ``load``       of the DB: ``/get-model`` and ``/retrieve-model``
 serves ``/get-model`` ``routes.py:183``     (``routes.py:163-201, 471-516``) and the next
 and ``/retrieve-model`` ``:498``)           cycle read the newest checkpoints from memory
+``base64.b64decode`` in ``fl_events.py``    ``report.b64decode`` into a page-locked block
+(``:257``, when ``report_module`` given)    (``PinnedPool``): the diff the DB stores and the
+                                            engine DMAs to HBM without a staging copy
 ==========================================  ==================================================
 
 One engine context is single-owner, so one open cycle at a time folds at report time (the first
@@ -86,7 +89,8 @@ class NodeEngine:
     def __init__(self, cm_module, executor=None, engine=None, devices: Optional[Sequence[int]] = None,
                  report_time: bool = True, close_trigger: str = "reference", deadline: bool = False,
                  keep_checkpoints: int = 4, slots: Optional[int] = None, fold_batch: int = 8,
-                 mean_plans: Optional[str] = None, framing: str = "fresh"):
+                 mean_plans: Optional[str] = None, framing: str = "fresh", report_module=None,
+                 pinned_reports: int = 16):
         if close_trigger not in ("reference", "replay"):
             raise AggregationError(f"close_trigger must be 'reference' or 'replay', not {close_trigger!r}")
         if deadline and close_trigger != "replay":
@@ -105,6 +109,12 @@ class NodeEngine:
         self.fold_batch = fold_batch
         self.framing = framing
         self.store = CheckpointStore(keep=keep_checkpoints) if keep_checkpoints else None
+        self.report_module = report_module
+        self.pinned = None
+        if report_module is not None:
+            from .report import PinnedPool
+
+            self.pinned = PinnedPool(max_blocks=pinned_reports) if pinned_reports else None
         self.trigger = CycleCloseTrigger(lambda fn, *a: fn(*a), executor=executor) if close_trigger == "replay" \
             else None
         self._cycles: Dict[object, object] = {}  # cycle id -> IncrementalCycle | _DECLINED | _ELSEWHERE
@@ -183,6 +193,8 @@ class NodeEngine:
 
             self._patch(mm, "save", save)
             self._patch(mm, "load", load)
+        if self.report_module is not None:
+            self._patch(self.report_module, "base64", _Base64(self.pinned))
         return self
 
     def uninstall(self):
@@ -194,6 +206,8 @@ class NodeEngine:
         self._patched.clear()
         if self.trigger is not None:
             self.trigger.shutdown()
+        if self.pinned is not None:
+            self.pinned.close()
 
     # ---- run_task_once ---------------------------------------------------------------------------
     @contextlib.contextmanager
@@ -340,6 +354,28 @@ class NodeEngine:
         self._owner = None
 
 
+class _Base64:
+    """Stands for the ``base64`` module inside ``fl_events``: ``b64decode(text)`` (``:257``) decodes
+    natively, into a page-locked block when the pool has one; everything else is ``base64``'s."""
+
+    def __init__(self, pool):
+        self._pool = pool
+
+    def b64decode(self, s, *args, **kwargs):
+        if args or kwargs:  # altchars / validate: not what the report handler uses
+            import base64
+
+            return base64.b64decode(s, *args, **kwargs)
+        from .report import b64decode
+
+        return b64decode(s, into=self._pool)
+
+    def __getattr__(self, name):
+        import base64
+
+        return getattr(base64, name)
+
+
 class _Missing:
     pass
 
@@ -373,5 +409,7 @@ def install_into_node(package: str = "src.app", **options) -> NodeEngine:
     from importlib import import_module
 
     cm_module = import_module(f"{package}.main.model_centric.cycles.cycle_manager")
+    fl_events = import_module(f"{package}.main.events.model_centric.fl_events")
     app = import_module(package)
+    options.setdefault("report_module", fl_events)
     return install(cm_module, executor=getattr(app, "executor", None), **options)

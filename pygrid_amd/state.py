@@ -30,13 +30,14 @@ def scan(pb: bytes) -> List[Tuple[int, int]]:
     """(byte offset, float count) of every tensor payload, in State order."""
     lib = _lib.load()
     n = C.c_int(0)
-    rc = lib.pgh_state_scan(pb, len(pb), 0, None, None, C.byref(n))
+    keep, arg = _lib.buf_arg(pb)
+    rc = lib.pgh_state_scan(arg, len(keep), 0, None, None, C.byref(n))
     if rc != 0:
         raise StateParseError(f"malformed State message ({_lib.STATUS_NAMES.get(rc, rc)})", status=rc)
     k = n.value
     offs = (C.c_int64 * max(k, 1))()
     cnts = (C.c_int64 * max(k, 1))()
-    rc = lib.pgh_state_scan(pb, len(pb), k, offs, cnts, C.byref(n))
+    rc = lib.pgh_state_scan(arg, len(keep), k, offs, cnts, C.byref(n))
     if rc != 0:
         raise StateParseError("malformed State message", status=rc)
     return [(offs[i], cnts[i]) for i in range(k)]

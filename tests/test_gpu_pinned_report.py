@@ -1,0 +1,65 @@
+"""GPU: reports decoded straight into page-locked blocks (report.b64decode(into=PinnedPool)) are
+DMA'd to HBM as they lie -- no host staging copy (pgh_stats h2d_staged_bytes_total does not move)
+-- and the close is bit-exact against the oracle, on one GPU and on a group (VERDICT r2 next #5;
+the report handler is fl_events.py:257-261)."""
+import base64
+import gc
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+SHAPES = [(512, 300), (300,), (4096,)]
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_pinned_reports_skip_the_staging_copy(devices):
+    from pygrid_amd import Engine
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.report import PinnedPool, b64decode
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(700)
+    ckpt = [rng.standard_normal(s).astype(F) for s in SHAPES]
+    diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES] for _ in range(10)]
+    texts = [base64.b64encode(build_state_fast(d)).decode() for d in diffs]
+    pool = PinnedPool(max_blocks=3)
+    eng = Engine(devices=devices) if devices else Engine(0)
+    try:
+        numel = [int(np.prod(s)) for s in SHAPES]
+        ck = build_state_fast(ckpt)
+        inc = IncrementalCycle(eng, numel, slots=12, fold_batch=3, checkpoint=ck)
+        for w in range(10):
+            inc.assigned(w, key=w)
+        eng.reset_stats()
+        staged = []
+        for w in (4, 0, 2, 1, 3, 9, 8, 7, 6, 5):
+            d = b64decode(texts[w], into=pool)
+            assert bytes(d) == base64.b64decode(texts[w])
+            before = eng.stats()["h2d_staged_bytes_total"]
+            inc.reported(w, d)
+            staged.append((isinstance(d, memoryview), eng.stats()["h2d_staged_bytes_total"] - before))
+            del d
+            gc.collect()
+        assert all(mv for mv, _ in staged) and pool.hits == 10 and pool.blocks <= 3
+        assert all(n == 0 for _, n in staged)  # every payload DMA'd from the pinned block
+        assert eng.stats()["h2d_bytes_total"] >= 10 * 4 * sum(numel)
+        new = inc.close(ck, order=list(range(10)), framing="template")
+        for g, w in zip(parse_state(new), O.fedavg_mean(ckpt, diffs)):
+            assert np.array_equal(bits(g), bits(w))
+        # the same diffs as pageable bytes DO go through the staging ring
+        inc = IncrementalCycle(eng, numel, slots=12, fold_batch=3, checkpoint=new)
+        inc.assigned(0)
+        before = eng.stats()["h2d_staged_bytes_total"]
+        inc.reported(0, base64.b64decode(texts[0]))
+        assert eng.stats()["h2d_staged_bytes_total"] - before >= 4 * sum(numel)
+    finally:
+        eng.close()
+        pool.close()

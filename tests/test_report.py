@@ -171,3 +171,87 @@ def test_str_text_is_decoded_in_place():
         base64.b64decode("QUJDé")
     with pytest.raises(ValueError):
         b64decode("QUJDé")
+
+
+class _FakePinnedLib:
+    """pgh_host_alloc / pgh_host_free over ordinary ctypes buffers (no GPU here); every other
+    entry point is the real library's."""
+
+    def __init__(self, real):
+        import ctypes as C
+
+        self._real, self._C = real, C
+        self.live = {}
+        self.allocs = self.frees = 0
+
+    def pgh_host_alloc(self, n, out):
+        buf = self._C.create_string_buffer(n)
+        addr = self._C.addressof(buf)
+        self.live[addr] = buf
+        out._obj.value = addr
+        self.allocs += 1
+        return 0
+
+    def pgh_host_free(self, p):
+        del self.live[p.value]
+        self.frees += 1
+        return 0
+
+    def __getattr__(self, name):
+        return getattr(self._real, name)
+
+
+def test_pinned_pool_decodes_into_blocks_and_recycles_them(monkeypatch):
+    """report.b64decode(into=pool): the diff lands in a pool block (a read-only memoryview); the
+    block returns when the last view is gone, is reused for the next report, a report with every
+    block taken falls back to bytes, and close() frees idle blocks and late returns."""
+    import base64
+    import gc
+
+    from pygrid_amd import _lib, report
+
+    fake = _FakePinnedLib(_lib.load())
+    monkeypatch.setattr(report._lib, "load", lambda: fake)
+    rng = np.random.default_rng(9)
+    raws = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (300_000, 200_001, 3_000_000)]
+    texts = [base64.b64encode(r).decode() for r in raws]
+    pool = report.PinnedPool(max_blocks=2)
+    a = report.b64decode(texts[0], into=pool)
+    assert isinstance(a, memoryview) and a.readonly and bytes(a) == raws[0]
+    b = report.b64decode(texts[1] + "\n", into=pool)  # the general route, into a second block
+    assert isinstance(b, memoryview) and bytes(b) == raws[1] and pool.blocks == 2
+    c = report.b64decode(texts[1], into=pool)  # every block in use: ordinary bytes
+    assert isinstance(c, bytes) and c == raws[1] and pool.misses == 1
+    held = np.frombuffer(a, np.uint8)  # another reference (the DB layer, a parked report ...)
+    del a
+    gc.collect()
+    d = report.b64decode(texts[1], into=pool)
+    assert isinstance(d, bytes)  # a's block is still referenced through `held`
+    del held, d
+    gc.collect()
+    e = report.b64decode(texts[1], into=pool)
+    assert isinstance(e, memoryview) and bytes(e) == raws[1] and fake.allocs == 2  # reused
+    f = report.b64decode(texts[2], into=pool)  # no block fits and none idle: bytes
+    assert isinstance(f, bytes)
+    del e
+    gc.collect()
+    g = report.b64decode(texts[2], into=pool)  # the idle block is too small: replaced
+    assert isinstance(g, memoryview) and bytes(g) == raws[2] and fake.frees == 1 and pool.blocks == 2
+    h = report.b64decode(texts[0], into=pool)  # both blocks in use (b, g): bytes
+    assert isinstance(h, bytes)
+    pool.close()
+    assert fake.frees == 1  # nothing idle to free yet
+    del b, g
+    gc.collect()
+    assert fake.frees == 3 and not fake.live  # the late returns are freed, not pooled
+
+
+def test_pinned_pool_without_a_gpu_falls_back_to_bytes():
+    import base64
+
+    from pygrid_amd import report
+
+    raw = bytes(range(256)) * 1000
+    pool = report.PinnedPool()
+    got = report.b64decode(base64.b64encode(raw), into=pool)
+    assert got == raw  # bytes on a box without HIP devices, a memoryview on the GPU box

@@ -6,10 +6,13 @@ an HBM slot), and the close when the cycle ends (cycle_manager.py:217).  ResNet-
 assigned per cycle, ~20 % never report (routes.py:314), shuffled arrival, several cycles chained
 through the resident checkpoint.
 
-    python tools/node_sim.py [cycles]
+    python tools/node_sim.py [cycles] [--pinned] [--tune] [--phases]
 
-Prints one JSON line: per-report handler latency (decode, ingest, total: p50 / p99 / max) and the
-close latency per cycle.
+Prints one JSON line: per-report handler latency (decode, ingest, total: p50 / p99 / max), the host
+bytes copied into the library's staging ring per report, and the close latency per cycle.
+``--pinned``: the report is decoded into a page-locked block (``report.PinnedPool``) and DMA'd as
+it lies.  ``--tune``: ``pygrid_amd.tune_process()`` first (glibc thresholds;
+the engine's own share of the close is the untuned run).
 """
 import base64
 import json
@@ -32,7 +35,18 @@ def pct(xs, q):
 
 
 def main():
-    cycles = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    cycles = int(args[0]) if args else 4
+    tuned = None
+    if "--tune" in sys.argv:
+        import pygrid_amd
+
+        tuned = pygrid_amd.tune_process(hw_queues=False)
+    pool = None
+    if "--pinned" in sys.argv:
+        from pygrid_amd.report import PinnedPool
+
+        pool = PinnedPool(max_blocks=8)
     rng = np.random.default_rng(2024)
     numel = [int(np.prod(s)) for s in RESNET18_SHAPES]
     ckpt = build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in RESNET18_SHAPES])
@@ -59,7 +73,7 @@ def main():
         for nm in ("fold_slots_finish_resident", "ckpt_patch_into", "fold_slots"):
             wrap(eng, nm)
         wrap(st, "fresh_frame_bytes")
-    dec, ing, tot, closes, close_phases = [], [], [], [], []
+    dec, ing, tot, closes, close_phases, staged = [], [], [], [], [], []
     for cyc in range(cycles + 1):  # cycle 0 warms up
         n = 100
         reporters = [w for w in range(n) if rng.random() >= 0.2]
@@ -67,15 +81,18 @@ def main():
         for w in range(n):
             inc.assigned(w)
         for w in rng.permutation(reporters):
+            s0 = eng.stats()["h2d_staged_bytes_total"]
             t0 = time.perf_counter()
-            diff = b64decode(texts[int(w) % 4])  # fl_events.py:257
+            diff = b64decode(texts[int(w) % 4], into=pool)  # fl_events.py:257
             t1 = time.perf_counter()
             inc.reported(int(w), diff)           # submit_worker_diff, cycle_manager.py:151-178
             t2 = time.perf_counter()
+            del diff                             # the handler returns (its pinned block goes back)
             if cyc:
                 dec.append((t1 - t0) * 1e3)
                 ing.append((t2 - t1) * 1e3)
                 tot.append((t2 - t0) * 1e3)
+                staged.append(eng.stats()["h2d_staged_bytes_total"] - s0)
         time.sleep(0.05)  # the cycle ends some time after the last report (cycle.end timer)
         phases.clear()
         t0 = time.perf_counter()
@@ -88,7 +105,12 @@ def main():
             close_phases.append(dict(phases, close_call=round((t1 - t0) * 1e3, 3), free_old=round((t2 - t1) * 1e3, 3),
                                      folded_before_close=inc.folded_early))
     eng.close()
+    if pool is not None:
+        pool.close()
     print(json.dumps({
+        "pinned_reports": pool is not None, "process_tuning": tuned,
+        "pinned_pool": {"hits": pool.hits, "misses": pool.misses} if pool is not None else None,
+        "host_staging_bytes_per_report": {"mean": round(float(np.mean(staged)), 1), "max": int(max(staged))},
         "workload": "ResNet-18 (62 tensors), 100 assigned per cycle, ~20 % never report, shuffled arrival, "
                     "base64 text -> report.b64decode -> IncrementalCycle.reported; close 50 ms after the last report",
         "cycles": cycles, "reports": len(tot),
