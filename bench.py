@@ -107,6 +107,15 @@ def parse():
     ap.add_argument("--no-live-traffic", action="store_true",
                     help="N = 1 resident lines: skip the two rocprofv3 --pmc passes that measure roofline.traffic "
                          "in this run (the committed profiles/pmc_traffic.json is quoted instead)")
+    ap.add_argument("--report-gap-ms", type=float, default=0.0,
+                    help="resnet18-report: pause between reports (0: back to back; a node decodes each report's "
+                         "base64 for ~4-7 ms anyway, tools/node_sim.py)")
+    ap.add_argument("--sync-before-close", action="store_true",
+                    help="resnet18-report: wait for the GPU before the close and time that wait apart")
+    ap.add_argument("--eager-speculate", action="store_true",
+                    help="resnet18-report: speculative folds at every report even while the GPU is busy")
+    ap.add_argument("--no-speculate", action="store_true",
+                    help="resnet18-report: fold only certain positions early (no speculative folds / rewinds)")
     ap.add_argument("--no-group-line", action="store_true",
                     help="N > 1 per-rank runs: skip the one-process group over the same GPUs measured after the "
                          "ranks exit (the JSON line's `group` record)")
@@ -1020,24 +1029,33 @@ def run_resnet18_report(ctx, args, eng, N):
     reporters = [w for w in range(N) if w != 0 and rng.random() >= 0.2]
     arrival = [int(w) for w in rng.permutation(reporters)]
     slots, batch = args.ring or N, 8
-    closes, early = [], []
+    closes, early, at_close, rewinds, pending = [], [], [], [], []
 
     def cycle():
-        inc = IncrementalCycle(eng, numel, slots=slots, fold_batch=batch, checkpoint=ck_pb)
+        inc = IncrementalCycle(eng, numel, slots=slots, fold_batch=batch, checkpoint=ck_pb,
+                               speculate=False if args.no_speculate else None, lazy=not args.eager_speculate)
         for w in range(N):
             inc.assigned(w)
         for w in arrival:
             inc.reported(w, distinct[w % 4])
+            if args.report_gap_ms:
+                time.sleep(args.report_gap_ms / 1e3)
         early.append(inc.n_folded)
         t0 = time.perf_counter()
+        if args.sync_before_close:  # the GPU work the reports left queued, timed apart from the close call
+            eng.sync()
+            pending.append((time.perf_counter() - t0) * 1e3)
+            t0 = time.perf_counter()
         new = inc.close(ck_pb)
         closes.append((time.perf_counter() - t0) * 1e3)
+        at_close.append(inc.last_close["n"] - inc.last_close["early"])
+        rewinds.append(inc.rewinds)
         return new
 
     for _ in range(args.warmup):
         cycle()
-    closes.clear()
-    early.clear()
+    for x in (closes, early, at_close, rewinds, pending):
+        x.clear()
     eng.reset_stats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -1056,6 +1074,11 @@ def run_resnet18_report(ctx, args, eng, N):
     extra = {"close_ms_after_last_report": round(float(np.median(closes)), 3),
              "close_ms_after_last_report_all": [round(c, 3) for c in closes],
              "folded_before_close": int(np.median(early)) if early else 0,
+             "rows_folded_at_close": int(np.median(at_close)) if at_close else 0,
+             "speculative_folds": not args.no_speculate,
+             "report_gap_ms": args.report_gap_ms,
+             "pending_gpu_ms_at_close": [round(x, 3) for x in pending] if pending else None,
+             "rewinds_per_cycle": float(np.median(rewinds)) if rewinds else 0,
              "h2d_GBps": round(st["h2d_bytes_total"] / (st["h2d_ms_total"] / 1e3) / 1e9, 2) if st["h2d_ms_total"] else None,
              "new_checkpoint_bytes": len(new),
              "note": "PCIe-inclusive whole cycle (reports + close); compare close_ms_after_last_report with "

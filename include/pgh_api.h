@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PGH_ABI_VERSION 5
+#define PGH_ABI_VERSION 6
 
 typedef struct pgh_ctx pgh_ctx;
 
@@ -113,6 +113,10 @@ const char* pgh_last_error(const pgh_ctx* ctx);   /* ctx may be NULL (creation e
 /* Page-locked host buffers: ingest DMAs them straight to HBM (no staging copy). */
 int pgh_host_alloc(size_t bytes, void** out);
 int pgh_host_free(void* p);
+/* Fault in the pages of a (fresh, pageable) host buffer now, on up to 8 threads, so that a later
+ * copy into it -- the new checkpoint's payloads at a cycle close -- takes no page faults.  Best
+ * effort (Linux 5.14+ MADV_POPULATE_WRITE); always returns PGH_OK for a valid range. */
+int pgh_host_prefault(void* p, size_t n);
 
 /* ---- layout ------------------------------------------------------------------------------
  * Flat parameter vector = tensors concatenated in State order
@@ -202,6 +206,24 @@ int pgh_fold_slots_finish_resident(pgh_ctx* ctx, int mode, const int32_t* slots,
  * assumed, or a folded worker re-reported (submit_worker_diff overwrites its diff, :162-174):
  * the caller then re-folds every diff in the query's order, bit-identical to the reference. */
 int pgh_fold_slots_restart(pgh_ctx* ctx);
+/* Speculative report-time folds (ABI 6).  The close-time order is only certain up to the first
+ * assigned worker that has not reported; pgh_fold_slots_keep folds slots beyond that point into the
+ * running state WITHOUT freeing them (their diffs stay in HBM), and pgh_fold_mark saves the running
+ * state under `mark` (>= 0; replaces an older state of that id), so that when an earlier worker
+ * reports after all -- or re-reports -- pgh_fold_rewind restores the state saved before its
+ * position and the folds continue from there, bit-identical to folding in the final order.  The
+ * close then folds only the diffs after the last rewind point (pgh_fold_slots_finish_resident).
+ * Neither saving nor rewinding copies: a mark keeps the fold-state buffer as it stands (the next
+ * fold writes a spare one) and the fold after a rewind reads its state from the mark's buffer.
+ * Each mark holds P_shard floats of HBM until pgh_fold_unmark, pgh_reset or pgh_reserve; the
+ * weights of PGH_WEIGHTED_MEAN (fold order) are the caller's to set again after a rewind. */
+int pgh_fold_slots_keep(pgh_ctx* ctx, int mode, const int32_t* slots, int n);
+int pgh_fold_mark(pgh_ctx* ctx, int mark);
+int pgh_fold_rewind(pgh_ctx* ctx, int mark);
+int pgh_fold_unmark(pgh_ctx* ctx, int mark);
+/* *busy = 1 while the last slot fold issued is still running (a caller may then leave further
+ * speculative folds for later instead of queueing re-folds behind it), else 0.  Never blocks. */
+int pgh_fold_busy(pgh_ctx* ctx, int* busy);
 
 /* Z_2^64 share sum over all clients x parties, then decode float32(sum) / base**prec.
  * sum_out (int64) and dec_out (float32) are host arrays of P_shard; either may be NULL. */

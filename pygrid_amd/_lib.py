@@ -81,6 +81,7 @@ SIGNATURES = {
     "pgh_last_error": (C.c_char_p, [_vp]),
     "pgh_host_alloc": (_i, [_sz, C.POINTER(_vp)]),
     "pgh_host_free": (_i, [_vp]),
+    "pgh_host_prefault": (_i, [_vp, _sz]),
     "pgh_set_layout": (_i, [_vp, _i, _P64]),
     "pgh_set_shard": (_i, [_vp, _i64, _i64]),
     "pgh_reserve": (_i, [_vp, _i, _i, _i]),
@@ -103,6 +104,11 @@ SIGNATURES = {
     "pgh_fold_slots": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
     "pgh_fold_slots_finish_resident": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
     "pgh_fold_slots_restart": (_i, [_vp]),
+    "pgh_fold_slots_keep": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
+    "pgh_fold_mark": (_i, [_vp, _i]),
+    "pgh_fold_rewind": (_i, [_vp, _i]),
+    "pgh_fold_unmark": (_i, [_vp, _i]),
+    "pgh_fold_busy": (_i, [_vp, C.POINTER(C.c_int)]),
     "pgh_ckpt_download": (_i, [_vp, _vp]),
     "pgh_ckpt_patch_state": (_i, [_vp, C.c_char_p, _sz, _vp]),
     "pgh_secagg": (_i, [_vp, _i, _i, _vp, _vp]),
@@ -134,7 +140,7 @@ SIGNATURES = {
     "pgh_b64_decode_clean": (_i, [_vp, _sz, _vp, _sz, C.POINTER(_sz), _i]),
 }
 
-ABI_VERSION = 5  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
+ABI_VERSION = 6  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
 _LIB = None
 
 

@@ -43,6 +43,7 @@
 #include <deque>
 #include <fstream>
 #include <functional>
+#include <map>
 #include <string>
 #include <thread>
 #include <vector>
@@ -249,6 +250,14 @@ struct pgh_ctx {
     // the param ranges of the multi-GPU overlap): the copy stream waits on all before it
     // overwrites slots, and then forgets them (later copies are ordered after those waits).
     std::vector<std::pair<hipStream_t, hipEvent_t>> fold_evs;
+    // Folds that read every slab row (resident / stream / secagg): an ingest into any slot waits for
+    // them.  Slot folds (pgh_fold_slots*) read only their listed slots: each is numbered, a slot
+    // remembers the last one that read it, and an ingest into the slot waits for that fold alone --
+    // a report's DMA does not queue behind a fold of other slots (a speculative re-fold).
+    std::vector<std::pair<hipStream_t, hipEvent_t>> slab_evs;
+    std::vector<int64_t> slot_read_seq;                     // per slot; 0 = not read by a slot fold
+    std::deque<std::pair<int64_t, hipEvent_t>> slot_ring;  // recent slot folds on c->stream, in order
+    int64_t slot_seq = 0;
     std::vector<hipEvent_t> fold_ev_pool;
     // STREAM: one event per fold with the fold front after it, so overwriting a slot waits only
     // for the fold that consumed the slot's previous client (not for the latest fold).
@@ -312,6 +321,15 @@ struct pgh_ctx {
     size_t vtab_cap = 0;
     hipEvent_t vtab_ev = nullptr;
     bool vtab_used = false;
+    // page-locked fp32 State messages (pgh_ingest_state): DMA'd whole into d_vbytes, gathered into the
+    // slab row by k_gather_f32 with this chunk table (PGH_PINNED_GATHER=0: one DMA per payload piece)
+    pgh::GChunk* d_gtab = nullptr;
+    pgh::GChunk* h_gtab = nullptr;  // pinned
+    size_t gtab_cap = 0;
+    hipEvent_t gtab_ev = nullptr;    // the last table upload (h_gtab reusable after it)
+    hipEvent_t gdma_ev = nullptr;    // the last message DMA (the caller's buffer is free after it)
+    bool gtab_used = false;
+    bool pinned_gather = true;
     // PGH_SHARE_FILL_MB: cap on one pinned fill of share payloads (default: the whole slot; r01z:
     // 8 / 16 / 32 / 128 MiB fills gave 29.6 / 30.8 / 34.7 / 41.6 wire GB/s at ResNet-18 x 16 x 2)
     size_t share_fill = ~(size_t)0;
@@ -339,6 +357,14 @@ struct pgh_ctx {
     int64_t client_base = 0;  // synthetic client k is generated as global client client_base + k
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
+    // Saved slot-fold states (pgh_fold_mark / pgh_fold_rewind: speculative report-time folds).  A mark
+    // takes over the d_acc buffer it names (d_acc moves on to a spare one), so neither saving nor
+    // rewinding copies: after a rewind the next slot fold reads its running state from the mark's
+    // buffer (acc_src) and writes d_acc.
+    struct SavedFold { float* buf; int64_t folded; int mode; };
+    std::map<int, SavedFold> fold_marks;
+    std::vector<float*> acc_spare;     // [pvec] fold-state buffers not in use
+    const float* acc_src = nullptr;    // set by a rewind: the running state lives here, not in d_acc
     std::vector<float> weights;
     bool weights_on_device = false;
 
@@ -407,6 +433,8 @@ double now_ms() {
 
 size_t esize(int dtype) { return dtype == PGH_F32 ? 4 : 8; }
 
+void release_slot_fold_events(pgh_ctx* c);
+
 void free_slab(pgh_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
@@ -418,6 +446,11 @@ void free_slab(pgh_ctx* c) {
     for (auto& m : c->final_marks) c->rmark_pool.push_back(m.ev);
     c->final_marks.clear();
     (void)hipFree(c->d_acc); c->d_acc = nullptr;
+    for (auto& m : c->fold_marks) (void)hipFree(m.second.buf);
+    c->fold_marks.clear();
+    for (float* b : c->acc_spare) (void)hipFree(b);
+    c->acc_spare.clear();
+    c->acc_src = nullptr;
     (void)hipFree(c->d_uacc); c->d_uacc = nullptr;
     (void)hipFree(c->d_sum); c->d_sum = nullptr;
     (void)hipFree(c->d_dec); c->d_dec = nullptr;
@@ -431,6 +464,8 @@ void free_slab(pgh_ctx* c) {
     c->folded = 0;
     for (auto& fe : c->fold_evs) c->fold_ev_pool.push_back(fe.second);
     c->fold_evs.clear();
+    release_slot_fold_events(c);
+    c->slot_read_seq.clear();
     c->weights_on_device = false;
 }
 
@@ -661,6 +696,13 @@ void prefault_small(uint8_t* p, size_t n) {
     (void)madvise((void*)a, b - a, MADV_POPULATE_WRITE);
 }
 
+// MADV_POPULATE_WRITE over [p, p + n) whatever its size (pgh_host_prefault's per-thread piece).
+void prefault_small_any(uint8_t* p, size_t n) {
+    static const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
+    const uintptr_t a = (uintptr_t)p & ~(page - 1), b = ((uintptr_t)p + n + page - 1) & ~(page - 1);
+    (void)madvise((void*)a, b - a, MADV_POPULATE_WRITE);
+}
+
 // The same for a big fresh destination, split over the copy pool's threads: run while the fold
 // and the first D2H are still in flight, so the copy-out afterwards writes to resident pages
 // instead of taking a page fault per 4 KiB (PGH_PREFAULT=0 turns it off).
@@ -805,6 +847,67 @@ int order_after_ingest(pgh_ctx* c, hipStream_t s) {
     return PGH_OK;
 }
 
+void release_slot_fold_events(pgh_ctx* c) {
+    for (auto& fe : c->slab_evs) c->fold_ev_pool.push_back(fe.second);
+    c->slab_evs.clear();
+    for (auto& r : c->slot_ring) c->fold_ev_pool.push_back(r.second);
+    c->slot_ring.clear();
+    std::fill(c->slot_read_seq.begin(), c->slot_read_seq.end(), 0);
+}
+
+hipEvent_t take_fold_event(pgh_ctx* c) {
+    hipEvent_t ev = nullptr;
+    if (!c->fold_ev_pool.empty()) { ev = c->fold_ev_pool.back(); c->fold_ev_pool.pop_back(); }
+    else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+    return ev;
+}
+
+// A fold reading every slab row was issued on stream s.
+int record_slab_fold(pgh_ctx* c, hipStream_t s) {
+    hipEvent_t ev = nullptr;
+    for (auto& fe : c->slab_evs)
+        if (fe.first == s) ev = fe.second;
+    if (!ev) {
+        if (!(ev = take_fold_event(c))) return fail(c, PGH_E_HIP, "hipEventCreate failed");
+        c->slab_evs.push_back({s, ev});
+    }
+    CK(c, hipEventRecord(ev, s));
+    return PGH_OK;
+}
+
+// A slot fold reading `slots` was issued on c->stream.
+int record_slot_fold(pgh_ctx* c, const int32_t* slots, int n) {
+    hipEvent_t ev = take_fold_event(c);
+    if (!ev) return fail(c, PGH_E_HIP, "hipEventCreate failed");
+    CK(c, hipEventRecord(ev, c->stream));
+    const int64_t seq = ++c->slot_seq;
+    c->slot_ring.push_back({seq, ev});
+    for (int k = 0; k < n; ++k) c->slot_read_seq[(size_t)slots[k]] = seq;
+    while (c->slot_ring.size() > 64) {  // an older fold is done when a newer one on its stream is
+        c->fold_ev_pool.push_back(c->slot_ring.front().second);
+        c->slot_ring.pop_front();
+    }
+    return PGH_OK;
+}
+
+// RESIDENT: before the copy stream overwrites `slot`, it waits for the folds that may still read it.
+int order_slot_overwrite(pgh_ctx* c, int slot) {
+    for (auto& fe : c->slab_evs) CK(c, hipStreamWaitEvent(c->copy, fe.second, 0));
+    for (auto& fe : c->slab_evs) c->fold_ev_pool.push_back(fe.second);
+    c->slab_evs.clear();
+    const int64_t seq = c->slot_read_seq[(size_t)slot];
+    if (seq == 0 || c->slot_ring.empty()) return PGH_OK;
+    hipEvent_t ev = c->slot_ring.back().second;
+    for (auto& r : c->slot_ring)
+        if (r.first >= seq) { ev = r.second; break; }  // that fold, or a later one on c->stream
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return PGH_OK;
+    if (q != hipErrorNotReady) return fail(c, PGH_E_HIP, "hipEventQuery failed: %s", hipGetErrorString(q));
+    (void)hipGetLastError();
+    CK(c, hipStreamWaitEvent(c->copy, ev, 0));
+    return PGH_OK;
+}
+
 // Before the copy stream overwrites a slot, it waits for every fold issued so far (the last one
 // on each stream that ran folds).
 int order_before_overwrite(pgh_ctx* c) {
@@ -831,6 +934,16 @@ int record_fold(pgh_ctx* c, hipStream_t s) {
 void clear_marks(pgh_ctx* c) {
     for (auto& m : c->marks) c->mark_pool.push_back(m.ev);
     c->marks.clear();
+}
+
+// Forget every saved slot-fold state (and a pending rewind: the caller discards the fold state too).
+// Their buffers become spares; anything still reading them is ordered on c->stream before the next
+// writer (a slot fold on the same stream).
+void drop_fold_marks(pgh_ctx* c) {
+    for (auto& m : c->fold_marks)
+        if (m.second.buf) c->acc_spare.push_back(m.second.buf);
+    c->fold_marks.clear();
+    c->acc_src = nullptr;
 }
 
 // STREAM: the slots of clients up to `last_client` held clients up to last_client - R before;
@@ -986,7 +1099,8 @@ int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const Fina
         }
         done += seg;
     } while (done < n);
-    return record_fold(c, s);
+    RC(record_fold(c, s));
+    return record_slab_fold(c, s);
 }
 
 // Length of the run of ingested clients starting at `from` (slot ring order).
@@ -1024,7 +1138,7 @@ int claim_slot(pgh_ctx* c, int64_t client, int* slot_out) {
     if (!c->streaming) {
         if (client >= c->slots)
             return fail(c, PGH_E_ARG, "client %lld outside slab capacity %d", (long long)client, c->slots);
-        RC(order_before_overwrite(c));  // a fold issued earlier (any stream) may still read the slab
+        RC(order_slot_overwrite(c, (int)client));  // a fold issued earlier may still read the slot
         *slot_out = (int)client;
         return PGH_OK;
     }
@@ -1112,6 +1226,24 @@ int pgh_host_alloc(size_t bytes, void** out) {
     return PGH_OK;
 }
 
+int pgh_host_prefault(void* p, size_t n) {
+    if (!p || !n) return PGH_OK;
+    const size_t per = (size_t)8 << 20;
+    const int k = (int)std::min<size_t>(8, (n + per - 1) / per);
+    if (k <= 1) {
+        prefault_small_any((uint8_t*)p, n);
+        return PGH_OK;
+    }
+    std::vector<std::thread> ts;
+    const size_t step = (n + (size_t)k - 1) / (size_t)k;
+    for (int i = 0; i < k; ++i) {
+        const size_t a = (size_t)i * step, b = std::min(n, a + step);
+        if (a < b) ts.emplace_back([=] { prefault_small_any((uint8_t*)p + a, b - a); });
+    }
+    for (auto& t : ts) t.join();
+    return PGH_OK;
+}
+
 int pgh_host_free(void* p) {
     if (p && hipHostFree(p) != hipSuccess) return fail(nullptr, PGH_E_HIP, "hipHostFree failed");
     return PGH_OK;
@@ -1138,6 +1270,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     }
     c->pool_copy.reset(new CopyPool(c->copy_threads, c->local_cpus));
     if (const char* e = std::getenv("PGH_REGISTER_INGEST")) c->register_ingest = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PGH_PINNED_GATHER")) c->pinned_gather = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_SYNTH_WGS")) c->synth_wgs = std::max(0LL, std::atoll(e));
     if (const char* e = std::getenv("PGH_SYNTH_SERIAL")) c->synth_serial = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_SYNTH_NT")) c->synth_nt = std::atoi(e) != 0;
@@ -1233,6 +1366,10 @@ void pgh_destroy(pgh_ctx* c) {
     (void)hipFree(c->d_vtab);
     if (c->h_vtab) (void)hipHostFree(c->h_vtab);
     if (c->vtab_ev) (void)hipEventDestroy(c->vtab_ev);
+    (void)hipFree(c->d_gtab);
+    if (c->h_gtab) (void)hipHostFree(c->h_gtab);
+    if (c->gtab_ev) (void)hipEventDestroy(c->gtab_ev);
+    if (c->gdma_ev) (void)hipEventDestroy(c->gdma_ev);
     for (int k = 0; k < 2; ++k) {
         if (c->h_pin[k]) (void)hipHostFree(c->h_pin[k]);
         if (c->pin_ev[k]) (void)hipEventDestroy(c->pin_ev[k]);
@@ -1317,6 +1454,7 @@ int pgh_reserve(pgh_ctx* c, int max_clients, int dtype, int n_parties) {
     c->dtype = dtype;
     c->parties = n_parties;
     c->slot_client.assign((size_t)max_clients, -1);
+    c->slot_read_seq.assign((size_t)max_clients, 0);
     c->weights.clear();
     c->weights_on_device = false;
     c->st.max_clients = max_clients;
@@ -1334,6 +1472,8 @@ int pgh_reset(pgh_ctx* c) {
     for (auto& fe : c->fold_evs) c->fold_ev_pool.push_back(fe.second);
     c->fold_evs.clear();
     clear_marks(c);
+    drop_fold_marks(c);
+    release_slot_fold_events(c);  // c->stream is idle (synchronised above)
     std::fill(c->slot_client.begin(), c->slot_client.end(), -1);
     c->weights.clear();
     c->weights_on_device = false;
@@ -1367,6 +1507,10 @@ int pgh_ingest_raw(pgh_ctx* c, int client, const void* flat, size_t nbytes, int 
     return mark_ingested(c, client, slot);
 }
 
+namespace {
+int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>& pieces, int slot);
+}
+
 int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
     if (c && c->grp) return pgh_group_api::ingest_state(c, client, pb, n);
     RC(check_dtype(c, PGH_F32));
@@ -1381,10 +1525,20 @@ int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
     DeviceGuard g(c->device);
     int slot = 0;
     RC(claim_slot(c, client, &slot));
-    if (n && is_pinned(pb)) {
+    if (n && !pieces.empty() && c->pinned_gather && is_pinned(pb)) {
         // Page-locked message (a report decoded straight into pgh_host_alloc memory,
-        // pygrid_amd.report.PinnedPool): the payload spans are DMA'd as they lie, no staging copy.
-        // The buffer is only borrowed for the call, so the call waits for its copies.
+        // pygrid_amd.report.PinnedPool): no staging copy.  The part of the message holding this
+        // shard's payloads goes to HBM in ONE DMA (a few hundred bytes of framing ride along) and
+        // k_gather_f32 moves the payloads into the slab row; the call waits for the DMA only (the
+        // buffer is borrowed), the gather runs on behind it on the copy stream.
+        const double t0 = now_ms();
+        RC(pinned_gather_ingest(c, pb, pieces, slot));
+        c->st.h2d_ms_total += now_ms() - t0;
+        return mark_ingested(c, client, slot);
+    }
+    if (n && is_pinned(pb)) {
+        // Page-locked message, one DMA per payload piece (PGH_PINNED_GATHER=0).  The buffer is only
+        // borrowed for the call, so the call waits for its copies.
         const double t0 = now_ms();
         const Dest d = row_dest(c, slot, 0);
         size_t off = 0;
@@ -1545,6 +1699,58 @@ int stage_share_msg(pgh_ctx* c, ShareMsg& m) {
     c->st.h2d_ms_total += now_ms() - t0;
     c->st.h2d_bytes_total += m.bytes;
     c->st.h2d_staged_bytes_total += m.bytes;
+    return PGH_OK;
+}
+
+// pgh_ingest_state of a page-locked message: [first payload, last payload end) of this shard in one
+// DMA to d_vbytes, the gather table behind it, then k_gather_f32 into the slot's row.
+int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>& pieces, int slot) {
+    const size_t a = (size_t)(pieces.front().src - pb) & ~(size_t)63;
+    const size_t b = (size_t)(pieces.back().src - pb) + pieces.back().n;
+    std::vector<pgh::GChunk> tab;
+    int64_t dst = 0;
+    size_t total = 0;
+    for (auto& p : pieces) {
+        const int64_t nf = (int64_t)(p.n / 4);
+        const int64_t src = (int64_t)((size_t)(p.src - pb) - a);
+        for (int64_t k = 0; k < nf; k += pgh::GATHER_CHUNK)
+            tab.push_back({src + 4 * k, dst + k, (int32_t)std::min<int64_t>(pgh::GATHER_CHUNK, nf - k), 0});
+        dst += nf;
+        total += p.n;
+    }
+    if (tab.empty()) return PGH_OK;
+    RC(grow_device(c, (void**)&c->d_vbytes, &c->vbytes_cap, b - a + 16, "pinned message buffer"));
+    const size_t tb = tab.size() * sizeof(pgh::GChunk);
+    if (!c->gtab_ev) CK(c, hipEventCreateWithFlags(&c->gtab_ev, hipEventDisableTiming));
+    if (!c->gdma_ev) CK(c, hipEventCreateWithFlags(&c->gdma_ev, hipEventDisableTiming));
+    if (c->gtab_used) CK(c, hipEventSynchronize(c->gtab_ev));  // the previous table upload read h_gtab
+    if (tb > c->gtab_cap) {
+        if (c->h_gtab) (void)hipHostFree(c->h_gtab);
+        c->h_gtab = nullptr;
+        size_t cap = 0;
+        void* d = c->d_gtab;
+        RC(grow_device(c, &d, &cap, tb, "gather chunk table"));
+        c->d_gtab = (pgh::GChunk*)d;
+        if (hipHostMalloc((void**)&c->h_gtab, cap, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            c->gtab_cap = 0;
+            return fail(c, PGH_E_OOM, "pinned gather table of %zu bytes failed", cap);
+        }
+        c->gtab_cap = cap;
+        c->gtab_used = false;
+    }
+    std::memcpy(c->h_gtab, tab.data(), tb);
+    CK(c, hipMemcpyAsync(c->d_gtab, c->h_gtab, tb, hipMemcpyHostToDevice, c->copy));
+    CK(c, hipEventRecord(c->gtab_ev, c->copy));
+    c->gtab_used = true;
+    CK(c, hipMemcpyAsync(c->d_vbytes, pb + a, b - a, hipMemcpyHostToDevice, c->copy));
+    CK(c, hipEventRecord(c->gdma_ev, c->copy));
+    const Dest d = row_dest(c, slot, 0);
+    const hipError_t e = pgh::launch_gather_f32(c->d_vbytes, c->d_gtab, (int)tab.size(), (float*)d.base, d.map,
+                                                c->copy);
+    if (e != hipSuccess) return fail(c, PGH_E_HIP, "gather launch failed: %s", hipGetErrorString(e));
+    CK(c, hipEventSynchronize(c->gdma_ev));
+    c->st.h2d_bytes_total += total;
     return PGH_OK;
 }
 
@@ -1962,7 +2168,7 @@ int pgh_secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out)
 // ---- report-time folds of scattered slots (pgh_fold_slots) -------------------------------------
 
 namespace {
-int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
+int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final, bool keep = false) {
     RC(check_dtype(c, PGH_F32));
     if (!valid_mode(mode)) return fail(c, PGH_E_ARG, "unknown averaging mode %d", mode);
     if (c->streaming) return fail(c, PGH_E_STATE, "context is streaming: slot folds need a RESIDENT slab");
@@ -2028,6 +2234,7 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
             ar.map.off = lo;
             ar.p = hi - lo;
             ar.acc = c->d_acc + lo;
+            ar.acc_in = (done == 0 && c->acc_src) ? c->acc_src + lo : nullptr;  // rewound: the mark's buffer
             ar.ckpt = c->d_ckpt + lo;
             ar.out = c->d_out + lo;
             const uint64_t rp = (uint64_t)(hi - lo);
@@ -2039,7 +2246,10 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
         done += m;
     } while (done < n);
     RC(record_fold(c, s));
-    for (int k = 0; k < n; ++k) c->slot_client[(size_t)slots[k]] = -1;  // free for the next ingests
+    RC(record_slot_fold(c, slots, n));
+    c->acc_src = nullptr;  // the running state is in d_acc again
+    if (!keep)
+        for (int k = 0; k < n; ++k) c->slot_client[(size_t)slots[k]] = -1;  // free for the next ingests
     c->folded = total;
     c->st.n_folded = total;
     c->slot_mode = mode;
@@ -2067,13 +2277,119 @@ int pgh_fold_slots_finish_resident(pgh_ctx* c, int mode, const int32_t* slots, i
     return PGH_OK;
 }
 
+int pgh_fold_slots_keep(pgh_ctx* c, int mode, const int32_t* slots, int n) {
+    if (c && c->grp) return pgh_group_api::fold_slots_keep(c, mode, slots, n);
+    if (!c) return PGH_E_ARG;
+    return slot_fold(c, mode, slots, n, false, true);
+}
+
+namespace {
+int check_slot_folds(pgh_ctx* c) {
+    RC(check_dtype(c, PGH_F32));
+    if (c->streaming) return fail(c, PGH_E_STATE, "context is streaming: slot folds need a RESIDENT slab");
+    return PGH_OK;
+}
+constexpr size_t MAX_FOLD_MARKS = 4096;
+}  // namespace
+
+int pgh_fold_mark(pgh_ctx* c, int mark) {
+    if (c && c->grp) return pgh_group_api::fold_mark(c, mark);
+    if (!c) return PGH_E_ARG;
+    RC(check_slot_folds(c));
+    if (mark < 0) return fail(c, PGH_E_ARG, "negative mark %d", mark);
+    auto it = c->fold_marks.find(mark);
+    if (it == c->fold_marks.end() && c->fold_marks.size() >= MAX_FOLD_MARKS)
+        return fail(c, PGH_E_STATE, "more than %zu saved fold states", MAX_FOLD_MARKS);
+    DeviceGuard g(c->device);
+    pgh_ctx::SavedFold m{nullptr, c->folded, c->slot_mode};
+    if (c->folded > 0) {
+        float* spare = nullptr;
+        if (!c->acc_spare.empty()) {
+            spare = c->acc_spare.back();
+            c->acc_spare.pop_back();
+        } else if (hipMalloc((void**)&spare, (size_t)c->pvec * 4) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(c, PGH_E_OOM, "fold state buffer (%lld floats) allocation failed", (long long)c->pvec);
+        }
+        if (c->acc_src) {
+            // right after a rewind the state lives in another mark's buffer: this mark gets a copy
+            CK(c, hipMemcpyAsync(spare, c->acc_src, (size_t)c->pg * 4, hipMemcpyDeviceToDevice, c->stream));
+            m.buf = spare;
+        } else {
+            // the mark keeps d_acc as it stands; the next fold reads it there and writes the spare
+            m.buf = c->d_acc;
+            c->d_acc = spare;
+            c->acc_src = m.buf;
+        }
+    }
+    if (it != c->fold_marks.end()) {
+        if (it->second.buf) {
+            if (c->acc_src == it->second.buf) {  // the pending state is the mark being replaced
+                CK(c, hipMemcpyAsync(c->d_acc, c->acc_src, (size_t)c->pg * 4, hipMemcpyDeviceToDevice, c->stream));
+                c->acc_src = nullptr;
+            }
+            c->acc_spare.push_back(it->second.buf);
+        }
+        it->second = m;
+    } else {
+        c->fold_marks.emplace(mark, m);
+    }
+    return PGH_OK;
+}
+
+int pgh_fold_rewind(pgh_ctx* c, int mark) {
+    if (c && c->grp) return pgh_group_api::fold_rewind(c, mark);
+    if (!c) return PGH_E_ARG;
+    RC(check_slot_folds(c));
+    auto it = c->fold_marks.find(mark);
+    if (it == c->fold_marks.end()) return fail(c, PGH_E_ARG, "no saved fold state %d", mark);
+    c->folded = it->second.folded;
+    c->st.n_folded = c->folded;
+    c->slot_mode = it->second.folded > 0 ? it->second.mode : -1;
+    c->acc_src = it->second.buf;  // the next slot fold reads the state there (no copy)
+    return PGH_OK;
+}
+
+int pgh_fold_unmark(pgh_ctx* c, int mark) {
+    if (c && c->grp) return pgh_group_api::fold_unmark(c, mark);
+    if (!c) return PGH_E_ARG;
+    RC(check_slot_folds(c));
+    auto it = c->fold_marks.find(mark);
+    if (it == c->fold_marks.end()) return fail(c, PGH_E_ARG, "no saved fold state %d", mark);
+    if (it->second.buf) {
+        if (c->acc_src == it->second.buf) {  // rewound to it and not folded since: keep the state
+            DeviceGuard g(c->device);
+            CK(c, hipMemcpyAsync(c->d_acc, c->acc_src, (size_t)c->pg * 4, hipMemcpyDeviceToDevice, c->stream));
+            c->acc_src = nullptr;
+        }
+        c->acc_spare.push_back(it->second.buf);
+    }
+    c->fold_marks.erase(it);
+    return PGH_OK;
+}
+
+int pgh_fold_busy(pgh_ctx* c, int* busy) {
+    if (c && c->grp) return pgh_group_api::fold_busy(c, busy);
+    if (!c || !busy) return PGH_E_ARG;
+    *busy = 0;
+    if (c->slot_ring.empty()) return PGH_OK;
+    const hipError_t q = hipEventQuery(c->slot_ring.back().second);
+    if (q == hipErrorNotReady) {
+        (void)hipGetLastError();
+        *busy = 1;
+    } else if (q != hipSuccess) {
+        return fail(c, PGH_E_HIP, "hipEventQuery failed: %s", hipGetErrorString(q));
+    }
+    return PGH_OK;
+}
+
 int pgh_fold_slots_restart(pgh_ctx* c) {
     if (c && c->grp) return pgh_group_api::fold_restart(c);
     if (!c) return PGH_E_ARG;
-    RC(check_dtype(c, PGH_F32));
-    if (c->streaming) return fail(c, PGH_E_STATE, "context is streaming: slot folds need a RESIDENT slab");
+    RC(check_slot_folds(c));
     // The next slot fold's FL_FIRST pass overwrites the fold state on c->stream, behind any fold
-    // still in flight there: nothing to wait for.
+    // still in flight there: nothing to wait for.  Saved fold states are kept.
+    c->acc_src = nullptr;
     c->folded = 0;
     c->st.n_folded = 0;
     c->slot_mode = -1;

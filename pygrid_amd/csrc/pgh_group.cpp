@@ -803,6 +803,35 @@ int fold_restart(pgh_ctx* c) {
     return fan(c, [](int, pgh_ctx* k) -> int { return pgh_fold_slots_restart(k); });
 }
 
+int fold_slots_keep(pgh_ctx* c, int mode, const int32_t* slots, int n) {
+    RC(need_slab(c));
+    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_slots_keep(k, mode, slots, n); });
+}
+
+int fold_mark(pgh_ctx* c, int mark) {
+    RC(need_slab(c));
+    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_mark(k, mark); });
+}
+
+int fold_rewind(pgh_ctx* c, int mark) {
+    RC(need_slab(c));
+    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_rewind(k, mark); });
+}
+
+int fold_busy(pgh_ctx* c, int* busy) {
+    RC(need_slab(c));
+    std::vector<int> b((size_t)G(c)->kids.size(), 0);
+    RC(fan(c, [&](int i, pgh_ctx* k) -> int { return pgh_fold_busy(k, &b[(size_t)i]); }));
+    *busy = 0;
+    for (int x : b) *busy |= x;
+    return PGH_OK;
+}
+
+int fold_unmark(pgh_ctx* c, int mark) {
+    RC(need_slab(c));
+    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_unmark(k, mark); });
+}
+
 int secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out) {
     pgh_group* g = G(c);
     RC(need_slab(c));

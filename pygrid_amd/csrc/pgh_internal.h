@@ -65,6 +65,11 @@ int ckpt_download(pgh_ctx* c, float* out);
 int ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out);
 int fold_slots(pgh_ctx* c, int mode, const int32_t* slots, int n, bool finish);
 int fold_restart(pgh_ctx* c);
+int fold_slots_keep(pgh_ctx* c, int mode, const int32_t* slots, int n);
+int fold_mark(pgh_ctx* c, int mark);
+int fold_rewind(pgh_ctx* c, int mark);
+int fold_unmark(pgh_ctx* c, int mark);
+int fold_busy(pgh_ctx* c, int* busy);
 int secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out);
 int stream_begin(pgh_ctx* c, int kind, int fold_batch);
 int stream_flush(pgh_ctx* c);

@@ -39,7 +39,9 @@ struct FedavgArgs {
     int64_t p;              // params in this shard
     const float* weights;   // [n_rows] device, MODE_WEIGHTED only
     const double* recips;   // [n_rows] device, MODE_ITERATIVE: 1 / (double)(float)(client0 + r + 1)
-    float* acc;             // [p] running state; read unless FL_FIRST, written unless FL_FINAL
+    float* acc;             // [p] running state; written unless FL_FINAL
+    const float* acc_in;    // [p] running state read unless FL_FIRST (nullptr: acc; a saved fold
+                            // state, pgh_fold_rewind, is read from where it was saved)
     const float* ckpt;      // [p], FL_FINAL only
     float* out;             // [p], FL_FINAL only
     float divisor;          // float(N) or sum of weights, FL_FINAL of MEAN / WEIGHTED
@@ -105,6 +107,21 @@ struct VChunk {
 // lo <= i < hi.  Requires validated input (no varint longer than 10 bytes).
 hipError_t launch_varint_decode(const uint8_t* bytes, const VChunk* chunks, int n_chunks, int64_t* row,
                                 const SlabMap& m, int64_t lo, int64_t hi, hipStream_t s);
+
+// Float payloads of a page-locked State message, DMA'd into HBM as they lie in the message (no host
+// staging copy), gathered into one slab row: chunk k moves n floats starting at byte `src` of the
+// buffer (any alignment: protobuf puts a payload right after its varint length) to shard elements
+// dst .. dst + n - 1 of the row (row[m.at(i)]).  The buffer holds 8 readable bytes past the last
+// payload byte.
+constexpr int GATHER_CHUNK = 4096;
+struct GChunk {
+    int64_t src;
+    int64_t dst;
+    int32_t n;
+    int32_t pad;
+};
+hipError_t launch_gather_f32(const uint8_t* bytes, const GChunk* chunks, int n_chunks, float* row, const SlabMap& m,
+                             hipStream_t s);
 
 constexpr uint64_t STREAM_DIFF = 0, STREAM_CKPT = 1, STREAM_SECRET = 2, STREAM_SHARE = 3;
 constexpr float DIFF_SCALE = 2.6429e-7f;

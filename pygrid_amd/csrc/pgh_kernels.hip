@@ -204,7 +204,7 @@ __device__ __forceinline__ void fedavg_columns(const FedavgArgs& a, const RowTab
         r = 1;
     } else {
 #pragma unroll
-        for (int w = 0; w < W; ++w) acc[w] = L::load_tail(a.acc, q0 + w * qstep, a.p);
+        for (int w = 0; w < W; ++w) acc[w] = L::load_tail(a.acc_in, q0 + w * qstep, a.p);
         r = 0;
     }
     for (; r + U <= n; r += U) {
@@ -257,7 +257,7 @@ __device__ __forceinline__ void fedavg_columns_pipe(const FedavgArgs& a, int64_t
         if constexpr (MODE == MODE_WEIGHTED) acc[0] = acc[0] * a.weights[0];
         r = 1;
     } else {
-        acc[0] = L::load_tail(a.acc, q, a.p);
+        acc[0] = L::load_tail(a.acc_in, q, a.p);
         r = 0;
     }
     T A[U][1], B[U][1];
@@ -411,6 +411,22 @@ __global__ __launch_bounds__(TB) void k_secagg(SecaggArgs a, int64_t ncol) {
                 a.acc[i + e] = x;
             }
         }
+    }
+}
+
+// Page-locked report ingest (pgh_ingest_state): one workgroup per chunk of a float payload that
+// sits at an arbitrary byte offset of the DMA'd message; lanes read the two aligned dwords around
+// their float and funnel-shift it out (v_alignbyte), then store into the blocked slab row.  Bound by
+// HBM like a copy (4 B read + 4 B written per param; the message is read once).
+__global__ __launch_bounds__(BLOCK) void k_gather_f32(const uint8_t* bytes, const GChunk* tab, float* row,
+                                                      SlabMap m) {
+    const GChunk ch = tab[blockIdx.x];
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(bytes + (ch.src & ~int64_t(3)));
+    const uint32_t sh = (uint32_t)(ch.src & 3);
+    for (int t = threadIdx.x; t < ch.n; t += BLOCK) {
+        const uint32_t lo = w[t];
+        const uint32_t v = sh ? __builtin_amdgcn_alignbyte(w[t + 1], lo, sh) : lo;
+        row[m.at(ch.dst + t)] = __uint_as_float(v);
     }
 }
 
@@ -790,7 +806,12 @@ bool valid_map(const SlabMap& m, int64_t p) {
     return m.bshift > 0 && m.bshift < 40 && (int64_t(1) << m.bshift) == m.ld && m.bmask == m.ld - 1 && m.bstride >= m.ld;
 }
 
-hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+hipError_t launch_fedavg(const FedavgArgs& a_, hipStream_t s) {
+    FedavgArgs a = a_;
+    if (!a.acc_in) a.acc_in = a.acc;
+    if (!(a.flags & FL_FIRST) && (!a.acc_in || !aligned16(a.acc_in))) return hipErrorInvalidValue;
     if (a.p <= 0 || a.n_rows < 0 || !valid_map(a.map, a.p)) return hipErrorInvalidValue;
     if ((a.flags & FL_FIRST) && a.n_rows < 1) return hipErrorInvalidValue;
     if (a.n_rows > 0 && (!a.diffs || (reinterpret_cast<uintptr_t>(a.diffs) & 15))) return hipErrorInvalidValue;
@@ -810,7 +831,10 @@ hipError_t launch_fedavg(const FedavgArgs& a, hipStream_t s) {
     }
 }
 
-hipError_t launch_fedavg_rows(const FedavgArgs& a, const RowTab& t, hipStream_t s) {
+hipError_t launch_fedavg_rows(const FedavgArgs& a_, const RowTab& t, hipStream_t s) {
+    FedavgArgs a = a_;
+    if (!a.acc_in) a.acc_in = a.acc;
+    if (!(a.flags & FL_FIRST) && (!a.acc_in || !aligned16(a.acc_in))) return hipErrorInvalidValue;
     if (a.n_rows > ROWTAB_MAX) return hipErrorInvalidValue;
     if (a.p <= 0 || a.n_rows < 0 || !valid_map(a.map, a.p)) return hipErrorInvalidValue;
     if ((a.flags & FL_FIRST) && a.n_rows < 1) return hipErrorInvalidValue;
@@ -900,6 +924,15 @@ hipError_t launch_varint_decode(const uint8_t* bytes, const VChunk* chunks, int 
         return hipErrorInvalidValue;
     if (n_chunks == 0) return hipSuccess;
     k_varint_decode<<<(unsigned)n_chunks, 256, 0, s>>>(bytes, chunks, row, m, lo, hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_f32(const uint8_t* bytes, const GChunk* chunks, int n_chunks, float* row, const SlabMap& m,
+                             hipStream_t s) {
+    if (n_chunks < 0 || (n_chunks > 0 && (!bytes || !chunks || !row)) || (reinterpret_cast<uintptr_t>(bytes) & 3))
+        return hipErrorInvalidValue;
+    if (n_chunks == 0) return hipSuccess;
+    k_gather_f32<<<(unsigned)n_chunks, BLOCK, 0, s>>>(bytes, chunks, row, m);
     return hipGetLastError();
 }
 

@@ -312,6 +312,30 @@ class Engine:
         keep their diffs, weights must be set again."""
         self._check(self._lib.pgh_fold_slots_restart(self._h), "fold_slots_restart")
 
+    def fold_slots_keep(self, mode: int, slots: Sequence[int]):
+        """Fold ``slots`` into the running state and KEEP their diffs (a later rewind may fold them
+        again: speculative folds past a worker that has not reported yet)."""
+        a = np.ascontiguousarray(slots, dtype=np.int32)
+        self._check(self._lib.pgh_fold_slots_keep(self._h, int(mode), a.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                  a.size), "fold_slots_keep")
+
+    def fold_mark(self, mark: int):
+        """Save the running fold state under ``mark`` (no copy; P_shard floats of HBM until unmarked)."""
+        self._check(self._lib.pgh_fold_mark(self._h, int(mark)), "fold_mark")
+
+    def fold_rewind(self, mark: int):
+        """Restore the fold state saved under ``mark`` (weights must be set again)."""
+        self._check(self._lib.pgh_fold_rewind(self._h, int(mark)), "fold_rewind")
+
+    def fold_unmark(self, mark: int):
+        self._check(self._lib.pgh_fold_unmark(self._h, int(mark)), "fold_unmark")
+
+    def fold_busy(self) -> bool:
+        """The last slot fold issued is still running (non-blocking)."""
+        b = C.c_int(0)
+        self._check(self._lib.pgh_fold_busy(self._h, C.byref(b)), "fold_busy")
+        return bool(b.value)
+
     def ckpt_download(self) -> np.ndarray:
         out = np.empty(self.p_shard, dtype=np.float32)
         self._check(self._lib.pgh_ckpt_download(self._h, _ptr(out)), "ckpt_download")

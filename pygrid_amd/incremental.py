@@ -64,6 +64,8 @@ from .exceptions import AggregationError, ModelNotAcceleratedError, StateParseEr
 
 DEFAULT_HBM_BUDGET = 64 << 30  # bytes of diffs kept in HBM per cycle when `slots` is not given
 MAX_DEFAULT_SLOTS = 4096
+DEFAULT_SPECULATION_BUDGET = 16 << 30  # bytes of HBM for saved fold states (speculative folds)
+MAX_MARKS = 256
 
 log = logging.getLogger(__name__)
 
@@ -75,32 +77,48 @@ def default_slots(P: int, budget: int = DEFAULT_HBM_BUDGET) -> int:
 class IncrementalCycle:
     def __init__(self, engine: Engine, numel, mode: int = MEAN, slots: Optional[int] = None, fold_batch: int = 8,
                  weights_by_worker: Optional[Dict[object, float]] = None, checkpoint: Optional[bytes] = None,
-                 early_fold: bool = True):
+                 early_fold: bool = True, speculate: Optional[bool] = None,
+                 speculation_budget: int = DEFAULT_SPECULATION_BUDGET, mark_every: int = 8, lazy: bool = True):
         self.engine = engine
         self.mode = mode
         self._numel = tuple(int(n) for n in numel)
-        self.slots = int(slots) if slots else default_slots(sum(self._numel))
+        P = sum(self._numel)
+        self.slots = int(slots) if slots else default_slots(P)
         if self.slots < 2:
             raise AggregationError("report-time aggregation needs at least 2 HBM slots")
         self.fold_batch = max(1, int(fold_batch))
         self.early_fold = bool(early_fold)
+        # saved fold states the speculation may hold in HBM (each P floats); < 2 turns it off
+        self.max_marks = int(min(MAX_MARKS, speculation_budget // max(4 * P, 1)))
+        can = all(hasattr(engine, f) for f in ("fold_slots_keep", "fold_mark", "fold_rewind", "fold_unmark"))
+        self.speculate = bool(can and self.max_marks >= 2 and (speculate is None or speculate))
+        self.mark_every = max(1, int(mark_every))
+        # speculative folds wait while the GPU is still busy with the previous one (reports arriving
+        # back to back would otherwise queue re-folds that the next report discards)
+        self._lazy = bool(lazy) and hasattr(engine, "fold_busy")
+        if speculate and not self.speculate:
+            raise AggregationError("speculative folds need an engine with fold marks and HBM for >= 2 of them "
+                                   f"({self.max_marks} fit in the budget)")
         self._seq = itertools.count()
         self._order: List[object] = []      # assigned workers, sorted by assignment key
         self._keys: List[tuple] = []        # their keys (sorted, parallel to _order)
         self._key_of: Dict[object, tuple] = {}
+        self._behind = set()                # assigned behind the freed fold prefix: never folded early
         self._reported = set()              # workers whose latest report we accepted
-        self._slot_of: Dict[object, int] = {}  # latest diff in HBM, not folded
+        self._slot_of: Dict[object, int] = {}  # latest diff in HBM (not folded, or folded and kept)
         self._parked: Dict[object, bytes] = {}  # latest diff on the host (no free slot yet)
         self._bad: Dict[object, str] = {}   # latest report unusable here (malformed / failed ingest)
         self._free: List[int] = list(range(self.slots - 1, -1, -1))
-        self._ready: List[object] = []      # position taken as certain, in HBM, not folded yet
-        self._front = 0                     # index into _order of the next position not yet certain
-        self._folded: List[object] = []     # folded early, in fold order
+        self._folded: List[object] = []     # in the running fold state, in fold order
         self._folded_set = set()
+        self._base = 0                      # _folded[:_base]: certain, slots freed, never re-folded
+        self._marks: List[tuple] = []       # (fold length, mark id), increasing; the base's first
+        self._mark_ids = itertools.count()
         self._stale: Optional[str] = None   # why the early fold no longer matches the reports
         self._weights_by_worker = weights_by_worker
         self._weights: List[float] = []     # fold order
         self.folded_early = 0
+        self.rewinds = 0
         self.last_close: dict = {}
         self._lock = threading.Lock()
         self._closed = False
@@ -127,6 +145,14 @@ class IncrementalCycle:
                 raise
             engine.ckpt_owner = self
             self._ckpt = checkpoint
+        # the new checkpoint's bytes, framed and faulted in while the cycle is open (the close then
+        # copies into resident pages: with speculative folds there is little fold left to hide that)
+        self._prepared = None
+        if checkpoint is not None and hasattr(engine, "ckpt_patch_into"):
+            try:
+                self._prepared = (checkpoint, state_codec.prepared_fresh_frame(checkpoint))
+            except StateParseError:
+                self._prepared = None
 
     # ---- assignment (cycle_manager.assign, fl_controller.py:131-132) ---------------------------
     def assigned(self, worker, key=None):
@@ -136,16 +162,16 @@ class IncrementalCycle:
             if worker in self._key_of or self._closed:
                 return
             k = (0, key) if key is not None else (1, next(self._seq))
-            self._key_of[worker] = k
             i = bisect.bisect_right(self._keys, k)
+            if self._base and i <= bisect.bisect_left(self._keys, self._key_of[self._folded[self._base - 1]]):
+                # behind the freed fold prefix: never folded early; if it reports, close's order
+                # check sees the early prefix is not the DB's prefix and re-folds
+                self._behind.add(worker)
+            self._key_of[worker] = k
             self._keys.insert(i, k)
             self._order.insert(i, worker)
-            if i < self._front:
-                # behind the fold front: never folded early; if it reports, close's order check
-                # sees the early prefix is not the DB's prefix and re-folds
-                self._front += 1
-            elif i == self._front and worker in self._reported and self.early_fold:
-                self._advance()
+            if worker in self._reported:  # it reported before we heard of it (e.g. a restart)
+                self._sync()
 
     # ---- report (fl_events.py:257-261 -> submit_worker_diff, cycle_manager.py:151-178) ---------
     def reported(self, worker, diff: bytes):
@@ -162,10 +188,12 @@ class IncrementalCycle:
                 # refused to its sender now, not when a later report folds it
                 raise AggregationError(f"worker {worker!r} reported but has no aggregation weight")
             if worker in self._folded_set:
-                # its earlier diff is in the fold state already: the DB now holds another one
-                self._stale = f"worker {worker!r} re-reported after its diff was folded"
-                self._reported.add(worker)
-                return
+                # its earlier diff is in the fold state: go back to before it (its slot is still
+                # held), or -- when it was folded for good -- the close re-folds from the DB
+                if not self._rewind(self._folded.index(worker)):
+                    self._stale = f"worker {worker!r} re-reported after its diff was folded"
+                    self._reported.add(worker)
+                    return
             try:
                 self._take(worker, diff)
             except StateParseError:
@@ -177,20 +205,19 @@ class IncrementalCycle:
                     self._reported.add(worker)
                     return
                 self._forget(worker, "malformed diff")
+                self._sync()
                 raise
             self._reported.add(worker)
             self._bad.pop(worker, None)
-            if self.early_fold:
-                self._advance()
+            self._sync()
 
     def _take(self, worker, diff: bytes):
         """Store ``diff`` as the worker's latest: over its old slot, in a free slot, or parked."""
         if worker in self._slot_of:  # re-report before the fold: same slot (parse first, then DMA)
             self.engine.ingest_state(self._slot_of[worker], diff)
             return
-        front = self._is_front(worker)
         # a diff that cannot fold yet leaves one slot free for the fold front
-        if self._free and (front or len(self._free) > 1):
+        if self._free and (len(self._free) > 1 or self._is_front(worker)):
             self._to_hbm(worker, diff)  # raises StateParseError on a malformed diff: nothing recorded
             self._parked.pop(worker, None)
         else:
@@ -202,17 +229,18 @@ class IncrementalCycle:
         slot = self._slot_of.pop(worker, None)
         if slot is not None:
             self._free.append(slot)
-        if worker in self._ready:
-            # the positions from this worker on are no longer certain: the front goes back to it
-            j = self._ready.index(worker)
-            self._front -= len(self._ready) - j
-            self._ready = self._ready[:j]
         self._parked.pop(worker, None)
         self._reported.discard(worker)
         self._bad[worker] = why
 
     def _is_front(self, worker) -> bool:
-        return self._front < len(self._order) and self._order[self._front] == worker
+        """``worker`` is the first assigned worker whose diff is neither folded nor in HBM (the one
+        the fold waits for)."""
+        for w in self._order:
+            if w in self._folded_set or w in self._slot_of or w in self._behind:
+                continue
+            return w == worker
+        return False
 
     def _check_layout(self, worker, diff: bytes):
         got = tuple(state_codec.tensor_numels(diff))
@@ -232,48 +260,146 @@ class IncrementalCycle:
         return worker in self._slot_of or worker in self._parked
 
     # ---- early folds ---------------------------------------------------------------------------
-    def _fold(self, ws: Sequence, final: bool):
-        slots = [self._slot_of.pop(w) for w in ws]
-        if self.mode == WEIGHTED_MEAN and self._weights_by_worker is not None and (ws or final):
+    def _plan(self):
+        """The reporters in the order the close will fold them, as far as known now (assignment
+        order, non-reporters skipped), and how many of them are certain: those before the first
+        assigned worker that has not reported (a later report can only land behind that point)."""
+        plan, certain = [], None
+        for w in self._order:
+            if w in self._behind:
+                continue
+            if w in self._reported:
+                plan.append(w)
+            elif certain is None:
+                certain = len(plan)
+        return plan, len(plan) if certain is None else certain
+
+    def _sync(self):
+        """Bring the fold state up to date with the reports: go back to before the first position
+        that changed, then fold what follows -- every reported diff in HBM when speculating (folded
+        and kept, a mark after each fold), else only the certain ones, ``fold_batch`` at a time
+        (folded and freed).  Slots of certain positions before a mark are freed."""
+        if self._stale or self._declined or self._closed or not self.early_fold:
+            return
+        plan, certain = self._plan()
+        target = plan if self.speculate else plan[:certain]
+        common = _common_prefix(self._folded, target)
+        if common < len(self._folded) and not self._rewind(common):
+            return  # the early fold is not the plan's prefix any more: the close re-folds
+        if self.speculate and self._lazy and not self._parked and self.engine.fold_busy():
+            return  # the GPU is still folding: fold this report with a later one (or at close)
+        run: List = []
+        for w in target[len(self._folded):]:
+            if w not in self._slot_of:
+                if w not in self._parked:
+                    break
+                if not self._free and run and not self.speculate:
+                    self._fold_run(run)  # frees their slots for the parked diff
+                    run = []
+                if not (len(self._free) > 1 or self._free and self._is_front(w)):
+                    break  # the last free slot is the fold front's
+                try:
+                    self._to_hbm(w, self._parked[w])
+                except Exception as e:  # noqa: BLE001 -- not this caller's report (ADVICE r2)
+                    log.warning("parked diff of worker %r failed to ingest: %s", w, e)
+                    self._forget(w, f"ingest failed: {e}")
+                    break
+                del self._parked[w]
+            run.append(w)
+        if run and (self.speculate or len(run) >= self.fold_batch):
+            self._fold_run(run, certain)
+        if self.speculate:
+            self._advance_base(certain)
+
+    def _fold_run(self, ws: Sequence, certain: int = 0):
+        slots = [self._slot_of[w] for w in ws]
+        if self.mode == WEIGHTED_MEAN and self._weights_by_worker is not None:
             self._weights.extend(float(self._weights_by_worker[w]) for w in ws)
-            if self._weights:
-                self.engine.set_weights(self._weights)
-        if final:
-            self.engine.fold_slots_finish_resident(self.mode, slots)
+            self.engine.set_weights(self._weights)
+        if self.speculate:
+            # a saved state at least every `mark_every` rows (a later rewind goes back no further
+            # than that before the position that changed) and one exactly at the certain point,
+            # so that the certain diffs' slots are freed at once
+            n0 = len(self._folded)
+            cuts = sorted({*range(self.mark_every, len(ws), self.mark_every), len(ws)} |
+                          ({certain - n0} if 0 < certain - n0 < len(ws) else set()))
+            i = 0
+            for j in cuts:
+                self.engine.fold_slots_keep(self.mode, slots[i:j])
+                self._folded.extend(ws[i:j])
+                self._folded_set.update(ws[i:j])
+                self._mark()
+                self._advance_base(certain)
+                i = j
+            self.folded_early = len(self._folded)
+            return
         else:
             self.engine.fold_slots(self.mode, slots)
-        self._free.extend(reversed(slots))
-        return slots
-
-    def _fold_ready(self):
-        ws, self._ready = self._ready, []
-        self._fold(ws, final=False)
+            for w in ws:
+                del self._slot_of[w]
+            self._free.extend(reversed(slots))
         self._folded.extend(ws)
         self._folded_set.update(ws)
-        self.folded_early += len(ws)
+        self.folded_early = len(self._folded)
+        self._base = len(self._folded)
 
-    def _advance(self):
-        while self._front < len(self._order):
-            w = self._order[self._front]
-            if w in self._reported and self._held(w):
-                if w in self._parked:  # its turn: it needs a slot now
-                    if not self._free:
-                        if not self._ready:
-                            break  # (cannot happen: one slot is kept for the front)
-                        self._fold_ready()
-                    try:
-                        self._to_hbm(w, self._parked[w])
-                    except Exception as e:  # noqa: BLE001 -- not this caller's report
-                        log.warning("parked diff of worker %r failed to ingest: %s", w, e)
-                        self._forget(w, f"ingest failed: {e}")
-                        break
-                    del self._parked[w]
-                self._ready.append(w)
-            else:
-                break  # an earlier worker may still report: later positions are not certain yet
-            self._front += 1
-            if len(self._ready) >= self.fold_batch:
-                self._fold_ready()
+    def _mark(self):
+        n = len(self._folded)
+        if len(self._marks) >= self.max_marks:
+            # first drop the mark whose neighbours are closest (the base's stays), so that at most
+            # max_marks states are ever held
+            at = [m[0] for m in self._marks] + [n]
+            i = min(range(1, len(self._marks)), key=lambda j: at[j + 1] - at[j - 1])
+            self.engine.fold_unmark(self._marks.pop(i)[1])
+        mid = next(self._mark_ids)
+        self.engine.fold_mark(mid)
+        self._marks.append((n, mid))
+
+    def _advance_base(self, certain: int):
+        """Positions before ``certain`` never change again: free their slots up to the last mark
+        there, which becomes the base (the earliest point a rewind may go back to)."""
+        cert = min(certain, len(self._folded))
+        at = [i for i, (n, _) in enumerate(self._marks) if n <= cert]
+        if not at or self._marks[at[-1]][0] <= self._base:
+            return
+        i = at[-1]
+        new_base = self._marks[i][0]
+        for w in self._folded[self._base:new_base]:
+            slot = self._slot_of.pop(w, None)
+            if slot is not None:
+                self._free.append(slot)
+        for _, mid in self._marks[:i]:
+            self.engine.fold_unmark(mid)
+        del self._marks[:i]
+        self._base = new_base
+
+    def _rewind(self, n: int) -> bool:
+        """Go back to a fold state of at most ``n`` folded diffs (the latest saved one); False when
+        that would need diffs whose slots were freed."""
+        if n >= len(self._folded):
+            return True
+        if n < self._base:
+            return False
+        keep = [m for m in self._marks if m[0] <= n]
+        to = keep[-1][0] if keep else 0
+        if keep:
+            self.engine.fold_rewind(keep[-1][1])
+        else:  # before the first mark: the base is 0 (a mark is the base otherwise)
+            self.engine.fold_restart()
+        for _, mid in self._marks[len(keep):]:
+            self.engine.fold_unmark(mid)
+        del self._marks[len(keep):]
+        del self._folded[to:]
+        self._folded_set = set(self._folded)
+        del self._weights[to:]
+        self.folded_early = len(self._folded)
+        self.rewinds += 1
+        return True
+
+    def _drop_marks(self):
+        for _, mid in self._marks:
+            self.engine.fold_unmark(mid)
+        self._marks = []
 
     # ---- close (cycle_manager.py:217 -> _average_plan_diffs :240-303) ---------------------------
     def close(self, checkpoint: bytes, framing: str = "fresh", order: Optional[Sequence[Hashable]] = None,
@@ -303,13 +429,15 @@ class IncrementalCycle:
                 raise AggregationError("the completed-WorkerCycle order lists a worker twice")
             if not order:
                 raise AggregationError("no diffs to average")
-            k = len(self._folded)
-            refold = self._stale or (order[:k] != self._folded and
-                                     f"the DB order's first {k} workers are not the {k} folded early")
             if self._weights_by_worker is not None:
                 missing = [w for w in order if w not in self._weights_by_worker]
                 if missing:
                     raise AggregationError(f"workers {missing[:8]!r} have no aggregation weight")
+            folded_before = len(self._folded)
+            refold = self._stale
+            if not refold and not self._rewind(_common_prefix(self._folded, order)):
+                refold = f"the DB order's first {len(self._folded)} workers are not the ones folded early"
+            k = 0 if refold else len(self._folded)
             rest = order if refold else order[k:]
             if fetch is None:
                 unheld = [w for w in rest if not self._held(w)]
@@ -326,14 +454,31 @@ class IncrementalCycle:
                 log.info("re-folding the cycle in the DB's order: %s", refold)
                 self.engine.fold_restart()
                 self._weights = []
+            self._drop_marks()
             stats = self._fold_in_order(rest, fetch)
-            stats.update(refold=bool(refold), reason=refold or None, early=0 if refold else k, n=len(order))
+            stats.update(refold=bool(refold), reason=refold or None, early=k, n=len(order),
+                         folded_before_close=folded_before, rewinds=self.rewinds)
             self.last_close = stats
-            new = (state_codec.fresh_checkpoint(self.engine, checkpoint) if framing == "fresh"
+            prep = self._prepared[1] if self._prepared and self._prepared[0] is checkpoint else None
+            self._prepared = None
+            new = (state_codec.fresh_checkpoint(self.engine, checkpoint, prepared=prep) if framing == "fresh"
                    else self.engine.ckpt_patch_state(checkpoint))
             self.engine.ckpt_owner = self
             self.engine.ckpt_bytes = new
             return new
+
+    def _fold(self, ws: Sequence, final: bool):
+        slots = [self._slot_of.pop(w) for w in ws]
+        if self.mode == WEIGHTED_MEAN and self._weights_by_worker is not None and (ws or final):
+            self._weights.extend(float(self._weights_by_worker[w]) for w in ws)
+            if self._weights:
+                self.engine.set_weights(self._weights)
+        if final:
+            self.engine.fold_slots_finish_resident(self.mode, slots)
+        else:
+            self.engine.fold_slots(self.mode, slots)
+        self._free.extend(reversed(slots))
+        return slots
 
     def _fold_in_order(self, rest: List, fetch) -> dict:
         """Fold ``rest`` in order and finish into the resident checkpoint, within the slot budget:
@@ -342,9 +487,8 @@ class IncrementalCycle:
         later worker's diff -- the slot of the worker needed LAST is given up (its diff is fetched
         from the DB when its turn comes)."""
         pos = {w: i for i, w in enumerate(rest)}
-        for w in [w for w in self._slot_of if w not in pos]:  # held, but not in the DB's order
+        for w in [w for w in self._slot_of if w not in pos]:  # held (or folded and kept), not needed
             self._free.append(self._slot_of.pop(w))
-        self._ready = []
         batch: List = []
         from_hbm = from_host = from_db = 0
         for i, w in enumerate(rest):
@@ -382,6 +526,7 @@ class IncrementalCycle:
             self._closed = True
             self._slot_of.clear()
             self._parked.clear()
+            self._marks = []
             if getattr(self.engine, "ckpt_owner", None) is self:
                 self.engine.ckpt_owner = None
 
@@ -404,6 +549,14 @@ class IncrementalCycle:
     def n_parked(self) -> int:
         """Reported diffs waiting on the host because every HBM slot was taken."""
         return len(self._parked)
+
+
+def _common_prefix(a: Sequence, b: Sequence) -> int:
+    n = min(len(a), len(b))
+    i = 0
+    while i < n and a[i] == b[i]:
+        i += 1
+    return i
 
 
 def _raise_if_not_float32(pb: bytes, what: str):

@@ -90,7 +90,7 @@ class NodeEngine:
                  report_time: bool = True, close_trigger: str = "reference", deadline: bool = False,
                  keep_checkpoints: int = 4, slots: Optional[int] = None, fold_batch: int = 8,
                  mean_plans: Optional[str] = None, framing: str = "fresh", report_module=None,
-                 pinned_reports: int = 16):
+                 pinned_reports: int = 16, speculate: Optional[bool] = None):
         if close_trigger not in ("reference", "replay"):
             raise AggregationError(f"close_trigger must be 'reference' or 'replay', not {close_trigger!r}")
         if deadline and close_trigger != "replay":
@@ -107,6 +107,7 @@ class NodeEngine:
         self.deadline = deadline
         self.slots = slots
         self.fold_batch = fold_batch
+        self.speculate = speculate
         self.framing = framing
         self.store = CheckpointStore(keep=keep_checkpoints) if keep_checkpoints else None
         self.report_module = report_module
@@ -123,7 +124,7 @@ class NodeEngine:
         self._hold = threading.local()
         self._patched: list = []
         self.stats = {"closes_report_time": 0, "closes_close_time": 0, "closes_declined": 0, "refolds": 0,
-                      "diffs_from_db": 0, "report_errors": 0}
+                      "diffs_from_db": 0, "report_errors": 0, "rewinds": 0}
 
     # ---- patching ------------------------------------------------------------------------------
     def _patch(self, owner, name, value):
@@ -266,7 +267,7 @@ class NodeEngine:
                            shapes=lambda: _shapes(ckpt))
         self.aggregator._resident = None  # the report-time cycle takes over the engine's slab
         inc = IncrementalCycle(self.engine, numel, mode=mode, slots=self.slots, fold_batch=self.fold_batch,
-                               checkpoint=ckpt)
+                               checkpoint=ckpt, speculate=self.speculate)
         for row in _rows(cm, cycle_id=cycle.id):  # after a restart: the rows assigned before it
             inc.assigned(row.id, key=row.id)
         return inc
@@ -343,6 +344,7 @@ class NodeEngine:
             self.stats["closes_report_time"] += 1
             self.stats["refolds"] += int(st.last_close.get("refold", False))
             self.stats["diffs_from_db"] += st.last_close.get("from_db", 0)
+            self.stats["rewinds"] += st.last_close.get("rewinds", 0)
             self.aggregator._resident = None
             finish_cycle(cm, server_config, cycle, self.model_manager, model.id, new)
 

@@ -113,12 +113,23 @@ def fresh_frame_bytes(template: bytes, ids=None):
     return out, ptr
 
 
-def fresh_checkpoint(engine, template: bytes, ids=None) -> bytes:
+def prepared_fresh_frame(template: bytes, ids=None):
+    """``fresh_frame_bytes`` with the payload pages already faulted in (``pgh_host_prefault``): made
+    while a cycle is still open, so the close copies the new checkpoint into resident pages instead
+    of faulting ~11 K of them in while the D2H waits."""
+    out, ptr = fresh_frame_bytes(template, ids)
+    if ptr:
+        _lib.load().pgh_host_prefault(C.c_void_p(ptr), len(out))
+    return out, ptr
+
+
+def fresh_checkpoint(engine, template: bytes, ids=None, prepared=None) -> bytes:
     """The new checkpoint as ``serialize_model_params`` emits it (model_manager.py:79-92): a fresh
     State whose framing ``pgh_state_fresh`` builds from the template's tensor shapes and fresh ids
     (restated in ``state_schema.fresh_frame``) and whose payloads the engine writes in place from
-    the resident checkpoint in HBM (``pgh_ckpt_patch_state`` with out == tmpl)."""
-    out, ptr = fresh_frame_bytes(template, ids)
+    the resident checkpoint in HBM (``pgh_ckpt_patch_state`` with out == tmpl).  ``prepared``: a
+    ``prepared_fresh_frame(template)`` not handed out yet."""
+    out, ptr = prepared if prepared is not None else fresh_frame_bytes(template, ids)
     engine.ckpt_patch_into(ptr, len(out))
     return out
 

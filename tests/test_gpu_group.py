@@ -159,9 +159,10 @@ def test_group_subrange_and_stream(group2):
     assert np.array_equal(bits(got), bits(want))
 
 
-def test_group_report_time_cycle(group2):
+@pytest.mark.parametrize("speculate", [False, True])
+def test_group_report_time_cycle(group2, speculate):
     """IncrementalCycle over a group: shuffled reports with dropouts, folded through the row table
-    on every GPU."""
+    on every GPU (speculative folds: marks and rewinds fanned out to every child)."""
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast, parse_state
 
@@ -172,7 +173,8 @@ def test_group_report_time_cycle(group2):
     diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in reporters}
     ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
     ck_pb = build_state_fast(ckpt)
-    inc = IncrementalCycle(group2, [int(np.prod(s)) for s in shapes], slots=16, fold_batch=3, checkpoint=ck_pb)
+    inc = IncrementalCycle(group2, [int(np.prod(s)) for s in shapes], slots=16, fold_batch=3, checkpoint=ck_pb,
+                           speculate=speculate, mark_every=2)
     for w in range(n):
         inc.assigned(w)
     for w in rng.permutation(reporters):

@@ -36,8 +36,9 @@ def _check(new_pb, ckpt, rows, mode, weights=None):
         assert np.array_equal(bits(g), bits(w))
 
 
+@pytest.mark.parametrize("speculate", [False, True])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_re_reports_before_and_after_the_fold(engine, mode):
+def test_re_reports_before_and_after_the_fold(engine, mode, speculate):
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast
 
@@ -49,7 +50,8 @@ def test_re_reports_before_and_after_the_fold(engine, mode):
     ck = build_state_fast(ckpt)
     wts = {w: float(rng.uniform(0.5, 2)) for w in workers}
     inc = IncrementalCycle(engine, [int(np.prod(s)) for s in SHAPES], mode=mode, slots=4, fold_batch=1,
-                           weights_by_worker=wts if mode == 2 else None, checkpoint=ck)
+                           weights_by_worker=wts if mode == 2 else None, checkpoint=ck, speculate=speculate,
+                           lazy=False)
     for w in workers:
         inc.assigned(w, key=w)
     latest = {}
@@ -122,12 +124,15 @@ def test_node_wiring_on_the_gpu_matches_the_reference_node():
             node = pnode.install(mod, engine=eng, **opts) if installed else None
             proc, model, _ = host_process(mod, cfg, ck)
             keys = {}
+            closes = refolds = 0  # summed over the node objects a restart replaces
             for op in script:
                 if op[0] == "a":
                     keys[op[1]] = assign(mod, op[1], proc)
                 elif op[0] == "r":
                     mod.cycle_manager.submit_worker_diff(op[1], keys[op[1]], pb[(op[1], op[2])])
                 elif installed:
+                    closes += node.stats["closes_report_time"]
+                    refolds += node.stats["refolds"]
                     node.uninstall()
                     eng.reset()
                     eng.ckpt_owner = None  # a restarted process has nothing in HBM
@@ -135,6 +140,8 @@ def test_node_wiring_on_the_gpu_matches_the_reference_node():
             assert mod.cycle_manager.task_errors == []
             out.append([r.value for r in sorted(mod.model_manager._model_checkpoints.rows, key=lambda r: r.id)])
             if node:
-                assert node.stats["closes_report_time"] == 3 and node.stats["refolds"] >= 1
+                closes += node.stats["closes_report_time"]
+                refolds += node.stats["refolds"]
+                assert closes == 3 and refolds >= 1
                 node.uninstall()
     assert len(out[0]) == 4 and out[0] == out[1]

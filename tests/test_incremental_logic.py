@@ -497,3 +497,209 @@ def test_float64_checkpoint_declined_at_cycle_start():
 
     with pytest.raises(ModelNotAcceleratedError):
         IncrementalCycle(ScanningEngine(), [3], slots=4, checkpoint=_f64_diff())
+
+
+# ---- speculative folds (pgh_fold_slots_keep / pgh_fold_mark / pgh_fold_rewind) ----------------------
+
+class SpecEngine(RecordingEngine):
+    """RecordingEngine with the library's saved fold states: `state` is the running fold state as a
+    payload list; a kept fold appends the slots' current payloads without freeing them."""
+
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self.state = []
+        self.marks = {}
+        self.kept_rows = 0
+        self.max_marks_held = 0
+
+    def fold_slots(self, mode, slots):
+        self.state += [self.slot[s] for s in slots]
+        super().fold_slots(mode, slots)
+
+    def fold_slots_keep(self, mode, slots):
+        assert len(set(slots)) == len(slots) and all(s in self.slot for s in slots)
+        self.state += [self.slot[s] for s in slots]
+        self.kept_rows += len(slots)
+        self.calls.append(("keep", len(slots)))
+
+    def fold_mark(self, m):
+        self.marks[m] = list(self.state)
+        self.max_marks_held = max(self.max_marks_held, len(self.marks))
+
+    def fold_rewind(self, m):
+        self.state = list(self.marks[m])
+        self.calls.append(("rewind", len(self.state)))
+
+    def fold_unmark(self, m):
+        del self.marks[m]
+
+    def fold_restart(self):
+        self.state = []
+        super().fold_restart()
+
+    def fold_slots_finish_resident(self, mode, slots):
+        self.final_rows = len(slots)
+        self.state += [self.slot[s] for s in slots]
+        self.result = list(self.state)
+        self.state = []
+        super().fold_slots_finish_resident(mode, slots)
+
+
+def test_speculation_folds_every_report_and_closes_with_nothing_left():
+    """Worker 0 never reports, so nothing is ever certain; every reported diff is folded as it
+    arrives anyway (in assignment order), rewound when an earlier worker reports after it, and the
+    close only finishes: no rows left to fold."""
+    rng = np.random.default_rng(11)
+    eng = SpecEngine()
+    n = 40
+    inc = IncrementalCycle(eng, [3], slots=n, fold_batch=8)
+    assert inc.speculate
+    for w in range(n):
+        inc.assigned(w)
+    reporters = [w for w in range(1, n) if rng.random() >= 0.2]
+    seen = []
+    for w in rng.permutation(reporters):
+        inc.reported(int(w), bytes([int(w)]))
+        seen.append(int(w))
+        assert eng.state == [bytes([x]) for x in sorted(seen)]  # the fold state is the plan so far
+    assert eng.marks and any(c[0] == "rewind" for c in eng.calls)
+    inc.close(b"ck", framing="template")
+    assert eng.result == [bytes([w]) for w in sorted(reporters)]
+    assert eng.final_rows == 0 and inc.last_close["early"] == len(reporters) and not inc.last_close["refold"]
+    assert eng.marks == {}  # every saved state released at close
+
+
+def test_speculation_frees_certain_slots_and_rewinds_only_after_the_base():
+    eng = SpecEngine()
+    inc = IncrementalCycle(eng, [3], slots=6)
+    for w in "abcdefgh":
+        inc.assigned(w)
+    for w in "abd":            # a, b certain; d speculative (c outstanding)
+        inc.reported(w, w.encode())
+    assert eng.state == [b"a", b"b", b"d"] and inc._base == 2 and len(inc._free) == 6 - 1
+    inc.reported("c", b"c")    # lands before d: back to the mark after b, refold c, d
+    assert eng.state == [b"a", b"b", b"c", b"d"] and eng.calls[-2][0] == "rewind" or ("rewind", 2) in eng.calls
+    assert inc._base == 4 and len(inc._free) == 6
+    inc.reported("b", b"b2")   # re-report of a certain (freed) diff: the close re-folds from the DB
+    assert inc.stale
+    db = {"a": b"a", "b": b"b2", "c": b"c", "d": b"d"}
+    inc.close(b"ck", framing="template", order=list("abcd"), fetch=db.__getitem__)
+    assert eng.result == [b"a", b"b2", b"c", b"d"] and inc.last_close["refold"]
+
+
+def test_speculative_re_report_rewinds_and_folds_the_latest_diff():
+    eng = SpecEngine()
+    inc = IncrementalCycle(eng, [3], slots=8)
+    for w in range(6):
+        inc.assigned(w)
+    for w, v in ((2, b"2a"), (4, b"4a"), (3, b"3a"), (4, b"4b"), (2, b"2b")):
+        inc.reported(w, v)
+    assert eng.state == [b"2b", b"3a", b"4b"]  # worker 0 outstanding: all speculative, kept
+    inc.reported(0, b"0")
+    inc.close(b"ck", framing="template", order=[0, 2, 3, 4], fetch=None)
+    assert eng.result == [b"0", b"2b", b"3a", b"4b"] and not inc.last_close["refold"]
+
+
+def test_close_rewinds_to_the_db_order():
+    """The DB returns another order than assignment: the close goes back to the last saved state
+    inside the common prefix and folds the rest from the kept slots -- no DB reads."""
+    eng = SpecEngine()
+    inc = IncrementalCycle(eng, [3], slots=8, mark_every=1)
+    for w in range(6):
+        inc.assigned(w)
+    for w in (5, 1, 2, 4):
+        inc.reported(w, bytes([w]))
+    assert eng.state == [bytes([w]) for w in (1, 2, 4, 5)]
+    inc.close(b"ck", framing="template", order=[1, 2, 5, 4], fetch=lambda w: pytest.fail("DB read"))
+    assert eng.result == [bytes([w]) for w in (1, 2, 5, 4)]
+    assert inc.last_close["early"] == 2 and inc.last_close["from_hbm"] == 2 and not inc.last_close["refold"]
+
+
+def test_mark_budget_thins_saved_states():
+    rng = np.random.default_rng(12)
+    eng = SpecEngine()
+    n = 60
+    inc = IncrementalCycle(eng, [1000], slots=n, speculation_budget=5 * 4000)
+    assert inc.max_marks == 5
+    for w in range(n):
+        inc.assigned(w)
+    reporters = [w for w in range(1, n) if rng.random() >= 0.2]
+    for w in rng.permutation(reporters):
+        inc.reported(int(w), bytes([int(w)]))
+    assert eng.max_marks_held <= 5
+    inc.close(b"ck", framing="template")
+    assert eng.result == [bytes([w]) for w in sorted(reporters)]
+
+
+def test_no_speculation_without_budget():
+    assert not IncrementalCycle(SpecEngine(), [1000], slots=4, speculation_budget=4000).speculate
+    assert not IncrementalCycle(SpecEngine(), [10], slots=4, speculate=False).speculate
+    with pytest.raises(AggregationError):
+        IncrementalCycle(RecordingEngine(), [10], slots=4, speculate=True)
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_randomised_speculation_matches_the_reference_order(seed):
+    """Random scripts -- assignments (some announced behind the fold), shuffled reports, re-reports,
+    malformed re-reports, parked diffs under slot pressure, thinned marks, random DB orders -- fold
+    exactly the DB order's latest diffs, and speculation rewinds instead of reading the DB whenever
+    the order was the assignment order."""
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(3, 30))
+    slots = int(rng.integers(2, n + 3))
+    eng = SpecEngine(fail_on=b"bad")
+    inc = IncrementalCycle(eng, [3], slots=slots, fold_batch=int(rng.integers(1, 4)),
+                           speculation_budget=int(rng.integers(2, 12)) * 12)
+    late = set(int(x) for x in rng.choice(n, size=int(rng.integers(0, n // 3 + 1)), replace=False))
+    for w in range(n):
+        if w not in late:
+            inc.assigned(w, key=w)
+    db = {}
+    events = [("r", int(w)) for w in rng.permutation(n) if rng.random() >= 0.25]
+    events += [("r", int(w)) for w in rng.choice(n, size=int(rng.integers(0, 6)))]   # re-reports
+    events += [("a", w) for w in late]
+    rng.shuffle(events)
+    version = {}
+    for kind, w in events:
+        if kind == "a":
+            inc.assigned(w, key=w)
+            continue
+        version[w] = version.get(w, 0) + 1
+        if rng.random() < 0.05:
+            db[w] = b"bad"
+            with pytest.raises(StateParseError):
+                inc.reported(w, b"bad")
+        else:
+            db[w] = mk(100 * version[w] + w)
+            inc.reported(w, db[w])
+    order = sorted(db)
+    if not order:
+        return
+    if rng.random() < 0.3:
+        order = [order[i] for i in rng.permutation(len(order))]
+    if any(db[w] == b"bad" for w in order):
+        with pytest.raises(StateParseError):
+            inc.close(b"ck", framing="template", order=order, fetch=db.__getitem__)
+        return
+    inc.close(b"ck", framing="template", order=order, fetch=db.__getitem__)
+    assert eng.result == [db[w] for w in order]
+
+
+@pytest.mark.parametrize("slots", [2, 3, 5])
+@pytest.mark.parametrize("seed", range(8))
+def test_speculation_under_slot_pressure_closes_without_the_db(slots, seed):
+    """Few slots: speculative folds keep their slots, so the reserved slot of the fold front must
+    still come free (a mark at the certain point frees the certain diffs) -- every diff stays in
+    HBM or on the host and the close needs no DB read."""
+    rng = np.random.default_rng(50 + seed)
+    eng = SpecEngine()
+    n = 24
+    inc = IncrementalCycle(eng, [3], slots=slots, fold_batch=2, mark_every=3)
+    for w in range(n):
+        inc.assigned(w)
+    reporters = [w for w in range(n) if w % 5 != 3]
+    for w in rng.permutation(reporters):
+        inc.reported(int(w), mk(int(w)))
+        assert len([s for s in eng.slot]) <= slots
+    inc.close(b"ck", framing="template")
+    assert eng.result == [mk(w) for w in reporters]

@@ -213,10 +213,13 @@ def test_malformed_diff_fails_the_close_like_the_reference():
     assert errs == [1, 1]
 
 
-def test_randomised_report_sequences():
-    """Random assignment / report / re-report / late-report / restart scripts, random DB orders."""
-    totals = {"closes_report_time": 0, "refolds": 0, "diffs_from_db": 0}
-    for trial in range(25):
+@pytest.mark.parametrize("speculate", [True, False])
+def test_randomised_report_sequences(speculate):
+    """Random assignment / report / re-report / late-report / restart scripts, random DB orders;
+    with speculative folds (every reported diff folded at once, rewound when an earlier worker
+    reports) and with certain-only folds."""
+    totals = {"closes_report_time": 0, "refolds": 0, "diffs_from_db": 0, "rewinds": 0}
+    for trial in range(40):
         rng = np.random.default_rng(100 + trial)
         n = int(rng.integers(3, 9))
         need = int(rng.integers(1, n + 1))
@@ -247,14 +250,15 @@ def test_randomised_report_sequences():
         res = []
         for installed in (False, True):
             sc = Scenario(cfg, installed, row_order=(lambda r: r[::-1]) if reverse else None,
-                          **({"fold_batch": fb, "slots": slots} if installed else {}))
+                          **({"fold_batch": fb, "slots": slots, "speculate": speculate} if installed else {}))
             script(sc)
             res.append(sc.checkpoints())
         assert len(res[0]) >= 2 and res[0] == res[1], trial
         for k in totals:
             totals[k] += sc.node.stats[k]
     # the scripts did exercise every path
-    assert totals["closes_report_time"] >= 25 and totals["refolds"] >= 3 and totals["diffs_from_db"] >= 3, totals
+    assert totals["closes_report_time"] >= 40 and totals["refolds"] >= 3 and totals["diffs_from_db"] >= 3, totals
+    assert (totals["rewinds"] >= 10) if speculate else (totals["rewinds"] == 0), totals
 
 
 def test_checkpoint_cache_serves_get_model_and_stays_bounded():
