@@ -207,7 +207,7 @@ def wants_group_line(args) -> bool:
     return args.gpus > 1 and not args.group and not args.no_group_line and args.workload in GROUP_WORKLOADS
 
 
-def group_line(args, limit_s: int = 420) -> dict:
+def group_line(args, limit_s: int = 300) -> dict:
     """The path the node deploys at N > 1 (its single process drives every GPU through one library
     context, ``pgh_create_group``), measured on the same GPUs right after
     the per-rank world has exited: ``bench.py --group --gpus N`` in a FRESH child (no process that
