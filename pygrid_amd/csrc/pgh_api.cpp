@@ -706,11 +706,23 @@ void prefault_small_any(uint8_t* p, size_t n) {
 // The same for a big fresh destination, split over the copy pool's threads: run while the fold
 // and the first D2H are still in flight, so the copy-out afterwards writes to resident pages
 // instead of taking a page fault per 4 KiB (PGH_PREFAULT=0 turns it off).
+// Every page of [a, b) is already in memory (an output framed and faulted in beforehand,
+// pgh_host_prefault): one mincore call, far cheaper than MADV_POPULATE_WRITE walking the same
+// present pages again (≈1.6 ms for 47 MB, tools/patch_probe.py, profiles/r03l/).
+bool all_resident(uintptr_t a, uintptr_t b, uintptr_t page) {
+    std::vector<unsigned char> v((size_t)((b - a) / page));
+    if (v.empty() || mincore((void*)a, b - a, v.data()) != 0) return false;
+    for (unsigned char x : v)
+        if (!(x & 1)) return false;
+    return true;
+}
+
 void prefault_parallel(uint8_t* p, size_t n, CopyPool& pool) {
     if (!p || n == 0) return;
     if (n < (4u << 20)) { prefault_small(p, n); return; }
     static const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
     const uintptr_t a = (uintptr_t)p & ~(page - 1), b = ((uintptr_t)p + n + page - 1) & ~(page - 1);
+    if (all_resident(a, b, page)) return;
     // PGH_THP=1: the 2 MiB-aligned interior on transparent huge pages.  Off by default: this
     // populate already runs beside the fold and the first D2H, and the report-time close measured
     // the same either way (2.0-2.3 vs 2.1-2.3 ms medians, profiles/r02ad/).

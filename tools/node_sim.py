@@ -6,13 +6,16 @@ an HBM slot), and the close when the cycle ends (cycle_manager.py:217).  ResNet-
 assigned per cycle, ~20 % never report (routes.py:314), shuffled arrival, several cycles chained
 through the resident checkpoint.
 
-    python tools/node_sim.py [cycles] [--pinned] [--tune] [--phases]
+    python tools/node_sim.py [cycles] [--pinned] [--tune] [--phases] [--no-speculate] [--close-gap-ms=50]
 
 Prints one JSON line: per-report handler latency (decode, ingest, total: p50 / p99 / max), the host
 bytes copied into the library's staging ring per report, and the close latency per cycle.
 ``--pinned``: the report is decoded into a page-locked block (``report.PinnedPool``) and DMA'd as
 it lies.  ``--tune``: ``pygrid_amd.tune_process()`` first (glibc thresholds;
-the engine's own share of the close is the untuned run).
+the engine's own share of the close is the untuned run).  ``--no-speculate``: fold only certain
+positions early.  ``--close-gap-ms``: pause between the last report and the close (0: at once, as
+when the report that reaches ``max_diffs`` triggers ``complete_cycle``; 50 by default, a
+``cycle.end`` close).
 """
 import base64
 import json
@@ -37,6 +40,8 @@ def pct(xs, q):
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     cycles = int(args[0]) if args else 4
+    speculate = False if "--no-speculate" in sys.argv else None
+    gap_ms = next((float(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--close-gap-ms=")), 50.0)
     tuned = None
     if "--tune" in sys.argv:
         import pygrid_amd
@@ -77,7 +82,7 @@ def main():
     for cyc in range(cycles + 1):  # cycle 0 warms up
         n = 100
         reporters = [w for w in range(n) if rng.random() >= 0.2]
-        inc = IncrementalCycle(eng, numel, slots=n, fold_batch=8, checkpoint=ckpt)
+        inc = IncrementalCycle(eng, numel, slots=n, fold_batch=8, checkpoint=ckpt, speculate=speculate)
         for w in range(n):
             inc.assigned(w)
         for w in rng.permutation(reporters):
@@ -93,7 +98,8 @@ def main():
                 ing.append((t2 - t1) * 1e3)
                 tot.append((t2 - t0) * 1e3)
                 staged.append(eng.stats()["h2d_staged_bytes_total"] - s0)
-        time.sleep(0.05)  # the cycle ends some time after the last report (cycle.end timer)
+        if gap_ms:
+            time.sleep(gap_ms / 1e3)  # the cycle ends some time after the last report (cycle.end timer)
         phases.clear()
         t0 = time.perf_counter()
         new = inc.close(ckpt)
@@ -108,11 +114,12 @@ def main():
     if pool is not None:
         pool.close()
     print(json.dumps({
-        "pinned_reports": pool is not None, "process_tuning": tuned,
+        "pinned_reports": pool is not None, "process_tuning": tuned, "speculative_folds": inc.speculate,
+        "close_gap_ms": gap_ms,
         "pinned_pool": {"hits": pool.hits, "misses": pool.misses} if pool is not None else None,
         "host_staging_bytes_per_report": {"mean": round(float(np.mean(staged)), 1), "max": int(max(staged))},
         "workload": "ResNet-18 (62 tensors), 100 assigned per cycle, ~20 % never report, shuffled arrival, "
-                    "base64 text -> report.b64decode -> IncrementalCycle.reported; close 50 ms after the last report",
+                    "base64 text -> report.b64decode -> IncrementalCycle.reported; close close_gap_ms after the last report",
         "cycles": cycles, "reports": len(tot),
         "report_b64decode_ms": {"p50": pct(dec, 50), "p99": pct(dec, 99), "max": round(max(dec), 3)},
         "report_ingest_ms": {"p50": pct(ing, 50), "p99": pct(ing, 99), "max": round(max(ing), 3)},
