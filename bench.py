@@ -248,8 +248,9 @@ def group_line(args, limit_s: int = 300) -> dict:
            "frac": (g.get("roofline") or {}).get("frac"), "rccl": cfg.get("rccl"),
            "exchange": cfg.get("exchange"), "parallelism": cfg.get("parallelism"),
            "devices": cfg.get("devices"), "command": " ".join(cmd[1:])}
-    if "cycle_close_e2e" in g:
-        out["cycle_close_e2e"] = g["cycle_close_e2e"]
+    for k in ("cycle_close_e2e", "cycle_close_report_time"):
+        if k in g:
+            out[k] = g[k]
     return out
 
 
@@ -1141,6 +1142,47 @@ def e2e_close(ctx, args, eng, n_clients: int, steps: int = 2):
                           "State bytes in host memory -> new checkpoint bytes (BASELINE.md cycle close; PCIe-inclusive)"}
 
 
+def report_close(ctx, args, eng, cycles: int = 4, gap_ms: float = 5.0, assigned: int = 100):
+    """The close as a node running report-time aggregation sees it: per cycle
+    `assigned` ResNet-18 workers, ~20 % never report (worker 0 among them, routes.py:314), the rest in
+    shuffled order `gap_ms` apart (a node decodes each report's base64 for 4-5 ms anyway,
+    tools/node_sim.py); each State diff goes to HBM and is folded when reported; the close
+    (cycle_manager.py:217 -> :240-303) = what the DB order still changes + the new checkpoint bytes.
+    Wall time of IncrementalCycle.close after the last report returned; 1 warm-up cycle."""
+    import numpy as np
+
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast
+    from pygrid_amd.workloads import RESNET18_SHAPES
+
+    rng = np.random.default_rng(args.seed + 17)
+    numel = [int(np.prod(s)) for s in RESNET18_SHAPES]
+    ck_pb = build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in RESNET18_SHAPES])
+    distinct = [build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2)
+                                  for s in RESNET18_SHAPES]) for _ in range(4)]
+    reporters = [w for w in range(assigned) if w != 0 and rng.random() >= 0.2]
+    closes, left = [], []
+    for cyc in range(cycles + 1):
+        inc = IncrementalCycle(eng, numel, slots=assigned, checkpoint=ck_pb)
+        for w in range(assigned):
+            inc.assigned(w)
+        for w in rng.permutation(reporters):
+            inc.reported(int(w), distinct[int(w) % 4])
+            time.sleep(gap_ms / 1e3)
+        t0 = time.perf_counter()
+        ck_pb = inc.close(ck_pb)
+        if cyc:
+            closes.append((time.perf_counter() - t0) * 1e3)
+            left.append(inc.last_close["n"] - inc.last_close["early"])
+    return {"close_ms_after_last_report": round(float(np.median(closes)), 3),
+            "closes_ms": [round(c, 3) for c in closes], "assigned": assigned, "reporters": len(reporters),
+            "rows_left_to_fold_at_close": int(np.median(left)), "report_gap_ms": gap_ms,
+            "speculative_folds": inc.speculate, "gpus": ctx.n_gpus,
+            "definition": "wall time of IncrementalCycle.close after the last report (report-time aggregation, "
+                          "cycles chained through the resident checkpoint): fold what the DB order still changes "
+                          "+ new checkpoint bytes (PCIe-inclusive D2H)"}
+
+
 def group_exchange(eng) -> str:
     """How a group's collective ran: RCCL (distinct devices) or the library's peer copies (repeated
     devices, PGH_RCCL=0, or a group of one before its first collective)."""
@@ -1253,6 +1295,7 @@ def main_group(ctx, args):
         rec = run_group_resident(ctx, args, eng, mode, dtype, N, parties, Pg)
         if args.workload == "resnet18-fedavg" and not args.no_e2e:
             rec["cycle_close_e2e"] = e2e_close(ctx, args, eng, N)
+            rec["cycle_close_report_time"] = report_close(ctx, args, eng)
     print(json.dumps(rec), flush=True)
     eng.close()
 
@@ -1316,6 +1359,7 @@ def main():
         if args.workload == "resnet18-fedavg" and ctx.world == 1 and not args.no_e2e:
             # the bytes -> bytes close of the same config (BASELINE.md cycle close), beside the kernel line
             rec["cycle_close_e2e"] = e2e_close(ctx, args, eng, N)
+            rec["cycle_close_report_time"] = report_close(ctx, args, eng)
     eng.close()
     del eng
     if ctx.world > 1:
