@@ -61,11 +61,13 @@ def _worker(rank, world, port, P, N, mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("P,N,mode", [(10_007, 5, 0), (130, 3, 1), (64, 4, 2), (1, 2, 0)])
-def test_sharded_fold_and_gather_is_bit_identical(P, N, mode):
+@pytest.mark.parametrize("P,N,mode,world", [(10_007, 5, 0, 2), (130, 3, 1, 2), (64, 4, 2, 2), (1, 2, 0, 2),
+                                             (10_007, 5, 1, 4), (1_000, 3, 2, 8), (200, 2, 0, 8)])
+def test_sharded_fold_and_gather_is_bit_identical(P, N, mode, world):
+    """World 2 and -- rehearsing the driver's 4- and 8-GPU runs on the CPU -- worlds 4 and 8,
+    including shards of fewer than 64 params and ranks holding nothing."""
     from oracle import coracle
 
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -84,7 +86,7 @@ def test_sharded_fold_and_gather_is_bit_identical(P, N, mode):
     for rank, blob, tmax in res:
         got = np.frombuffer(blob, dtype=np.float32)
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), rank
-        assert tmax == 2.0
+        assert tmax == float(world)
 
 
 @pytest.mark.parametrize("P", [1, 63, 64, 65, 10_000, 11_689_512, 100_000_000])
@@ -139,14 +141,14 @@ def _cs_worker(rank, world, port, P, N, S, chunks, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("P,N,S,chunks", [(10_007, 5, 2, 3), (130, 3, 3, 8), (1, 1, 2, 1), (300, 7, 2, 2)])
-def test_client_sharded_secagg_reduce_scatter_is_bit_identical(P, N, S, chunks):
+@pytest.mark.parametrize("P,N,S,chunks,world", [(10_007, 5, 2, 3, 2), (130, 3, 3, 8, 2), (1, 1, 2, 1, 2),
+                                                  (300, 7, 2, 2, 2), (10_007, 9, 2, 3, 4), (500, 5, 2, 2, 8)])
+def test_client_sharded_secagg_reduce_scatter_is_bit_identical(P, N, S, chunks, world):
     """Secure aggregation with the CLIENTS sharded (north_star: reduce-scatter when clients are
     sharded): per-rank Z_2^64 sums reduce-scattered, decoded per slice, all-gathered -- equal bit
     for bit to one rank summing every client, and the reduced slices are the full sum's."""
     from oracle import oracle as O
 
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
