@@ -329,7 +329,18 @@ int threads_for(size_t n, int threads) {
     return n < (1u << 18) ? 1 : t;
 }
 
+// Where the fast path takes the first '=' to be: the first one in the last 4 KiB of the text (a
+// client's base64 ends in its padding), else n.  An earlier '=' sits inside the prefix the fast path
+// decodes, whose per-thread alphabet check then fails (PGH_E_STATE: the general route decides) --
+// so no single-threaded memchr over the whole 62 MB text (twice per report: size, then decode).
 size_t first_eq(const unsigned char* s, size_t n) {
+    const size_t from = n > 4096 ? n - 4096 : 0;
+    const void* eq = n ? std::memchr(s + from, '=', n - from) : nullptr;
+    return eq ? (size_t)((const unsigned char*)eq - s) : n;
+}
+
+// The general route needs the true first '=' (the machine takes over there).
+size_t first_eq_exact(const unsigned char* s, size_t n) {
     const void* eq = n ? std::memchr(s, '=', n) : nullptr;
     return eq ? (size_t)((const unsigned char*)eq - s) : n;
 }
@@ -346,8 +357,7 @@ size_t pgh_b64_decoded_cap(size_t n) { return n / 4 * 3 + 3; }
 int pgh_b64_clean_size(const char* in, size_t n, size_t* size) {
     if ((!in && n) || !size) return PGH_E_ARG;
     const unsigned char* s = (const unsigned char*)in;
-    const void* eq = n ? std::memchr(s, '=', n) : nullptr;
-    const size_t fe = eq ? (size_t)((const unsigned char*)eq - s) : n;
+    const size_t fe = first_eq(s, n);
     const size_t n4f = fe / 4;
     Machine m;
     std::vector<uint8_t> tail;
@@ -374,11 +384,11 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
     if ((!in && n) || !written) return PGH_E_ARG;
     const unsigned char* s = (const unsigned char*)in;
     const int t = threads_for(n, threads);
-    const size_t fe = first_eq(s, n);  // the machine's fast prefix
     if (std::getenv("PGH_B64_GENERAL") == nullptr) {
-        const int rc = decode_fast(s, n, fe, out, pgh_b64_decoded_cap(n), written, t);
+        const int rc = decode_fast(s, n, first_eq(s, n), out, pgh_b64_decoded_cap(n), written, t);
         if (rc != PGH_E_STATE) return rc;  // clean text: decoded, or a padding error
     }
+    const size_t fe = first_eq_exact(s, n);  // the machine's prefix
     // count alphabet characters per chunk of [0, fe)
     const size_t per = (fe + t - 1) / t;
     std::vector<size_t> good((size_t)t, 0);
