@@ -113,6 +113,13 @@ const char* pgh_last_error(const pgh_ctx* ctx);   /* ctx may be NULL (creation e
 /* Page-locked host buffers: ingest DMAs them straight to HBM (no staging copy). */
 int pgh_host_alloc(size_t bytes, void** out);
 int pgh_host_free(void* p);
+/* Mark (on = 1) a pgh_host_alloc block of n bytes as ASYNC: an ingest of State bytes lying in it
+ * returns once its DMA is queued instead of waiting for it, so the caller must pgh_host_wait(p, n)
+ * before writing to or reusing the block (pgh_host_free waits by itself).  on = 0 waits, then
+ * unmarks.  Unmarked page-locked memory keeps the synchronous contract. */
+int pgh_host_async(void* p, size_t n, int on);
+/* Wait for every DMA still reading host memory [p, p + n), queued by any context. */
+int pgh_host_wait(const void* p, size_t n);
 /* Fault in the pages of a (fresh, pageable) host buffer now, on up to 8 threads, so that a later
  * copy into it -- the new checkpoint's payloads at a cycle close -- takes no page faults.  Best
  * effort (Linux 5.14+ MADV_POPULATE_WRITE); always returns PGH_OK for a valid range. */

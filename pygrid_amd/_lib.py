@@ -82,6 +82,8 @@ SIGNATURES = {
     "pgh_host_alloc": (_i, [_sz, C.POINTER(_vp)]),
     "pgh_host_free": (_i, [_vp]),
     "pgh_host_prefault": (_i, [_vp, _sz]),
+    "pgh_host_async": (_i, [_vp, _sz, _i]),
+    "pgh_host_wait": (_i, [_vp, _sz]),
     "pgh_set_layout": (_i, [_vp, _i, _P64]),
     "pgh_set_shard": (_i, [_vp, _i64, _i64]),
     "pgh_reserve": (_i, [_vp, _i, _i, _i]),

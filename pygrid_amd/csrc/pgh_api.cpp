@@ -1227,6 +1227,73 @@ int pgh_device_count(int* n) {
 
 const char* pgh_last_error(const pgh_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
+// ---- page-locked blocks whose DMAs may outlive the ingest call -------------------------------------
+// pgh_host_async marks a pgh_host_alloc block: an ingest from it then returns once the DMA is queued
+// (not done), and records the DMA's event here; pgh_host_wait(p, n) waits for every DMA still reading
+// [p, p + n) (any context, any GPU) before the owner reuses or frees the block.  Unmarked page-locked
+// memory keeps the synchronous contract (the call waits for its copies).
+namespace {
+struct HostDma { uintptr_t lo, hi; hipEvent_t ev; };
+std::mutex g_host_mu;
+std::vector<std::pair<uintptr_t, uintptr_t>> g_async_blocks;  // [lo, hi)
+std::vector<HostDma> g_host_dmas;
+
+bool host_async(const void* p, size_t n) {
+    const uintptr_t a = (uintptr_t)p, b = a + n;
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    for (auto& r : g_async_blocks)
+        if (a >= r.first && b <= r.second) return true;
+    return false;
+}
+
+// Record that a DMA reading [p, p + n) was queued on stream s (the event is recorded here).
+int host_dma_queued(pgh_ctx* c, const void* p, size_t n, hipStream_t s) {
+    hipEvent_t ev = nullptr;
+    CK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    const hipError_t e = hipEventRecord(ev, s);
+    if (e != hipSuccess) {
+        (void)hipEventDestroy(ev);
+        return fail(c, PGH_E_HIP, "hipEventRecord failed: %s", hipGetErrorString(e));
+    }
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    g_host_dmas.push_back({(uintptr_t)p, (uintptr_t)p + n, ev});
+    return PGH_OK;
+}
+}  // namespace
+
+int pgh_host_async(void* p, size_t n, int on) {
+    if (!p || !n) return fail(nullptr, PGH_E_ARG, "bad block");
+    if (!on) RC(pgh_host_wait(p, n));
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    const std::pair<uintptr_t, uintptr_t> r{(uintptr_t)p, (uintptr_t)p + n};
+    auto it = std::find(g_async_blocks.begin(), g_async_blocks.end(), r);
+    if (on && it == g_async_blocks.end()) g_async_blocks.push_back(r);
+    if (!on && it != g_async_blocks.end()) g_async_blocks.erase(it);
+    return PGH_OK;
+}
+
+int pgh_host_wait(const void* p, size_t n) {
+    const uintptr_t a = (uintptr_t)p, b = a + n;
+    std::vector<hipEvent_t> evs;
+    {
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        auto keep = g_host_dmas.begin();
+        for (auto& d : g_host_dmas) {
+            if (d.lo < b && a < d.hi) evs.push_back(d.ev);
+            else *keep++ = d;
+        }
+        g_host_dmas.erase(keep, g_host_dmas.end());
+    }
+    int rc = PGH_OK;
+    for (hipEvent_t ev : evs) {
+        const hipError_t e = hipEventSynchronize(ev);
+        if (e != hipSuccess && rc == PGH_OK) rc = fail(nullptr, PGH_E_HIP, "DMA from host buffer failed: %s",
+                                                       hipGetErrorString(e));
+        (void)hipEventDestroy(ev);
+    }
+    return rc;
+}
+
 int pgh_host_alloc(size_t bytes, void** out) {
     if (!out || !bytes) return fail(nullptr, PGH_E_ARG, "bad pinned allocation request");
     *out = nullptr;
@@ -1257,6 +1324,19 @@ int pgh_host_prefault(void* p, size_t n) {
 }
 
 int pgh_host_free(void* p) {
+    if (p) {
+        size_t n = 0;
+        {
+            std::lock_guard<std::mutex> lk(g_host_mu);
+            for (auto it = g_async_blocks.begin(); it != g_async_blocks.end(); ++it)
+                if (it->first == (uintptr_t)p) {
+                    n = it->second - it->first;
+                    g_async_blocks.erase(it);
+                    break;
+                }
+        }
+        if (n) (void)pgh_host_wait(p, n);  // a DMA from the block may still be running
+    }
     if (p && hipHostFree(p) != hipSuccess) return fail(nullptr, PGH_E_HIP, "hipHostFree failed");
     return PGH_OK;
 }
@@ -1756,12 +1836,14 @@ int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>
     CK(c, hipEventRecord(c->gtab_ev, c->copy));
     c->gtab_used = true;
     CK(c, hipMemcpyAsync(c->d_vbytes, pb + a, b - a, hipMemcpyHostToDevice, c->copy));
-    CK(c, hipEventRecord(c->gdma_ev, c->copy));
+    const bool async = host_async(pb + a, b - a);
+    if (async) RC(host_dma_queued(c, pb + a, b - a, c->copy));  // the block's owner waits (pgh_host_wait)
+    else CK(c, hipEventRecord(c->gdma_ev, c->copy));
     const Dest d = row_dest(c, slot, 0);
     const hipError_t e = pgh::launch_gather_f32(c->d_vbytes, c->d_gtab, (int)tab.size(), (float*)d.base, d.map,
                                                 c->copy);
     if (e != hipSuccess) return fail(c, PGH_E_HIP, "gather launch failed: %s", hipGetErrorString(e));
-    CK(c, hipEventSynchronize(c->gdma_ev));
+    if (!async) CK(c, hipEventSynchronize(c->gdma_ev));
     c->st.h2d_bytes_total += total;
     return PGH_OK;
 }

@@ -454,8 +454,8 @@ class IncrementalCycle:
                 log.info("re-folding the cycle in the DB's order: %s", refold)
                 self.engine.fold_restart()
                 self._weights = []
-            self._drop_marks()
             stats = self._fold_in_order(rest, fetch)
+            self._drop_marks()  # after the FINAL pass: it reads a rewound state from its mark in place
             stats.update(refold=bool(refold), reason=refold or None, early=k, n=len(order),
                          folded_before_close=folded_before, rewinds=self.rewinds)
             self.last_close = stats

@@ -47,7 +47,11 @@ class PinnedPool:
     """Page-locked host blocks (``pgh_host_alloc``) for decoded report diffs.  At most
     ``max_blocks`` blocks (each rounded up to 2 MiB) are allocated; a report beyond that -- more
     reports in flight than blocks, or a diff larger than ``max_block_bytes`` -- is decoded into
-    ordinary memory, as without a pool.  Counters: ``hits`` (decoded into a block), ``misses``."""
+    ordinary memory, as without a pool.  Counters: ``hits`` (decoded into a block), ``misses``.
+
+    Blocks are marked async (``pgh_host_async``): an ingest of a diff lying in one returns with its
+    DMA queued, and a block that comes back is handed out again only after ``pgh_host_wait`` --
+    the report handler does not wait for PCIe, the next decode never overwrites bytes in flight."""
 
     def __init__(self, max_blocks: int = 16, max_block_bytes: int = 1 << 30):
         self.max_blocks = int(max_blocks)
@@ -83,7 +87,7 @@ class PinnedPool:
                 self._n += 1  # reserved; allocated below, outside the lock
                 cap, addr = (n + _BLOCK_ALIGN - 1) // _BLOCK_ALIGN * _BLOCK_ALIGN, None
         if evict is not None:
-            lib.pgh_host_free(C.c_void_p(evict[1]))
+            lib.pgh_host_free(C.c_void_p(evict[1]))  # waits for a DMA still reading it
         if addr is None:
             p = C.c_void_p()
             if lib.pgh_host_alloc(cap, C.byref(p)) != 0:
@@ -92,6 +96,11 @@ class PinnedPool:
                     self.misses += 1
                 return None
             addr = p.value
+            # an ingest from the block returns with its DMA queued, not done (pgh_host_async) ...
+            lib.pgh_host_async(C.c_void_p(addr), cap, 1)
+        else:
+            # ... so a returned block is written again only after that DMA has read it
+            lib.pgh_host_wait(C.c_void_p(addr), cap)
         with self._lock:
             self.hits += 1
         arr = (C.c_uint8 * n).from_address(addr)

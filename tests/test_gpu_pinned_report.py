@@ -111,3 +111,41 @@ def test_pinned_messages_at_any_payload_alignment(monkeypatch, shapes, devices, 
     finally:
         eng.close()
         pool.close()
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_one_block_reused_by_every_report_while_dmas_fly(devices):
+    """Async page-locked ingest: the ingest returns with the DMA queued, so the pool's single block
+    is decoded into again by the next report only after pgh_host_wait -- otherwise the next diff would
+    overwrite bytes still in flight.  12 reports through ONE block, bit-exact close."""
+    import base64
+
+    from pygrid_amd import Engine
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.report import PinnedPool, b64decode
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(730)
+    shapes = [(2048, 1024), (1024,)]  # 8 MB per diff: the DMA takes ~0.15 ms
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for _ in range(12)]
+    texts = [base64.b64encode(build_state_fast(d)).decode() for d in diffs]
+    pool = PinnedPool(max_blocks=1)
+    eng = Engine(devices=devices) if devices else Engine(0)
+    try:
+        ck = build_state_fast(ckpt)
+        inc = IncrementalCycle(eng, [int(np.prod(s)) for s in shapes], slots=16, checkpoint=ck)
+        for w in range(12):
+            inc.assigned(w)
+        for w in (3, 0, 7, 1, 2, 11, 4, 5, 10, 6, 8, 9):
+            d = b64decode(texts[w], into=pool)
+            assert isinstance(d, memoryview)
+            inc.reported(w, d)
+            del d
+        assert pool.hits == 12 and pool.blocks == 1
+        new = inc.close(ck, framing="template")
+        for g, w in zip(parse_state(new), O.fedavg_mean(ckpt, diffs)):
+            assert np.array_equal(bits(g), bits(w))
+    finally:
+        eng.close()
+        pool.close()
