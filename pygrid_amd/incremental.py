@@ -13,24 +13,32 @@ diff lives from WHEN it is folded:
 * ``reported(w, diff)`` copies the diff into HBM at once, into whichever slab slot is free
   (``pgh_ingest_state``: PCIe + host copy happen while the report is handled, in any arrival
   order);
-* the fold speculates on the assignment order (``assigned(w, key)``, ``key`` = the WorkerCycle row
-  id): a diff's position is taken as certain once every worker assigned before it has reported,
-  and the certain prefix is folded from its scattered slots (``pgh_fold_slots``: the kernel reads
-  the slots through a row table), freeing them;
+* the fold follows the assignment order (``assigned(w, key)``, ``key`` = the WorkerCycle row id),
+  reporters only, through the slots where the diffs landed (the kernel reads them through a row
+  table).  A position is CERTAIN once every worker assigned before it has reported.  Speculative
+  folds (default): every reported diff is folded at once (``pgh_fold_slots_keep``: its slot is kept)
+  and the fold state is saved every ``mark_every`` rows and at the certain point
+  (``pgh_fold_mark``); when an earlier worker reports after all, or a kept one re-reports, the fold
+  goes back to the last saved state before its position (``pgh_fold_rewind``) and continues; slots
+  before the last saved state at the certain point are freed.  While the GPU is still busy with the
+  previous fold, a report is folded with a later one (``pgh_fold_busy``).  Certain-only folds
+  (``speculate=False``): the certain prefix is folded ``fold_batch`` at a time and freed
+  (``pgh_fold_slots``);
 * ``close(checkpoint, order=..., fetch=...)`` takes the AUTHORITATIVE order -- the keys of the
-  completed-WorkerCycle query, as the node's DB returns them -- checks that the early-folded
-  prefix is that order's prefix, and folds the rest of the order from HBM (slots), the host
-  (parked diffs) or the DB (``fetch(w)``: diffs this process never saw, e.g. reported before a
-  restart).  When the prefix does not match (the DB returned another order, a folded worker
-  re-reported, an assignment arrived behind the fold front) the fold restarts
+  completed-WorkerCycle query, as the node's DB returns them -- keeps the early fold up to the last
+  saved state inside its common prefix with that order, and folds the rest of the order from HBM
+  (slots), the host (parked diffs) or the DB (``fetch(w)``: diffs this process never saw, e.g.
+  reported before a restart).  When even that is impossible (the order differs inside the freed
+  prefix, a freed worker re-reported, an assignment arrived behind it) the fold restarts
   (``pgh_fold_slots_restart``) and re-folds the whole order, the folded diffs fetched from the DB:
   bit-identical to the reference in every case, early folding is only ever a speedup.
 
 Report semantics (``cycle_manager.py:162-174``, ``fl_events.py:257-263``):
 
 * **re-report** before the worker's diff was folded: the new diff replaces the old one (same slot,
-  or the parked copy); after it was folded: the early fold is stale and ``close`` re-folds from the
-  DB (the reference averages the LATEST diff at the worker's original row position);
+  or the parked copy); after it was folded: the fold goes back to before it if its slot is still
+  kept, else the early fold is stale and ``close`` re-folds from the DB (the reference averages the
+  LATEST diff at the worker's original row position);
 * **late report** (after ``close``): accepted and ignored -- the reference stores it and its
   ``complete_cycle`` returns early for a completed cycle (``:186-188``);
 * **a report from a worker this object was not told about** (assigned before a restart):
