@@ -64,6 +64,7 @@ import bisect
 import itertools
 import logging
 import threading
+import time
 from typing import Callable, Dict, Hashable, List, Optional, Sequence
 
 from . import state as state_codec
@@ -86,7 +87,8 @@ class IncrementalCycle:
     def __init__(self, engine: Engine, numel, mode: int = MEAN, slots: Optional[int] = None, fold_batch: int = 8,
                  weights_by_worker: Optional[Dict[object, float]] = None, checkpoint: Optional[bytes] = None,
                  early_fold: bool = True, speculate: Optional[bool] = None,
-                 speculation_budget: int = DEFAULT_SPECULATION_BUDGET, mark_every: int = 8, lazy: bool = True):
+                 speculation_budget: int = DEFAULT_SPECULATION_BUDGET, mark_every: int = 8, lazy: bool = True,
+                 min_gap_ms: float = 2.0):
         self.engine = engine
         self.mode = mode
         self._numel = tuple(int(n) for n in numel)
@@ -104,6 +106,9 @@ class IncrementalCycle:
         # speculative folds wait while the GPU is still busy with the previous one (reports arriving
         # back to back would otherwise queue re-folds that the next report discards)
         self._lazy = bool(lazy) and hasattr(engine, "fold_busy")
+        self.min_gap_s = max(0.0, float(min_gap_ms)) / 1e3
+        self._last_report = None
+        self._hurried = False  # the last report came less than min_gap after the one before
         if speculate and not self.speculate:
             raise AggregationError("speculative folds need an engine with fold marks and HBM for >= 2 of them "
                                    f"({self.max_marks} fit in the budget)")
@@ -195,6 +200,9 @@ class IncrementalCycle:
             if self._weights_by_worker is not None and worker not in self._weights_by_worker:
                 # refused to its sender now, not when a later report folds it
                 raise AggregationError(f"worker {worker!r} reported but has no aggregation weight")
+            now = time.monotonic()
+            self._hurried = self._last_report is not None and now - self._last_report < self.min_gap_s
+            self._last_report = now
             if worker in self._folded_set:
                 # its earlier diff is in the fold state: go back to before it (its slot is still
                 # held), or -- when it was folded for good -- the close re-folds from the DB
@@ -294,8 +302,11 @@ class IncrementalCycle:
         common = _common_prefix(self._folded, target)
         if common < len(self._folded) and not self._rewind(common):
             return  # the early fold is not the plan's prefix any more: the close re-folds
-        if self.speculate and self._lazy and not self._parked and self.engine.fold_busy():
-            return  # the GPU is still folding: fold this report with a later one (or at close)
+        if self.speculate and self._lazy and not self._parked and (self._hurried or self.engine.fold_busy()):
+            # reports arriving faster than a re-fold takes, or the GPU still folding: fold this
+            # report with a later one (or at close) instead of queueing re-folds the next report
+            # throws away
+            return
         run: List = []
         for w in target[len(self._folded):]:
             if w not in self._slot_of:

@@ -174,7 +174,7 @@ def test_group_report_time_cycle(group2, speculate):
     ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
     ck_pb = build_state_fast(ckpt)
     inc = IncrementalCycle(group2, [int(np.prod(s)) for s in shapes], slots=16, fold_batch=3, checkpoint=ck_pb,
-                           speculate=speculate, mark_every=2)
+                           speculate=speculate, mark_every=2, lazy=False)
     for w in range(n):
         inc.assigned(w)
     for w in rng.permutation(reporters):

@@ -32,7 +32,8 @@ def test_incremental_cycle_matches_reference_order(engine, mode, ckpt_at_start, 
     ckpt_pb = build_state_fast(ckpt)
     inc = IncrementalCycle(engine, [int(np.prod(s)) for s in shapes], mode=mode, slots=slots, fold_batch=2,
                            weights_by_worker=weights if mode == 2 else None,
-                           checkpoint=ckpt_pb if ckpt_at_start else None, speculate=speculate, mark_every=3)
+                           checkpoint=ckpt_pb if ckpt_at_start else None, speculate=speculate, mark_every=3,
+                           lazy=False)
     assert inc.speculate == speculate
     for w in range(n_assigned):
         inc.assigned(w)
