@@ -703,3 +703,36 @@ def test_speculation_under_slot_pressure_closes_without_the_db(slots, seed):
         assert len([s for s in eng.slot]) <= slots
     inc.close(b"ck", framing="template")
     assert eng.result == [mk(w) for w in reporters]
+
+
+class BusySpecEngine(SpecEngine):
+    """SpecEngine with pgh_fold_busy: `busy` says whether the GPU is still folding."""
+
+    busy = False
+
+    def fold_busy(self):
+        return self.busy
+
+
+@pytest.mark.parametrize("gap_ms,busy,folds_during_reports", [(5.0, False, True), (0.5, False, False),
+                                                              (5.0, True, False)])
+def test_lazy_speculation_waits_for_slow_reports_and_an_idle_gpu(monkeypatch, gap_ms, busy, folds_during_reports):
+    """Lazy speculation (the default with a real engine): a report is folded at once only when the
+    previous one came at least min_gap_ms before and the GPU is idle; otherwise it waits for a later
+    report or the close -- the result is the same either way."""
+    import pygrid_amd.incremental as inc_mod
+
+    clock = [100.0]
+    monkeypatch.setattr(inc_mod.time, "monotonic", lambda: clock[0])
+    eng = BusySpecEngine()
+    eng.busy = busy
+    inc = IncrementalCycle(eng, [3], slots=16)
+    assert inc.speculate and inc._lazy
+    for w in range(8):
+        inc.assigned(w)
+    for w in (3, 1, 6, 2, 5, 7, 4):   # worker 0 never reports
+        clock[0] += gap_ms / 1e3
+        inc.reported(w, bytes([w]))
+    assert (len(eng.state) > 1) == folds_during_reports
+    inc.close(b"ck", framing="template")
+    assert eng.result == [bytes([w]) for w in range(1, 8)]
