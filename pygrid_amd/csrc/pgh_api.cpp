@@ -1256,6 +1256,14 @@ int host_dma_queued(pgh_ctx* c, const void* p, size_t n, hipStream_t s) {
         return fail(c, PGH_E_HIP, "hipEventRecord failed: %s", hipGetErrorString(e));
     }
     std::lock_guard<std::mutex> lk(g_host_mu);
+    // forget DMAs that have finished (a block held elsewhere for long would otherwise collect them)
+    auto keep = g_host_dmas.begin();
+    for (auto& d : g_host_dmas) {
+        if (hipEventQuery(d.ev) == hipSuccess) (void)hipEventDestroy(d.ev);
+        else *keep++ = d;
+    }
+    g_host_dmas.erase(keep, g_host_dmas.end());
+    (void)hipGetLastError();  // hipErrorNotReady from the queries above
     g_host_dmas.push_back({(uintptr_t)p, (uintptr_t)p + n, ev});
     return PGH_OK;
 }
