@@ -231,6 +231,16 @@ int pgh_fold_unmark(pgh_ctx* ctx, int mark);
 /* *busy = 1 while the last slot fold issued is still running (a caller may then leave further
  * speculative folds for later instead of queueing re-folds behind it), else 0.  Never blocks. */
 int pgh_fold_busy(pgh_ctx* ctx, int* busy);
+/* Speculative close (ABI 6).  pgh_fold_peek runs the FINAL pass of the fold state as it stands --
+ * ckpt - avg over the clients folded so far, into a buffer of its own -- and copies the result to a
+ * pinned host buffer behind it (its own stream: beside the ingest DMAs), without ending the cycle.
+ * pgh_peek_patch_state(out) then, if NOTHING changed since (no fold, rewind, restart, weights or
+ * checkpoint change), writes this context's payload slices of the framed State message `out`
+ * (pgh_state_fresh's framing) from that copy and makes the peeked result the resident checkpoint --
+ * exactly as pgh_fold_slots_finish_resident(no slots) + pgh_ckpt_patch_state(out, out) would -- and
+ * sets *ok = 1; otherwise *ok = 0 and nothing changes.  A group commits all of its GPUs or none. */
+int pgh_fold_peek(pgh_ctx* ctx, int mode);
+int pgh_peek_patch_state(pgh_ctx* ctx, uint8_t* out, size_t n, int* ok);
 
 /* Z_2^64 share sum over all clients x parties, then decode float32(sum) / base**prec.
  * sum_out (int64) and dec_out (float32) are host arrays of P_shard; either may be NULL. */

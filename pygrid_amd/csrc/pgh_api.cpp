@@ -246,6 +246,16 @@ struct pgh_ctx {
     hipEvent_t xsync = nullptr;    // caller-stream <-> context-stream ordering
     hipStream_t aux = nullptr;     // second reduction stream: alternate ranges of a split FINAL pass
     hipEvent_t aux_ev = nullptr;
+    // Speculative close (pgh_fold_peek): the FINAL pass of the fold state as it stands, written to
+    // d_out and copied to the pinned h_peek on peek_stream (D2H beside the ingest H2D), valid while
+    // state_gen is unchanged -- every fold, rewind, restart, weight or checkpoint change bumps it.
+    hipStream_t peek_stream = nullptr;
+    hipEvent_t peek_ev = nullptr;
+    float* h_peek = nullptr;   // pinned, peek_cap floats
+    size_t peek_cap = 0;
+    float* d_peek = nullptr;   // [pvec]: the peeked new checkpoint (swapped with d_ckpt on commit)
+    uint64_t state_gen = 1;
+    uint64_t peek_gen = 0;  // state_gen the peek was taken at (0: none)
     // The last fold issued on each stream (folds may run on several caller streams at once, e.g.
     // the param ranges of the multi-GPU overlap): the copy stream waits on all before it
     // overwrites slots, and then forgets them (later copies are ordered after those waits).
@@ -436,13 +446,17 @@ size_t esize(int dtype) { return dtype == PGH_F32 ? 4 : 8; }
 void release_slot_fold_events(pgh_ctx* c);
 
 void free_slab(pgh_ctx* c) {
+    if (c->peek_stream) (void)hipStreamSynchronize(c->peek_stream);  // a peek's D2H reads d_peek
+    (void)hipFree(c->d_peek); c->d_peek = nullptr;
+    if (c->h_peek) (void)hipHostFree(c->h_peek);
+    c->h_peek = nullptr; c->peek_cap = 0; c->peek_gen = 0;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     for (auto& fe : c->fold_evs) (void)hipEventSynchronize(fe.second);  // folds on caller streams
     (void)hipFree(c->d_slab); c->d_slab = nullptr; c->slab_bytes = 0;
     (void)hipFree(c->d_ckpt); c->d_ckpt = nullptr;
     (void)hipFree(c->d_out); c->d_out = nullptr;
-    c->ckpt_valid = false;
+    c->ckpt_valid = false; ++c->state_gen;
     for (auto& m : c->final_marks) c->rmark_pool.push_back(m.ev);
     c->final_marks.clear();
     (void)hipFree(c->d_acc); c->d_acc = nullptr;
@@ -1112,6 +1126,7 @@ int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const Fina
         done += seg;
     } while (done < n);
     RC(record_fold(c, s));
+    ++c->state_gen;
     return record_slab_fold(c, s);
 }
 
@@ -1481,6 +1496,8 @@ void pgh_destroy(pgh_ctx* c) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
     if (c->aux) (void)hipStreamDestroy(c->aux);
+    if (c->peek_ev) (void)hipEventDestroy(c->peek_ev);
+    if (c->peek_stream) (void)hipStreamDestroy(c->peek_stream);
     delete c;
 }
 
@@ -1574,6 +1591,7 @@ int pgh_reset(pgh_ctx* c) {
     clear_marks(c);
     drop_fold_marks(c);
     release_slot_fold_events(c);  // c->stream is idle (synchronised above)
+    ++c->state_gen;
     std::fill(c->slot_client.begin(), c->slot_client.end(), -1);
     c->weights.clear();
     c->weights_on_device = false;
@@ -2002,7 +2020,7 @@ int pgh_synth_ckpt_device(pgh_ctx* c, uint64_t seed, float* d_ckpt, void* stream
         return PGH_OK;
     }
     if (!c->d_ckpt) return fail(c, PGH_E_STATE, "pgh_reserve has not been called");
-    c->ckpt_valid = false;  // the resident checkpoint is used as scratch here
+    c->ckpt_valid = false; ++c->state_gen;  // the resident checkpoint is used as scratch here
     clear_final_marks(c);
     hipError_t e = pgh::launch_synth_f32(c->d_ckpt, pgh::single_block(c->pvec), c->pvec, 1, c->pg, seed,
                                          pgh::STREAM_CKPT, 0, c->lo, pgh::CKPT_SCALE, s);
@@ -2023,6 +2041,7 @@ int pgh_set_weights(pgh_ctx* c, const float* w, int n) {
     }
     c->weights.assign(w, w + n);
     c->weights_on_device = false;
+    ++c->state_gen;
     return PGH_OK;
 }
 
@@ -2072,10 +2091,10 @@ int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
     const double t0 = now_ms();
     const size_t bytes = sizeof(float) * (size_t)c->pg;
     RC(order_before_overwrite(c));
-    c->ckpt_valid = false;
+    c->ckpt_valid = false; ++c->state_gen;
     clear_final_marks(c);
     RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
-    c->ckpt_valid = true;
+    c->ckpt_valid = true; ++c->state_gen;
     RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
     if (is_pinned(out)) {
         CK(c, hipMemcpyAsync(out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
@@ -2100,10 +2119,10 @@ int pgh_ckpt_upload(pgh_ctx* c, const float* ckpt, size_t nbytes) {
     DeviceGuard g(c->device);
     RC(order_before_overwrite(c));
     const uint8_t* src = (const uint8_t*)ckpt + (nbytes == whole ? 4 * (size_t)c->lo : 0);
-    c->ckpt_valid = false;
+    c->ckpt_valid = false; ++c->state_gen;
     clear_final_marks(c);
     RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), src, shard, is_pinned(ckpt)));
-    c->ckpt_valid = true;
+    c->ckpt_valid = true; ++c->state_gen;
     return PGH_OK;
 }
 
@@ -2117,10 +2136,10 @@ int pgh_ckpt_upload_state(pgh_ctx* c, const uint8_t* pb, size_t n) {
     for (auto& sp : spans) pieces.push_back(Piece{pb + sp.first, sp.second});
     DeviceGuard g(c->device);
     RC(order_before_overwrite(c));
-    c->ckpt_valid = false;
+    c->ckpt_valid = false; ++c->state_gen;
     clear_final_marks(c);
     RC(stage_pieces_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), pieces));
-    c->ckpt_valid = true;
+    c->ckpt_valid = true; ++c->state_gen;
     return PGH_OK;
 }
 
@@ -2349,6 +2368,7 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final, boo
     } while (done < n);
     RC(record_fold(c, s));
     RC(record_slot_fold(c, slots, n));
+    ++c->state_gen;
     c->acc_src = nullptr;  // the running state is in d_acc again
     if (!keep)
         for (int k = 0; k < n; ++k) c->slot_client[(size_t)slots[k]] = -1;  // free for the next ingests
@@ -2449,6 +2469,7 @@ int pgh_fold_rewind(pgh_ctx* c, int mark) {
     c->st.n_folded = c->folded;
     c->slot_mode = it->second.folded > 0 ? it->second.mode : -1;
     c->acc_src = it->second.buf;  // the next slot fold reads the state there (no copy)
+    ++c->state_gen;
     return PGH_OK;
 }
 
@@ -2467,6 +2488,81 @@ int pgh_fold_unmark(pgh_ctx* c, int mark) {
         c->acc_spare.push_back(it->second.buf);
     }
     c->fold_marks.erase(it);
+    return PGH_OK;
+}
+
+// ---- speculative close: the FINAL pass of the fold state as it stands, ahead of the close -----------
+int pgh_fold_peek(pgh_ctx* c, int mode) {
+    if (c && c->grp) return pgh_group_api::fold_peek(c, mode);
+    if (!c) return PGH_E_ARG;
+    RC(check_slot_folds(c));
+    RC(check_ckpt(c, "pgh_fold_peek"));
+    if (!valid_mode(mode)) return fail(c, PGH_E_ARG, "unknown averaging mode %d", mode);
+    if (c->folded <= 0) return fail(c, PGH_E_STATE, "pgh_fold_peek: nothing folded yet");
+    if (c->slot_mode >= 0 && c->slot_mode != mode)
+        return fail(c, PGH_E_STATE, "averaging mode changed from %d to %d within a cycle", c->slot_mode, mode);
+    FinalArgs fa;
+    RC(fedavg_divisor(c, mode, c->folded, &fa.divisor));
+    DeviceGuard g(c->device);
+    if (!c->peek_stream) {
+        CK(c, hipStreamCreateWithFlags(&c->peek_stream, hipStreamNonBlocking));
+        CK(c, hipEventCreateWithFlags(&c->peek_ev, hipEventDisableTiming));
+    }
+    if (!c->d_peek && hipMalloc((void**)&c->d_peek, (size_t)c->pvec * 4) != hipSuccess) {
+        (void)hipGetLastError();
+        c->d_peek = nullptr;
+        return fail(c, PGH_E_OOM, "peek buffer (%lld floats) allocation failed", (long long)c->pvec);
+    }
+    if (c->peek_cap < (size_t)c->pg) {
+        CK(c, hipStreamSynchronize(c->peek_stream));
+        if (c->h_peek) (void)hipHostFree(c->h_peek);
+        c->h_peek = nullptr;
+        c->peek_cap = 0;
+        if (hipHostMalloc((void**)&c->h_peek, (size_t)c->pg * 4, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            c->h_peek = nullptr;
+            return fail(c, PGH_E_OOM, "pinned peek buffer of %lld floats failed", (long long)c->pg);
+        }
+        c->peek_cap = (size_t)c->pg;
+    }
+    const hipStream_t s = c->stream;
+    if (c->peek_gen) CK(c, hipStreamWaitEvent(s, c->peek_ev, 0));  // the last peek's D2H reads d_peek
+    pgh::FedavgArgs a{};
+    a.diffs = (const float*)c->d_slab;
+    a.map = slab_map(c);
+    a.n_rows = 0;
+    a.client0 = c->folded;
+    a.p = c->pg;
+    a.acc = c->d_acc;
+    a.acc_in = c->acc_src;  // a rewound state is read where it was saved
+    a.ckpt = c->d_ckpt;
+    a.out = c->d_peek;
+    a.divisor = fa.divisor;
+    a.flags = pgh::FL_FINAL;
+    a.mode = mode;
+    a.variant = c->variant;
+    pgh::RowTab tab{};
+    const uint64_t bytes = 12ull * (uint64_t)c->pg;
+    RC(timed_launch(c, s, bytes, [&] { return pgh::launch_fedavg_rows(a, tab, s); }));
+    RC(record_fold(c, s));  // a checkpoint upload waits for this read of d_ckpt
+    CK(c, hipEventRecord(c->peek_ev, s));
+    CK(c, hipStreamWaitEvent(c->peek_stream, c->peek_ev, 0));
+    CK(c, hipMemcpyAsync(c->h_peek, c->d_peek, (size_t)c->pg * 4, hipMemcpyDeviceToHost, c->peek_stream));
+    CK(c, hipEventRecord(c->peek_ev, c->peek_stream));
+    c->peek_gen = c->state_gen;
+    return PGH_OK;
+}
+
+
+int pgh_peek_patch_state(pgh_ctx* c, uint8_t* out, size_t n, int* ok) {
+    if (c && c->grp) return pgh_group_api::peek_patch_state(c, out, n, ok);
+    if (!c || !ok || !out) return PGH_E_ARG;
+    *ok = 0;
+    if (!pgh_int::peek_valid(c)) return PGH_OK;
+    const double t0 = now_ms();
+    RC(pgh_int::peek_commit(c, out, n, out));
+    c->st.close_ms_last = now_ms() - t0;
+    *ok = 1;
     return PGH_OK;
 }
 
@@ -2495,6 +2591,7 @@ int pgh_fold_slots_restart(pgh_ctx* c) {
     c->folded = 0;
     c->st.n_folded = 0;
     c->slot_mode = -1;
+    ++c->state_gen;
     c->weights.clear();
     c->weights_on_device = false;
     return PGH_OK;
@@ -2581,10 +2678,10 @@ int pgh_stream_finish(pgh_ctx* c, const float* ckpt, float* out) {
     // d_ckpt, so fold_run's order_after_ingest orders the final fold after it (a pageable
     // pgh_ckpt_upload's last ring DMA can no longer land after this copy)
     RC(order_before_overwrite(c));
-    c->ckpt_valid = false;
+    c->ckpt_valid = false; ++c->state_gen;
     clear_final_marks(c);
     RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
-    c->ckpt_valid = true;
+    c->ckpt_valid = true; ++c->state_gen;
     RC(pgh_stream_finish_device(c, c->d_ckpt, c->d_out, c->stream));
     CK(c, hipMemcpyAsync(out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));
@@ -2684,6 +2781,32 @@ int pgh_sync(pgh_ctx* c) {
 // ---- internals for the multi-GPU group driver (pgh_internal.h) ------------------------------------
 
 namespace pgh_int {
+bool peek_valid(const pgh_ctx* c) { return c->peek_gen != 0 && c->peek_gen == c->state_gen; }
+
+int peek_commit(pgh_ctx* c, const uint8_t* out_frame, size_t n, uint8_t* out) {
+    std::vector<std::pair<size_t, size_t>> spans;
+    RC(state_shard_spans(c, out_frame, n, &spans, "peeked checkpoint frame"));
+    DeviceGuard g(c->device);
+    CK(c, hipEventSynchronize(c->peek_ev));
+    std::vector<OutPiece> pieces;
+    size_t total = 0;
+    for (auto& sp : spans) {
+        pieces.push_back(OutPiece{out + sp.first, sp.second});
+        total += sp.second;
+    }
+    if (total != (size_t)c->pg * 4) return fail(c, PGH_E_ARG, "frame holds %zu payload bytes of this shard, %lld expected",
+                                                 total, (long long)c->pg * 4);
+    scatter_out((const uint8_t*)c->h_peek, 0, total, pieces, *c->pool_copy);
+    std::swap(c->d_ckpt, c->d_peek);  // the peeked result IS the new checkpoint, as after a FINAL fold
+    c->acc_src = nullptr;
+    c->folded = 0;
+    c->st.n_folded = 0;
+    c->slot_mode = -1;
+    c->peek_gen = 0;
+    ++c->state_gen;
+    return PGH_OK;
+}
+
 
 int usable_cpus() {
     static const int n = [] {

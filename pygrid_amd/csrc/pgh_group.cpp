@@ -827,6 +827,23 @@ int fold_busy(pgh_ctx* c, int* busy) {
     return PGH_OK;
 }
 
+int fold_peek(pgh_ctx* c, int mode) {
+    RC(need_slab(c));
+    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_peek(k, mode); });
+}
+
+// All children's peeks must still hold, or none is committed (the group's checkpoint stays whole).
+int peek_patch_state(pgh_ctx* c, uint8_t* out, size_t n, int* ok) {
+    RC(need_slab(c));
+    if (!ok || !out) return fail(c, PGH_E_ARG, "out / ok is NULL");
+    *ok = 0;
+    for (pgh_ctx* k : G(c)->kids)
+        if (!pgh_int::peek_valid(k)) return PGH_OK;
+    RC(fan(c, [&](int, pgh_ctx* k) -> int { return pgh_int::peek_commit(k, out, n, out); }));
+    *ok = 1;
+    return PGH_OK;
+}
+
 int fold_unmark(pgh_ctx* c, int mark) {
     RC(need_slab(c));
     return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_unmark(k, mark); });

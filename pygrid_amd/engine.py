@@ -330,6 +330,17 @@ class Engine:
     def fold_unmark(self, mark: int):
         self._check(self._lib.pgh_fold_unmark(self._h, int(mark)), "fold_unmark")
 
+    def fold_peek(self, mode: int):
+        """The FINAL pass of the fold state as it stands, copied to the host behind it (async)."""
+        self._check(self._lib.pgh_fold_peek(self._h, int(mode)), "fold_peek")
+
+    def peek_patch_into(self, ptr: int, n: int) -> bool:
+        """If nothing changed since the last fold_peek: write the peeked payloads into the framed
+        message at ``ptr`` (n bytes), make the peeked result the resident checkpoint, return True."""
+        ok = C.c_int(0)
+        self._check(self._lib.pgh_peek_patch_state(self._h, C.c_void_p(ptr), n, C.byref(ok)), "peek_patch_state")
+        return bool(ok.value)
+
     def fold_busy(self) -> bool:
         """The last slot fold issued is still running (non-blocking)."""
         b = C.c_int(0)

@@ -88,7 +88,7 @@ class IncrementalCycle:
                  weights_by_worker: Optional[Dict[object, float]] = None, checkpoint: Optional[bytes] = None,
                  early_fold: bool = True, speculate: Optional[bool] = None,
                  speculation_budget: int = DEFAULT_SPECULATION_BUDGET, mark_every: int = 8, lazy: bool = True,
-                 min_gap_ms: float = 2.0):
+                 min_gap_ms: float = 2.0, peek: bool = True):
         self.engine = engine
         self.mode = mode
         self._numel = tuple(int(n) for n in numel)
@@ -107,6 +107,10 @@ class IncrementalCycle:
         # back to back would otherwise queue re-folds that the next report discards)
         self._lazy = bool(lazy) and hasattr(engine, "fold_busy")
         self.min_gap_s = max(0.0, float(min_gap_ms)) / 1e3
+        # speculative close: the FINAL pass of the fold state peeked ahead (pgh_fold_peek) whenever
+        # every reporter is folded; a close that finds nothing changed commits it
+        self._peek = self.speculate and bool(peek) and hasattr(engine, "fold_peek")
+        self._peeked = None  # (fold length, rewinds) of the last peek
         self._last_report = None
         self._hurried = False  # the last report came less than min_gap after the one before
         if speculate and not self.speculate:
@@ -329,6 +333,11 @@ class IncrementalCycle:
             self._fold_run(run, certain)
         if self.speculate:
             self._advance_base(certain)
+            if self._peek and self._prepared is not None and self._folded and self._folded == plan \
+                    and self._peeked != (len(self._folded), self.rewinds):
+                # every reporter so far is folded: take the close's FINAL pass now, in the background
+                self.engine.fold_peek(self.mode)
+                self._peeked = (len(self._folded), self.rewinds)
 
     def _fold_run(self, ws: Sequence, certain: int = 0):
         slots = [self._slot_of[w] for w in ws]
@@ -473,15 +482,23 @@ class IncrementalCycle:
                 log.info("re-folding the cycle in the DB's order: %s", refold)
                 self.engine.fold_restart()
                 self._weights = []
-            stats = self._fold_in_order(rest, fetch)
-            self._drop_marks()  # after the FINAL pass: it reads a rewound state from its mark in place
-            stats.update(refold=bool(refold), reason=refold or None, early=k, n=len(order),
-                         folded_before_close=folded_before, rewinds=self.rewinds)
-            self.last_close = stats
             prep = self._prepared[1] if self._prepared and self._prepared[0] is checkpoint else None
             self._prepared = None
-            new = (state_codec.fresh_checkpoint(self.engine, checkpoint, prepared=prep) if framing == "fresh"
-                   else self.engine.ckpt_patch_state(checkpoint))
+            # nothing left to fold and the last peek still matches: its result IS the new checkpoint
+            peeked = bool(not refold and not rest and framing == "fresh" and prep is not None and prep[1]
+                          and self._peek and self.engine.peek_patch_into(prep[1], len(prep[0])))
+            if peeked:
+                stats = {"from_hbm": 0, "from_host": 0, "from_db": 0}
+                new = prep[0]
+            else:
+                stats = self._fold_in_order(rest, fetch)
+            self._drop_marks()  # after the FINAL pass: it reads a rewound state from its mark in place
+            stats.update(refold=bool(refold), reason=refold or None, early=k, n=len(order),
+                         folded_before_close=folded_before, rewinds=self.rewinds, peeked=peeked)
+            self.last_close = stats
+            if not peeked:
+                new = (state_codec.fresh_checkpoint(self.engine, checkpoint, prepared=prep) if framing == "fresh"
+                       else self.engine.ckpt_patch_state(checkpoint))
             self.engine.ckpt_owner = self
             self.engine.ckpt_bytes = new
             return new

@@ -1,0 +1,93 @@
+"""GPU: the speculative close (pgh_fold_peek / pgh_peek_patch_state).  Whenever every reporter is
+folded, IncrementalCycle takes the close's FINAL pass ahead (into a buffer of its own, copied to the
+host behind it); a close that finds nothing changed commits it -- the new checkpoint bytes come from
+that copy and the peeked result becomes the resident checkpoint.  Bit-exact against the oracle in
+every mode, on one GPU and on groups, chained over cycles, and when the peek goes stale (a later
+report, a DB order that differs, a checkpoint handed over anew)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+SHAPES = [(300, 41), (41,), (7, 300), (7,)]
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _want(mode, ckpt, rows, weights=None):
+    if mode == 0:
+        return O.fedavg_mean(ckpt, rows)
+    if mode == 1:
+        return O.fedavg_iterative(ckpt, rows)
+    return O.fedavg_weighted(ckpt, rows, np.array(weights, F))
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_committed_peek_is_bit_exact_and_chains(devices, mode):
+    from pygrid_amd import Engine
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(800 + mode)
+    numel = [int(np.prod(s)) for s in SHAPES]
+    ckpt = [rng.standard_normal(s).astype(F) for s in SHAPES]
+    ck = build_state_fast(ckpt)
+    weights = {w: float(rng.uniform(0.5, 2.0)) for w in range(12)}
+    eng = Engine(devices=devices) if devices else Engine(0)
+    try:
+        want = ckpt
+        for cyc in range(3):
+            diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES] for w in range(12)}
+            reporters = [w for w in range(12) if w % 4 != 1]
+            inc = IncrementalCycle(eng, numel, mode=mode, slots=16, checkpoint=ck, lazy=False,
+                                   weights_by_worker=weights if mode == 2 else None)
+            for w in range(12):
+                inc.assigned(w)
+            for w in rng.permutation(reporters):
+                inc.reported(int(w), build_state_fast(diffs[int(w)]))
+            new = inc.close(ck)
+            assert inc.last_close["peeked"], inc.last_close
+            want = _want(mode, want, [diffs[w] for w in reporters], [weights[w] for w in reporters])
+            for g, w in zip(parse_state(new), want):
+                assert np.array_equal(bits(g), bits(w)), cyc
+            ck = new  # the next cycle starts from the committed resident checkpoint, no upload
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("case", ["late_report", "db_order", "new_checkpoint", "no_peek"])
+def test_stale_peek_falls_back_bit_exact(case):
+    from pygrid_amd import Engine
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(810)
+    numel = [int(np.prod(s)) for s in SHAPES]
+    ckpt = [rng.standard_normal(s).astype(F) for s in SHAPES]
+    ck = build_state_fast(ckpt)
+    diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES] for w in range(8)}
+    with Engine(0) as eng:
+        inc = IncrementalCycle(eng, numel, slots=10, checkpoint=ck, lazy=False, peek=case != "no_peek")
+        for w in range(8):
+            inc.assigned(w)
+        for w in (5, 2, 0, 3):
+            inc.reported(w, build_state_fast(diffs[w]))
+        order = [0, 2, 3, 5]
+        if case == "late_report":  # a report after the last peek: the close folds it (no commit)
+            inc._lazy, inc.min_gap_s = True, 10.0  # it arrives "too soon": not folded, not peeked
+            inc.reported(7, build_state_fast(diffs[7]))
+            order = [0, 2, 3, 5, 7]
+        elif case == "db_order":
+            order = [0, 3, 2, 5]
+        close_ck = ck
+        if case == "new_checkpoint":  # the close gets other checkpoint bytes: uploaded, the peek is stale
+            close_ck = build_state_fast(ckpt)
+        new = inc.close(close_ck, order=order, fetch=lambda w: build_state_fast(diffs[w]))
+        assert not inc.last_close["peeked"]
+        for g, w in zip(parse_state(new), O.fedavg_mean(ckpt, [diffs[w] for w in order])):
+            assert np.array_equal(bits(g), bits(w)), case
