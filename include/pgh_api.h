@@ -233,7 +233,8 @@ int pgh_fold_unmark(pgh_ctx* ctx, int mark);
 int pgh_fold_busy(pgh_ctx* ctx, int* busy);
 /* Speculative close (ABI 6).  pgh_fold_peek runs the FINAL pass of the fold state as it stands --
  * ckpt - avg over the clients folded so far, into a buffer of its own -- and copies the result to a
- * pinned host buffer behind it (its own stream: beside the ingest DMAs), without ending the cycle.
+ * pinned host buffer behind it (its own stream: beside the ingest DMAs), without ending the cycle;
+ * while the previous peek's copy is still running it does nothing (there is no valid peek then).
  * pgh_peek_patch_state(out) then, if NOTHING changed since (no fold, rewind, restart, weights or
  * checkpoint change), writes this context's payload slices of the framed State message `out`
  * (pgh_state_fresh's framing) from that copy and makes the peeked result the resident checkpoint --

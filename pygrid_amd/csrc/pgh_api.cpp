@@ -2504,6 +2504,17 @@ int pgh_fold_peek(pgh_ctx* c, int mode) {
     FinalArgs fa;
     RC(fedavg_divisor(c, mode, c->folded, &fa.divisor));
     DeviceGuard g(c->device);
+    if (c->peek_stream) {
+        // the previous peek's copy still running (reports arriving faster than 47 MB cross PCIe):
+        // skip this one rather than stall the fold stream behind it -- the close then folds itself
+        const hipError_t q = hipEventQuery(c->peek_ev);
+        if (q == hipErrorNotReady) {
+            (void)hipGetLastError();
+            c->peek_gen = 0;
+            return PGH_OK;
+        }
+        if (q != hipSuccess) return fail(c, PGH_E_HIP, "hipEventQuery failed: %s", hipGetErrorString(q));
+    }
     if (!c->peek_stream) {
         CK(c, hipStreamCreateWithFlags(&c->peek_stream, hipStreamNonBlocking));
         CK(c, hipEventCreateWithFlags(&c->peek_ev, hipEventDisableTiming));
@@ -2525,8 +2536,7 @@ int pgh_fold_peek(pgh_ctx* c, int mode) {
         }
         c->peek_cap = (size_t)c->pg;
     }
-    const hipStream_t s = c->stream;
-    if (c->peek_gen) CK(c, hipStreamWaitEvent(s, c->peek_ev, 0));  // the last peek's D2H reads d_peek
+    const hipStream_t s = c->stream;  // (the last peek's D2H from d_peek has finished: queried above)
     pgh::FedavgArgs a{};
     a.diffs = (const float*)c->d_slab;
     a.map = slab_map(c);
