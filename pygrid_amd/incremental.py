@@ -336,8 +336,12 @@ class IncrementalCycle:
             if self._peek and self._prepared is not None and self._folded and self._folded == plan \
                     and self._peeked != (len(self._folded), self.rewinds):
                 # every reporter so far is folded: take the close's FINAL pass now, in the background
-                self.engine.fold_peek(self.mode)
-                self._peeked = (len(self._folded), self.rewinds)
+                try:
+                    self.engine.fold_peek(self.mode)
+                    self._peeked = (len(self._folded), self.rewinds)
+                except AggregationError as e:  # e.g. no HBM for the peek buffer: close the usual way
+                    log.warning("speculative close disabled for this cycle: %s", e)
+                    self._peek = False
 
     def _fold_run(self, ws: Sequence, certain: int = 0):
         slots = [self._slot_of[w] for w in ws]
