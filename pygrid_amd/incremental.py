@@ -384,7 +384,12 @@ class IncrementalCycle:
             i = min(range(1, len(self._marks)), key=lambda j: at[j + 1] - at[j - 1])
             self.engine.fold_unmark(self._marks.pop(i)[1])
         mid = next(self._mark_ids)
-        self.engine.fold_mark(mid)
+        try:
+            self.engine.fold_mark(mid)
+        except AggregationError as e:  # no HBM for another saved state: keep fewer from now on
+            log.warning("fold state not saved at %d (%s); speculation keeps %d saved states", n, e, len(self._marks))
+            self.max_marks = max(2, len(self._marks))
+            return
         self._marks.append((n, mid))
 
     def _advance_base(self, certain: int):

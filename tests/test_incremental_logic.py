@@ -736,3 +736,25 @@ def test_lazy_speculation_waits_for_slow_reports_and_an_idle_gpu(monkeypatch, ga
     assert (len(eng.state) > 1) == folds_during_reports
     inc.close(b"ck", framing="template")
     assert eng.result == [bytes([w]) for w in range(1, 8)]
+
+
+def test_out_of_hbm_for_saved_states_degrades_not_fails():
+    """pgh_fold_mark failing (no HBM for another saved state) keeps speculating with fewer saved
+    states; reports never fail for it and the close is still the reference's order."""
+    class TightEngine(SpecEngine):
+        def fold_mark(self, m):
+            if len(self.marks) >= 3:
+                raise AggregationError("fold state buffer allocation failed")
+            super().fold_mark(m)
+
+    rng = np.random.default_rng(77)
+    eng = TightEngine()
+    inc = IncrementalCycle(eng, [3], slots=40, mark_every=2)
+    for w in range(40):
+        inc.assigned(w)
+    reporters = [w for w in range(1, 40) if rng.random() >= 0.2]
+    for w in rng.permutation(reporters):
+        inc.reported(int(w), bytes([int(w)]))
+    assert len(eng.marks) <= 3 and inc.max_marks <= 3
+    inc.close(b"ck", framing="template")
+    assert eng.result == [bytes([w]) for w in sorted(reporters)]
