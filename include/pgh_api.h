@@ -241,6 +241,12 @@ int pgh_fold_busy(pgh_ctx* ctx, int* busy);
  * exactly as pgh_fold_slots_finish_resident(no slots) + pgh_ckpt_patch_state(out, out) would -- and
  * sets *ok = 1; otherwise *ok = 0 and nothing changes.  A group commits all of its GPUs or none. */
 int pgh_fold_peek(pgh_ctx* ctx, int mode);
+/* pgh_fold_peek, and then a host thread of the context copies the peek's payload slices into the
+ * framed message `out` (pgh_state_fresh's framing) as soon as the D2H lands, while the cycle is
+ * still open: a pgh_peek_patch_state(out) that commits this peek then only swaps buffers.  `out`
+ * must stay valid, and unread by the caller, until the next pgh_fold_peek* / pgh_peek_patch_state /
+ * pgh_reset / pgh_destroy returns. */
+int pgh_fold_peek_into(pgh_ctx* ctx, int mode, uint8_t* out, size_t n);
 int pgh_peek_patch_state(pgh_ctx* ctx, uint8_t* out, size_t n, int* ok);
 
 /* Z_2^64 share sum over all clients x parties, then decode float32(sum) / base**prec.

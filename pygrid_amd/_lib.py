@@ -112,6 +112,7 @@ SIGNATURES = {
     "pgh_fold_unmark": (_i, [_vp, _i]),
     "pgh_fold_busy": (_i, [_vp, C.POINTER(C.c_int)]),
     "pgh_fold_peek": (_i, [_vp, _i]),
+    "pgh_fold_peek_into": (_i, [_vp, _i, _vp, _sz]),
     "pgh_peek_patch_state": (_i, [_vp, _vp, _sz, C.POINTER(C.c_int)]),
     "pgh_ckpt_download": (_i, [_vp, _vp]),
     "pgh_ckpt_patch_state": (_i, [_vp, C.c_char_p, _sz, _vp]),

@@ -254,6 +254,18 @@ struct pgh_ctx {
     float* h_peek = nullptr;   // pinned, peek_cap floats
     size_t peek_cap = 0;
     float* d_peek = nullptr;   // [pvec]: the peeked new checkpoint (swapped with d_ckpt on commit)
+    // pgh_fold_peek_into: a host thread waits for the peek's D2H and copies its payload slices into
+    // the caller's framed output while the cycle is still open (the close then only commits)
+    std::thread pk_thread;
+    std::mutex pk_mu;
+    std::condition_variable pk_cv;
+    bool pk_stop = false, pk_busy = false;
+    uint64_t pk_gen = 0;       // peek the posted job copies
+    uint64_t pk_done_gen = 0;  // peek whose payloads are in pk_done_out
+    uint8_t* pk_out = nullptr;
+    const uint8_t* pk_done_out = nullptr;
+    std::vector<std::pair<uint8_t*, size_t>> pk_pieces;
+    std::unique_ptr<CopyPool> pool_peek;
     uint64_t state_gen = 1;
     uint64_t peek_gen = 0;  // state_gen the peek was taken at (0: none)
     // The last fold issued on each stream (folds may run on several caller streams at once, e.g.
@@ -444,8 +456,11 @@ double now_ms() {
 size_t esize(int dtype) { return dtype == PGH_F32 ? 4 : 8; }
 
 void release_slot_fold_events(pgh_ctx* c);
+void peek_job_wait(pgh_ctx* c);
+void peek_thread_stop(pgh_ctx* c);
 
 void free_slab(pgh_ctx* c) {
+    peek_job_wait(c);  // the peek thread reads h_peek
     if (c->peek_stream) (void)hipStreamSynchronize(c->peek_stream);  // a peek's D2H reads d_peek
     (void)hipFree(c->d_peek); c->d_peek = nullptr;
     if (c->h_peek) (void)hipHostFree(c->h_peek);
@@ -1471,6 +1486,7 @@ void pgh_destroy(pgh_ctx* c) {
     if (c->grp) { pgh_group_api::destroy(c); return; }
     DeviceGuard g(c->device);
     free_slab(c);
+    peek_thread_stop(c);
     for (auto& t : c->pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto e : c->pool) (void)hipEventDestroy(e);
     clear_marks(c);
@@ -1591,6 +1607,7 @@ int pgh_reset(pgh_ctx* c) {
     clear_marks(c);
     drop_fold_marks(c);
     release_slot_fold_events(c);  // c->stream is idle (synchronised above)
+    peek_job_wait(c);             // the caller may drop the output a peek is copying into after this
     ++c->state_gen;
     std::fill(c->slot_client.begin(), c->slot_client.end(), -1);
     c->weights.clear();
@@ -2201,6 +2218,7 @@ int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out
     std::vector<std::pair<size_t, size_t>> spans;
     RC(state_shard_spans(c, tmpl, n, &spans, "checkpoint template"));
     DeviceGuard g(c->device);
+    peek_job_wait(c);  // a peek's payload copy may still be writing the same output
     std::vector<CopyPool::Seg> gaps;
     bool ordered = true;
     if (out != tmpl) {  // template bytes outside this shard's payload slices (framing, other shards)
@@ -2492,6 +2510,59 @@ int pgh_fold_unmark(pgh_ctx* c, int mark) {
 }
 
 // ---- speculative close: the FINAL pass of the fold state as it stands, ahead of the close -----------
+namespace {
+// Wait until the peek thread is idle (its copy read h_peek and wrote the caller's buffer).
+void peek_job_wait(pgh_ctx* c) {
+    std::unique_lock<std::mutex> lk(c->pk_mu);
+    c->pk_cv.wait(lk, [c] { return !c->pk_busy; });
+}
+
+void peek_thread_main(pgh_ctx* c) {
+    (void)hipSetDevice(c->device);
+    for (;;) {
+        uint8_t* out = nullptr;
+        std::vector<std::pair<uint8_t*, size_t>> pieces;
+        uint64_t gen = 0;
+        {
+            std::unique_lock<std::mutex> lk(c->pk_mu);
+            c->pk_cv.wait(lk, [c] { return c->pk_stop || (c->pk_busy && c->pk_out); });
+            if (c->pk_stop) return;
+            out = c->pk_out;
+            pieces.swap(c->pk_pieces);
+            gen = c->pk_gen;
+        }
+        bool ok = hipEventSynchronize(c->peek_ev) == hipSuccess;
+        if (ok) {
+            std::vector<OutPiece> op;
+            size_t total = 0;
+            for (auto& pc : pieces) {
+                op.push_back(OutPiece{pc.first, pc.second});
+                total += pc.second;
+            }
+            scatter_out((const uint8_t*)c->h_peek, 0, total, op, *c->pool_peek);
+        }
+        {
+            std::lock_guard<std::mutex> lk(c->pk_mu);
+            c->pk_done_gen = ok ? gen : 0;
+            c->pk_done_out = out;
+            c->pk_out = nullptr;
+            c->pk_busy = false;
+        }
+        c->pk_cv.notify_all();
+    }
+}
+
+void peek_thread_stop(pgh_ctx* c) {
+    if (!c->pk_thread.joinable()) return;
+    {
+        std::lock_guard<std::mutex> lk(c->pk_mu);
+        c->pk_stop = true;
+    }
+    c->pk_cv.notify_all();
+    c->pk_thread.join();
+}
+}  // namespace
+
 int pgh_fold_peek(pgh_ctx* c, int mode) {
     if (c && c->grp) return pgh_group_api::fold_peek(c, mode);
     if (!c) return PGH_E_ARG;
@@ -2508,8 +2579,13 @@ int pgh_fold_peek(pgh_ctx* c, int mode) {
         // the previous peek's copy still running (reports arriving faster than 47 MB cross PCIe):
         // skip this one rather than stall the fold stream behind it -- the close then folds itself
         const hipError_t q = hipEventQuery(c->peek_ev);
-        if (q == hipErrorNotReady) {
-            (void)hipGetLastError();
+        bool busy = q == hipErrorNotReady;
+        if (busy) (void)hipGetLastError();
+        {
+            std::lock_guard<std::mutex> lk(c->pk_mu);
+            busy = busy || c->pk_busy;
+        }
+        if (busy) {
             c->peek_gen = 0;
             return PGH_OK;
         }
@@ -2536,6 +2612,7 @@ int pgh_fold_peek(pgh_ctx* c, int mode) {
         }
         c->peek_cap = (size_t)c->pg;
     }
+    peek_job_wait(c);  // the last peek's payload copy reads h_peek
     const hipStream_t s = c->stream;  // (the last peek's D2H from d_peek has finished: queried above)
     pgh::FedavgArgs a{};
     a.diffs = (const float*)c->d_slab;
@@ -2563,6 +2640,28 @@ int pgh_fold_peek(pgh_ctx* c, int mode) {
     return PGH_OK;
 }
 
+
+int pgh_fold_peek_into(pgh_ctx* c, int mode, uint8_t* out, size_t n) {
+    if (c && c->grp) return pgh_group_api::fold_peek_into(c, mode, out, n);
+    if (!c) return PGH_E_ARG;
+    std::vector<std::pair<size_t, size_t>> spans;
+    if (out) RC(state_shard_spans(c, out, n, &spans, "peek output frame"));
+    RC(pgh_fold_peek(c, mode));
+    if (!out || !pgh_int::peek_valid(c)) return PGH_OK;  // skipped: nothing to copy
+    if (!c->pool_peek) c->pool_peek.reset(new CopyPool(4, c->local_cpus));
+    if (!c->pk_thread.joinable()) c->pk_thread = std::thread(peek_thread_main, c);
+    {
+        std::lock_guard<std::mutex> lk(c->pk_mu);
+        c->pk_pieces.clear();
+        for (auto& sp : spans) c->pk_pieces.push_back({out + sp.first, sp.second});
+        c->pk_out = out;
+        c->pk_gen = c->peek_gen;
+        c->pk_done_gen = 0;
+        c->pk_busy = true;
+    }
+    c->pk_cv.notify_all();
+    return PGH_OK;
+}
 
 int pgh_peek_patch_state(pgh_ctx* c, uint8_t* out, size_t n, int* ok) {
     if (c && c->grp) return pgh_group_api::peek_patch_state(c, out, n, ok);
@@ -2797,6 +2896,22 @@ int peek_commit(pgh_ctx* c, const uint8_t* out_frame, size_t n, uint8_t* out) {
     std::vector<std::pair<size_t, size_t>> spans;
     RC(state_shard_spans(c, out_frame, n, &spans, "peeked checkpoint frame"));
     DeviceGuard g(c->device);
+    peek_job_wait(c);
+    bool copied;
+    {
+        std::lock_guard<std::mutex> lk(c->pk_mu);
+        copied = c->pk_done_gen == c->peek_gen && c->pk_done_out == out;
+    }
+    if (copied) {  // the peek thread already put this peek's payloads into `out`
+        std::swap(c->d_ckpt, c->d_peek);
+        c->acc_src = nullptr;
+        c->folded = 0;
+        c->st.n_folded = 0;
+        c->slot_mode = -1;
+        c->peek_gen = 0;
+        ++c->state_gen;
+        return PGH_OK;
+    }
     CK(c, hipEventSynchronize(c->peek_ev));
     std::vector<OutPiece> pieces;
     size_t total = 0;
@@ -2887,6 +3002,7 @@ void* vec(pgh_ctx* c, int which) {
     }
 }
 int patch_payloads(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out) {
+    peek_job_wait(c);  // a peek's payload copy may still be writing the same output
     RC(check_dtype(c, PGH_F32));
     if (!tmpl || !out) return fail(c, PGH_E_ARG, "tmpl / out is NULL");
     RC(check_ckpt(c, "pgh_ckpt_patch_state"));

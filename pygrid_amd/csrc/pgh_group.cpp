@@ -832,6 +832,11 @@ int fold_peek(pgh_ctx* c, int mode) {
     return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_peek(k, mode); });
 }
 
+int fold_peek_into(pgh_ctx* c, int mode, uint8_t* out, size_t n) {
+    RC(need_slab(c));
+    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_peek_into(k, mode, out, n); });
+}
+
 // All children's peeks must still hold, or none is committed (the group's checkpoint stays whole).
 int peek_patch_state(pgh_ctx* c, uint8_t* out, size_t n, int* ok) {
     RC(need_slab(c));

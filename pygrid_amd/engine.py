@@ -330,9 +330,17 @@ class Engine:
     def fold_unmark(self, mark: int):
         self._check(self._lib.pgh_fold_unmark(self._h, int(mark)), "fold_unmark")
 
-    def fold_peek(self, mode: int):
-        """The FINAL pass of the fold state as it stands, copied to the host behind it (async)."""
-        self._check(self._lib.pgh_fold_peek(self._h, int(mode)), "fold_peek")
+    def fold_peek(self, mode: int, into=None):
+        """The FINAL pass of the fold state as it stands, copied to the host behind it (async).
+        ``into``: (bytes, address) of a framed output (``state.prepared_fresh_frame``): a library
+        thread also copies the payloads into it while the cycle is still open; the engine keeps
+        the bytes alive until the next peek."""
+        if into is None:
+            self._check(self._lib.pgh_fold_peek(self._h, int(mode)), "fold_peek")
+            return
+        buf, ptr = into
+        self._check(self._lib.pgh_fold_peek_into(self._h, int(mode), C.c_void_p(ptr), len(buf)), "fold_peek_into")
+        self._peek_keep = buf
 
     def peek_patch_into(self, ptr: int, n: int) -> bool:
         """If nothing changed since the last fold_peek: write the peeked payloads into the framed

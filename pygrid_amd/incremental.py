@@ -337,7 +337,7 @@ class IncrementalCycle:
                     and self._peeked != (len(self._folded), self.rewinds):
                 # every reporter so far is folded: take the close's FINAL pass now, in the background
                 try:
-                    self.engine.fold_peek(self.mode)
+                    self.engine.fold_peek(self.mode, into=self._prepared[1] if self._prepared[1][1] else None)
                     self._peeked = (len(self._folded), self.rewinds)
                 except AggregationError as e:  # e.g. no HBM for the peek buffer: close the usual way
                     log.warning("speculative close disabled for this cycle: %s", e)
