@@ -244,8 +244,9 @@ int pgh_fold_peek(pgh_ctx* ctx, int mode);
 /* pgh_fold_peek, and then a host thread of the context copies the peek's payload slices into the
  * framed message `out` (pgh_state_fresh's framing) as soon as the D2H lands, while the cycle is
  * still open: a pgh_peek_patch_state(out) that commits this peek then only swaps buffers.  `out`
- * must stay valid, and unread by the caller, until the next pgh_fold_peek* / pgh_peek_patch_state /
- * pgh_reset / pgh_destroy returns. */
+ * must stay valid, and unread by the caller, until the next pgh_fold_peek_into with another output,
+ * pgh_peek_patch_state, pgh_ckpt_patch_state, pgh_reset or pgh_destroy returns (each waits for the
+ * copy). */
 int pgh_fold_peek_into(pgh_ctx* ctx, int mode, uint8_t* out, size_t n);
 int pgh_peek_patch_state(pgh_ctx* ctx, uint8_t* out, size_t n, int* ok);
 

@@ -2646,6 +2646,12 @@ int pgh_fold_peek_into(pgh_ctx* c, int mode, uint8_t* out, size_t n) {
     if (!c) return PGH_E_ARG;
     std::vector<std::pair<size_t, size_t>> spans;
     if (out) RC(state_shard_spans(c, out, n, &spans, "peek output frame"));
+    {
+        // a copy into another output (a cycle that ended without a close) finishes first: the
+        // caller keeps only the output of its latest peek alive
+        std::unique_lock<std::mutex> lk(c->pk_mu);
+        c->pk_cv.wait(lk, [c, out] { return !c->pk_busy || c->pk_out == out; });
+    }
     RC(pgh_fold_peek(c, mode));
     if (!out || !pgh_int::peek_valid(c)) return PGH_OK;  // skipped: nothing to copy
     if (!c->pool_peek) c->pool_peek.reset(new CopyPool(4, c->local_cpus));
@@ -2667,7 +2673,10 @@ int pgh_peek_patch_state(pgh_ctx* c, uint8_t* out, size_t n, int* ok) {
     if (c && c->grp) return pgh_group_api::peek_patch_state(c, out, n, ok);
     if (!c || !ok || !out) return PGH_E_ARG;
     *ok = 0;
-    if (!pgh_int::peek_valid(c)) return PGH_OK;
+    if (!pgh_int::peek_valid(c)) {
+        peek_job_wait(c);  // the caller may reuse `out` once this returns
+        return PGH_OK;
+    }
     const double t0 = now_ms();
     RC(pgh_int::peek_commit(c, out, n, out));
     c->st.close_ms_last = now_ms() - t0;
@@ -2891,6 +2900,8 @@ int pgh_sync(pgh_ctx* c) {
 
 namespace pgh_int {
 bool peek_valid(const pgh_ctx* c) { return c->peek_gen != 0 && c->peek_gen == c->state_gen; }
+
+void peek_wait(pgh_ctx* c) { peek_job_wait(c); }
 
 int peek_commit(pgh_ctx* c, const uint8_t* out_frame, size_t n, uint8_t* out) {
     std::vector<std::pair<size_t, size_t>> spans;

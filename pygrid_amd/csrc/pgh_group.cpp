@@ -843,7 +843,10 @@ int peek_patch_state(pgh_ctx* c, uint8_t* out, size_t n, int* ok) {
     if (!ok || !out) return fail(c, PGH_E_ARG, "out / ok is NULL");
     *ok = 0;
     for (pgh_ctx* k : G(c)->kids)
-        if (!pgh_int::peek_valid(k)) return PGH_OK;
+        if (!pgh_int::peek_valid(k)) {
+            for (pgh_ctx* w : G(c)->kids) pgh_int::peek_wait(w);  // the caller may reuse `out` now
+            return PGH_OK;
+        }
     RC(fan(c, [&](int, pgh_ctx* k) -> int { return pgh_int::peek_commit(k, out, n, out); }));
     *ok = 1;
     return PGH_OK;

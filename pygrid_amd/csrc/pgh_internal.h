@@ -44,6 +44,8 @@ int patch_payloads(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out);
 // Speculative close: a peek (pgh_fold_peek) still matches the fold state; commit it -- this shard's
 // payload slices of the framed message `out` from the peek, the peeked result becomes the checkpoint.
 bool peek_valid(const pgh_ctx* c);
+// Wait until the context's peek thread has finished copying into a caller's output.
+void peek_wait(pgh_ctx* c);
 int peek_commit(pgh_ctx* c, const uint8_t* out_frame, size_t n, uint8_t* out);
 }  // namespace pgh_int
 

@@ -91,3 +91,37 @@ def test_stale_peek_falls_back_bit_exact(case):
         assert not inc.last_close["peeked"]
         for g, w in zip(parse_state(new), O.fedavg_mean(ckpt, [diffs[w] for w in order])):
             assert np.array_equal(bits(g), bits(w)), case
+
+
+def test_abandoned_cycle_peek_copy_finishes_before_the_next_peek():
+    """A cycle whose peek copy is still running is dropped without a close (the node fell back to
+    the DB path); the next cycle's peek into another output waits for that copy, so the dropped
+    output can be freed, and its own close is bit-exact."""
+    import gc
+
+    from pygrid_amd import Engine
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    shapes = [(2048, 2048), (41,)]
+    rng = np.random.default_rng(820)
+    numel = [int(np.prod(s)) for s in shapes]
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    ck = build_state_fast(ckpt)
+    with Engine(0) as eng:
+        for cyc in range(3):
+            diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in range(4)}
+            inc = IncrementalCycle(eng, numel, slots=6, checkpoint=ck, lazy=False)
+            for w in range(4):
+                inc.assigned(w)
+            for w in (2, 0, 3, 1):
+                inc.reported(w, build_state_fast(diffs[w]))
+            if cyc < 2:
+                del inc  # dropped with its peek copy in flight
+                gc.collect()
+                continue
+            new = inc.close(ck)
+            assert inc.last_close["peeked"], inc.last_close
+            want = O.fedavg_mean(ckpt, [diffs[w] for w in range(4)])
+            for g, w in zip(parse_state(new), want):
+                assert np.array_equal(bits(g), bits(w))
