@@ -125,3 +125,31 @@ def test_abandoned_cycle_peek_copy_finishes_before_the_next_peek():
             want = O.fedavg_mean(ckpt, [diffs[w] for w in range(4)])
             for g, w in zip(parse_state(new), want):
                 assert np.array_equal(bits(g), bits(w))
+
+
+def test_peek_into_another_output_while_a_copy_runs():
+    """Engine level: a second peek into another output while the first peek's payload copy may still
+    run waits for it, then copies its own; committing the second is bit-exact."""
+    from pygrid_amd import Engine
+    from pygrid_amd import state as state_codec
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    shapes = [(2048, 2048), (41,)]
+    rng = np.random.default_rng(830)
+    numel = [int(np.prod(s)) for s in shapes]
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    ck = build_state_fast(ckpt)
+    diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in range(3)}
+    with Engine(0) as eng:
+        inc = IncrementalCycle(eng, numel, slots=5, checkpoint=ck, lazy=False)
+        for w in range(3):
+            inc.assigned(w)
+        for w in (1, 2, 0):
+            inc.reported(w, build_state_fast(diffs[w]))  # the last one peeks into the cycle's output
+        other = state_codec.prepared_fresh_frame(ck)
+        eng.fold_peek(0, into=other)
+        assert eng.peek_patch_into(other[1], len(other[0]))
+        want = O.fedavg_mean(ckpt, [diffs[w] for w in range(3)])
+        for g, w in zip(parse_state(bytes(other[0])), want):
+            assert np.array_equal(bits(g), bits(w))
