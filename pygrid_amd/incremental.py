@@ -21,7 +21,8 @@ diff lives from WHEN it is folded:
   (``pgh_fold_mark``); when an earlier worker reports after all, or a kept one re-reports, the fold
   goes back to the last saved state before its position (``pgh_fold_rewind``) and continues; slots
   before the last saved state at the certain point are freed.  While the GPU is still busy with the
-  previous fold, a report is folded with a later one (``pgh_fold_busy``).  Certain-only folds
+  previous fold (``pgh_fold_busy``), or reports arrive less than ``min_gap_ms`` apart, a report is
+  folded with a later one -- or by a timer once the reports pause.  Certain-only folds
   (``speculate=False``): the certain prefix is folded ``fold_batch`` at a time and freed
   (``pgh_fold_slots``);
 * ``close(checkpoint, order=..., fetch=...)`` takes the AUTHORITATIVE order -- the keys of the
@@ -31,7 +32,11 @@ diff lives from WHEN it is folded:
   reported before a restart).  When even that is impossible (the order differs inside the freed
   prefix, a freed worker re-reported, an assignment arrived behind it) the fold restarts
   (``pgh_fold_slots_restart``) and re-folds the whole order, the folded diffs fetched from the DB:
-  bit-identical to the reference in every case, early folding is only ever a speedup.
+  bit-identical to the reference in every case, early folding is only ever a speedup;
+* speculative close (``peek=True``): whenever every reporter is folded, the close's FINAL pass,
+  its D2H and the copy of the payloads into the cycle's prepared output bytes run ahead
+  (``pgh_fold_peek_into``); a close whose order and fold state match that peek only commits it
+  (``pgh_peek_patch_state``), any other close folds and copies as usual.
 
 Report semantics (``cycle_manager.py:162-174``, ``fl_events.py:257-263``):
 
@@ -49,8 +54,8 @@ Report semantics (``cycle_manager.py:162-174``, ``fl_events.py:257-263``):
   reference's close does (its ``unserialize_model_params`` raises).
 
 Thread safety: the node calls ``reported`` from request handlers and ``close`` from its executor
-thread (``tasks/cycle.py``), so every method holds the cycle's lock (the engine context itself is
-single-owner).  A well-formed diff holding non-float32 tensors is accepted (the reference would
+thread (``tasks/cycle.py``), and the deferred fold runs on a timer thread, so every method holds
+the cycle's lock (the engine context itself is single-owner).  A well-formed diff holding non-float32 tensors is accepted (the reference would
 average it with torch's type promotion): the cycle is then declined as a whole -- later reports
 are only recorded, and ``close`` raises ``ModelNotAcceleratedError`` so the node averages the cycle
 with its own code, from its DB.
@@ -75,6 +80,7 @@ DEFAULT_HBM_BUDGET = 64 << 30  # bytes of diffs kept in HBM per cycle when `slot
 MAX_DEFAULT_SLOTS = 4096
 DEFAULT_SPECULATION_BUDGET = 16 << 30  # bytes of HBM for saved fold states (speculative folds)
 MAX_MARKS = 256
+DEFER_LIMIT = 500  # timer re-arms after a report (min_gap each) before the close is left to fold
 
 log = logging.getLogger(__name__)
 
@@ -113,6 +119,8 @@ class IncrementalCycle:
         self._peeked = None  # (fold length, rewinds) of the last peek
         self._last_report = None
         self._hurried = False  # the last report came less than min_gap after the one before
+        self._timer: Optional[threading.Timer] = None  # folds what a lazy skip left once reports pause
+        self._defer_left = 0
         if speculate and not self.speculate:
             raise AggregationError("speculative folds need an engine with fold marks and HBM for >= 2 of them "
                                    f"({self.max_marks} fit in the budget)")
@@ -207,6 +215,7 @@ class IncrementalCycle:
             now = time.monotonic()
             self._hurried = self._last_report is not None and now - self._last_report < self.min_gap_s
             self._last_report = now
+            self._defer_left = DEFER_LIMIT
             if worker in self._folded_set:
                 # its earlier diff is in the fold state: go back to before it (its slot is still
                 # held), or -- when it was folded for good -- the close re-folds from the DB
@@ -308,8 +317,9 @@ class IncrementalCycle:
             return  # the early fold is not the plan's prefix any more: the close re-folds
         if self.speculate and self._lazy and not self._parked and (self._hurried or self.engine.fold_busy()):
             # reports arriving faster than a re-fold takes, or the GPU still folding: fold this
-            # report with a later one (or at close) instead of queueing re-folds the next report
-            # throws away
+            # report with a later one instead of queueing re-folds the next report throws away;
+            # if none comes within min_gap, a timer folds it (before the close, when that is later)
+            self._defer()
             return
         run: List = []
         for w in target[len(self._folded):]:
@@ -342,6 +352,35 @@ class IncrementalCycle:
                 except AggregationError as e:  # e.g. no HBM for the peek buffer: close the usual way
                     log.warning("speculative close disabled for this cycle: %s", e)
                     self._peek = False
+
+    def _defer(self):
+        if self._timer is None and self._defer_left > 0:
+            self._defer_left -= 1
+            self._timer = threading.Timer(max(self.min_gap_s, 1e-3), self._deferred)
+            self._timer.daemon = True
+            self._timer.start()
+
+    def _deferred(self):
+        """Timer thread: the reports paused (no new one within min_gap) -- fold what the lazy skips
+        left, as a report arriving then would have; while the GPU is still folding, wait again."""
+        with self._lock:
+            self._timer = None
+            if self._closed or self._stale or self._declined:
+                return
+            if self._last_report is not None and time.monotonic() - self._last_report < self.min_gap_s:
+                self._defer()  # still arriving
+                return
+            self._hurried = False
+            try:
+                self._sync()
+            except Exception as e:  # noqa: BLE001 -- nobody to raise to: the close re-folds from the DB
+                log.warning("deferred fold failed (%s): the close re-folds this cycle", e)
+                self._stale = f"deferred fold failed: {e}"
+
+    def _cancel_timer(self):
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
 
     def _fold_run(self, ws: Sequence, certain: int = 0):
         slots = [self._slot_of[w] for w in ws]
@@ -451,6 +490,7 @@ class IncrementalCycle:
             if self._closed:
                 raise AggregationError("cycle already closed")
             self._closed = True
+            self._cancel_timer()
             if self._declined:
                 raise ModelNotAcceleratedError(self._declined)
             if order is None:
@@ -569,6 +609,7 @@ class IncrementalCycle:
         reports are ignored and ``close`` raises; the node closes this cycle from its DB rows."""
         with self._lock:
             self._closed = True
+            self._cancel_timer()
             self._slot_of.clear()
             self._parked.clear()
             self._marks = []

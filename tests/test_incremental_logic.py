@@ -758,3 +758,38 @@ def test_out_of_hbm_for_saved_states_degrades_not_fails():
     assert len(eng.marks) <= 3 and inc.max_marks <= 3
     inc.close(b"ck", framing="template")
     assert eng.result == [bytes([w]) for w in sorted(reporters)]
+
+
+def test_lazy_skips_are_folded_by_a_timer_once_reports_pause(monkeypatch):
+    """Reports back to back leave their folds to a later report; when none comes within min_gap (the
+    close comes later, e.g. at the cycle's end), a timer folds them -- and waits while the GPU is
+    still busy -- so the close finds the fold done.  The result is unchanged."""
+    import time as _time
+
+    import pygrid_amd.incremental as inc_mod
+
+    clock = [100.0]
+    monkeypatch.setattr(inc_mod.time, "monotonic", lambda: clock[0])
+    eng = BusySpecEngine()
+    eng.busy = True
+    inc = IncrementalCycle(eng, [3], slots=16, min_gap_ms=2.0)
+    for w in range(8):
+        inc.assigned(w)
+    for w in (3, 1, 0, 6, 2, 5, 7, 4):
+        clock[0] += 0.5e-3
+        inc.reported(w, bytes([w]))
+    assert len(eng.state) <= 1  # nothing folded while the reports came back to back
+    _time.sleep(0.05)
+    assert len(eng.state) <= 1  # the fake clock says the reports are still arriving
+    clock[0] += 0.01
+    _time.sleep(0.05)
+    assert len(eng.state) <= 1  # paused, but the GPU is still busy
+    eng.busy = False
+    deadline = _time.time() + 5
+    while len(eng.state) < 8 and _time.time() < deadline:
+        _time.sleep(0.01)
+    assert len(eng.state) == 8, eng.state  # folded by the timer
+    inc.close(b"ck", framing="template")
+    assert inc.last_close["folded_before_close"] == 8
+    assert eng.result == [bytes([w]) for w in range(8)]
+    assert inc._timer is None
