@@ -110,6 +110,9 @@ def parse():
     ap.add_argument("--report-gap-ms", type=float, default=0.0,
                     help="resnet18-report: pause between reports (0: back to back; a node decodes each report's "
                          "base64 for ~4-7 ms anyway, tools/node_sim.py)")
+    ap.add_argument("--close-gap-ms", type=float, default=0.0,
+                    help="resnet18-report: pause between the last report and the close (the cycle's end "
+                         "comes later than its last report; 0: at once)")
     ap.add_argument("--sync-before-close", action="store_true",
                     help="resnet18-report: wait for the GPU before the close and time that wait apart")
     ap.add_argument("--eager-speculate", action="store_true",
@@ -1041,6 +1044,8 @@ def run_resnet18_report(ctx, args, eng, N):
             inc.reported(w, distinct[w % 4])
             if args.report_gap_ms:
                 time.sleep(args.report_gap_ms / 1e3)
+        if args.close_gap_ms:
+            time.sleep(args.close_gap_ms / 1e3)
         early.append(inc.n_folded)
         t0 = time.perf_counter()
         if args.sync_before_close:  # the GPU work the reports left queued, timed apart from the close call
@@ -1078,6 +1083,7 @@ def run_resnet18_report(ctx, args, eng, N):
              "rows_folded_at_close": int(np.median(at_close)) if at_close else 0,
              "speculative_folds": not args.no_speculate,
              "report_gap_ms": args.report_gap_ms,
+             "close_gap_ms": args.close_gap_ms,
              "pending_gpu_ms_at_close": [round(x, 3) for x in pending] if pending else None,
              "rewinds_per_cycle": float(np.median(rewinds)) if rewinds else 0,
              "h2d_GBps": round(st["h2d_bytes_total"] / (st["h2d_ms_total"] / 1e3) / 1e9, 2) if st["h2d_ms_total"] else None,

@@ -2,7 +2,8 @@
 # Report-time close A/Bs (round 3: speculative folds, page-locked ingest, the close's output pages).
 #   bash tools/report_close_ab.sh <outdir> bench [steps]  bench.py --workload resnet18-report: speculative
 #                                                         (lazy) / eager / certain-only, back to back and
-#                                                         5 ms apart; --sync-before-close splits the queued
+#                                                         5 ms apart, back to back with the close 20 ms
+#                                                         later; --sync-before-close splits the queued
 #                                                         GPU work from the close call
 #   bash tools/report_close_ab.sh <outdir> node           tools/node_sim.py: speculative / certain-only, the
 #                                                         close at once / 50 ms after the last report
@@ -24,10 +25,11 @@ PY
 case $mode in
 tests)
   timeout -k 10 600 python -u -m pytest tests/test_gpu_incremental.py tests/test_gpu_group.py tests/test_gpu_report_semantics.py \
-      tests/test_gpu_pinned_report.py -x -q --timeout 300 --timeout-method thread > "$out/pytest_new.log" 2>&1
+      tests/test_gpu_pinned_report.py tests/test_gpu_speculative_close.py -x -q --timeout 300 --timeout-method thread > "$out/pytest_new.log" 2>&1
   rc=$?; tail -3 "$out/pytest_new.log"; exit $rc ;;
 bench)
-  for arm in "spec:" "eager:--eager-speculate" "nospec:--no-speculate" "spec5:--report-gap-ms 5" "nospec5:--no-speculate --report-gap-ms 5"; do
+  for arm in "spec:" "eager:--eager-speculate" "nospec:--no-speculate" "spec5:--report-gap-ms 5" "nospec5:--no-speculate --report-gap-ms 5" \
+      "spec_end20:--close-gap-ms 20" "nospec_end20:--no-speculate --close-gap-ms 20"; do
     name=${arm%%:*}; flags=${arm#*:}
     timeout -k 10 200 python -u bench.py --workload resnet18-report --steps "$steps" --warmup 2 --no-cpu-baseline \
         --sync-before-close $flags > "$out/report_$name.json" 2> "$out/report_$name.err" || exit 1
