@@ -153,3 +153,39 @@ def test_peek_into_another_output_while_a_copy_runs():
         want = O.fedavg_mean(ckpt, [diffs[w] for w in range(3)])
         for g, w in zip(parse_state(bytes(other[0])), want):
             assert np.array_equal(bits(g), bits(w))
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_burst_then_pause_is_folded_and_peeked_by_the_timer(mode):
+    """Reports back to back (lazy: none folded at once), then a pause before the close: the timer
+    folds them and peeks on its own thread, the close commits that peek -- bit-exact."""
+    import time
+
+    from pygrid_amd import Engine
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(840 + mode)
+    numel = [int(np.prod(s)) for s in SHAPES]
+    ckpt = [rng.standard_normal(s).astype(F) for s in SHAPES]
+    ck = build_state_fast(ckpt)
+    weights = {w: float(rng.uniform(0.5, 2.0)) for w in range(10)}
+    diffs = {w: build_state_fast([(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES]) for w in range(10)}
+    reporters = [w for w in range(10) if w != 4]
+    with Engine(0) as eng:
+        inc = IncrementalCycle(eng, numel, mode=mode, slots=12, checkpoint=ck, min_gap_ms=50.0,
+                               weights_by_worker=weights if mode == 2 else None)
+        for w in range(10):
+            inc.assigned(w)
+        for w in rng.permutation(reporters):
+            inc.reported(int(w), diffs[int(w)])
+        deadline = time.time() + 10
+        while (len(inc._folded) < len(reporters) or inc._timer is not None) and time.time() < deadline:
+            time.sleep(0.01)
+        assert len(inc._folded) == len(reporters)
+        new = inc.close(ck)
+        assert inc.last_close["peeked"], inc.last_close
+        rows = [parse_state(diffs[w]) for w in reporters]
+        want = _want(mode, ckpt, rows, [weights[w] for w in reporters])
+        for g, w in zip(parse_state(new), want):
+            assert np.array_equal(bits(g), bits(w))
