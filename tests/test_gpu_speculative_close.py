@@ -155,8 +155,9 @@ def test_peek_into_another_output_while_a_copy_runs():
             assert np.array_equal(bits(g), bits(w))
 
 
+@pytest.mark.parametrize("devices", [None, [0, 0]])
 @pytest.mark.parametrize("mode", [0, 2])
-def test_burst_then_pause_is_folded_and_peeked_by_the_timer(mode):
+def test_burst_then_pause_is_folded_and_peeked_by_the_timer(mode, devices):
     """Reports back to back (lazy: none folded at once), then a pause before the close: the timer
     folds them and peeks on its own thread, the close commits that peek -- bit-exact."""
     import time
@@ -172,7 +173,7 @@ def test_burst_then_pause_is_folded_and_peeked_by_the_timer(mode):
     weights = {w: float(rng.uniform(0.5, 2.0)) for w in range(10)}
     diffs = {w: build_state_fast([(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES]) for w in range(10)}
     reporters = [w for w in range(10) if w != 4]
-    with Engine(0) as eng:
+    with (Engine(devices=devices) if devices else Engine(0)) as eng:
         inc = IncrementalCycle(eng, numel, mode=mode, slots=12, checkpoint=ck, min_gap_ms=50.0,
                                weights_by_worker=weights if mode == 2 else None)
         for w in range(10):
