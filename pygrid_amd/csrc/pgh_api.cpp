@@ -340,7 +340,6 @@ struct pgh_ctx {
     size_t vbytes_cap = 0;
     pgh::VChunk* d_vtab = nullptr;
     int64_t* d_vsink = nullptr;  // 256 int64s k_varint_decode's lanes without a value store into
-    int varint_prefetch = 1;     // PGH_VARINT_PREFETCH: windows k_varint_decode loads ahead (1 or 2)
     pgh::VChunk* h_vtab = nullptr;  // pinned
     size_t vtab_cap = 0;
     hipEvent_t vtab_ev = nullptr;
@@ -1411,7 +1410,6 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_NT_COPY")) c->nt_copy = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_PREFAULT")) c->prefault = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_FINAL_RANGES")) c->final_split = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("PGH_VARINT_PREFETCH")) c->varint_prefetch = std::atoi(e) > 1 ? 2 : 1;
     if (const char* e = std::getenv("PGH_FINAL_STREAMS")) c->final_streams = std::atoi(e) > 1 ? 2 : 1;
     if (const char* e = std::getenv("PGH_D2H_PIECE_MB")) {
         const long long mb = std::atoll(e);
@@ -1937,7 +1935,7 @@ int decode_share_msgs(pgh_ctx* c, std::vector<ShareMsg>& msgs, int slot) {
         const int n = (int)msgs[s].chunks.size();
         const hipError_t e = pgh::launch_varint_decode(c->d_vbytes, c->d_vtab + at, n,
                                                        (int64_t*)slot_row(c, slot, (int)s), slab_map(c), c->lo, c->hi,
-                                                       c->d_vsink, c->varint_prefetch, c->copy);
+                                                       c->d_vsink, c->copy);
         if (e != hipSuccess) return fail(c, PGH_E_HIP, "varint decode launch failed: %s", hipGetErrorString(e));
         at += (size_t)n;
     }

@@ -574,8 +574,6 @@ __device__ __forceinline__ uint64_t varint_at(const uint8_t* win, const uint16_t
 // varints) finish their remaining ranks in a loop.
 constexpr int VFIXED = 2;
 
-// PRE: windows loaded ahead (1 or 2; 16 bytes of registers per lane each).
-template <int PRE>
 __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, const VChunk* chunks, int64_t* row,
                                                        SlabMap m, int64_t lo, int64_t hi, int64_t* sink) {
     __shared__ u32x4 win4[1 + 256 + 1];  // [0]: the 16 bytes before the window; [257]: slack for reads past an end
@@ -595,12 +593,9 @@ __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, con
     const bool has_before = ch.off > ch.span_off;
     const u32x4 b16 = *reinterpret_cast<const u32x4*>(bytes + (has_before ? ch.off - 16 : ch.off));
     const int last16 = (ch.n - 1) & ~15;
-    // the next windows' 16 bytes are loaded PRE windows ahead (loading the whole chunk up front
+    // the next window's 16 bytes are loaded one window ahead (loading the whole chunk up front
     // costs occupancy: 79 vs 63 us per 111 MB message, profiles/r02x/)
     u32x4 nxt = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + ch.off + min(p, last16)));
-    u32x4 nxt2 = PRE > 1 ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + ch.off +
-                                                                                    min(VWIN + p, last16)))
-                         : zero;
     const u32x4 before = has_before ? b16 : zero;
     const uint32_t tb = term_mask16(before);
     int carry = tb ? (31 - __clz(tb)) - 16 : -16;
@@ -612,14 +607,7 @@ __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, con
         const int w0 = VWIN * i;
         if (w0 >= ch.n) break;  // uniform over the workgroup
         const u32x4 v = nxt;
-        if constexpr (PRE > 1) {
-            nxt = nxt2;
-            nxt2 = __builtin_nontemporal_load(
-                reinterpret_cast<const u32x4*>(bytes + ch.off + min(w0 + 2 * VWIN + p, last16)));
-        } else {
-            nxt = __builtin_nontemporal_load(
-                reinterpret_cast<const u32x4*>(bytes + ch.off + min(w0 + VWIN + p, last16)));
-        }
+        nxt = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + ch.off + min(w0 + VWIN + p, last16)));
         win4[1 + t] = v;
         if (t == 255) win4[0] = last;
         uint32_t tm = term_mask16(v);
@@ -953,16 +941,13 @@ hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_r
 }
 
 hipError_t launch_varint_decode(const uint8_t* bytes, const VChunk* chunks, int n_chunks, int64_t* row,
-                                const SlabMap& m, int64_t lo, int64_t hi, int64_t* sink, int prefetch, hipStream_t s) {
+                                const SlabMap& m, int64_t lo, int64_t hi, int64_t* sink, hipStream_t s) {
     if (n_chunks < 0 || (n_chunks > 0 && (!bytes || !chunks || !row || !sink)) ||
         (reinterpret_cast<uintptr_t>(bytes) & 15) ||
         m.off != 0 || !valid_map(m, 0) || lo > hi)
         return hipErrorInvalidValue;
     if (n_chunks == 0) return hipSuccess;
-    if (prefetch > 1)
-        k_varint_decode<2><<<(unsigned)n_chunks, 256, 0, s>>>(bytes, chunks, row, m, lo, hi, sink);
-    else
-        k_varint_decode<1><<<(unsigned)n_chunks, 256, 0, s>>>(bytes, chunks, row, m, lo, hi, sink);
+    k_varint_decode<<<(unsigned)n_chunks, 256, 0, s>>>(bytes, chunks, row, m, lo, hi, sink);
     return hipGetLastError();
 }
 
