@@ -339,7 +339,6 @@ struct pgh_ctx {
     uint8_t* d_vbytes = nullptr;
     size_t vbytes_cap = 0;
     pgh::VChunk* d_vtab = nullptr;
-    int64_t* d_vsink = nullptr;  // 256 int64s k_varint_decode's lanes without a value store into
     pgh::VChunk* h_vtab = nullptr;  // pinned
     size_t vtab_cap = 0;
     hipEvent_t vtab_ev = nullptr;
@@ -1496,7 +1495,6 @@ void pgh_destroy(pgh_ctx* c) {
     for (double* p : c->rec_old) (void)hipFree(p);
     (void)hipFree(c->d_vbytes);
     (void)hipFree(c->d_vtab);
-    (void)hipFree(c->d_vsink);
     if (c->h_vtab) (void)hipHostFree(c->h_vtab);
     if (c->vtab_ev) (void)hipEventDestroy(c->vtab_ev);
     (void)hipFree(c->d_gtab);
@@ -1922,11 +1920,6 @@ int decode_share_msgs(pgh_ctx* c, std::vector<ShareMsg>& msgs, int slot) {
         std::memcpy(c->h_vtab + at, m.chunks.data(), m.chunks.size() * sizeof(pgh::VChunk));
         at += m.chunks.size();
     }
-    if (!c->d_vsink && hipMalloc((void**)&c->d_vsink, 256 * sizeof(int64_t)) != hipSuccess) {
-        (void)hipGetLastError();
-        c->d_vsink = nullptr;
-        return fail(c, PGH_E_OOM, "varint decode scratch allocation failed");
-    }
     CK(c, hipMemcpyAsync(c->d_vtab, c->h_vtab, tb, hipMemcpyHostToDevice, c->copy));
     CK(c, hipEventRecord(c->vtab_ev, c->copy));
     c->vtab_used = true;
@@ -1935,7 +1928,7 @@ int decode_share_msgs(pgh_ctx* c, std::vector<ShareMsg>& msgs, int slot) {
         const int n = (int)msgs[s].chunks.size();
         const hipError_t e = pgh::launch_varint_decode(c->d_vbytes, c->d_vtab + at, n,
                                                        (int64_t*)slot_row(c, slot, (int)s), slab_map(c), c->lo, c->hi,
-                                                       c->d_vsink, c->copy);
+                                                       c->copy);
         if (e != hipSuccess) return fail(c, PGH_E_HIP, "varint decode launch failed: %s", hipGetErrorString(e));
         at += (size_t)n;
     }

@@ -105,9 +105,8 @@ struct VChunk {
 };
 // Decode every chunk into one slab row: value with flat index i goes to row[m.at(i - lo)] when
 // lo <= i < hi.  Requires validated input (no varint longer than 10 bytes).
-// `sink`: 256 int64s of scratch the kernel's lanes without a value store into.
 hipError_t launch_varint_decode(const uint8_t* bytes, const VChunk* chunks, int n_chunks, int64_t* row,
-                                const SlabMap& m, int64_t lo, int64_t hi, int64_t* sink, hipStream_t s);
+                                const SlabMap& m, int64_t lo, int64_t hi, hipStream_t s);
 
 // Float payloads of a page-locked State message, DMA'd into HBM as they lie in the message (no host
 // staging copy), gathered into one slab row: chunk k moves n floats starting at byte `src` of the

@@ -544,38 +544,8 @@ __device__ __forceinline__ uint32_t term_mask16(const u32x4& v) {  // bit k: byt
     return tm;
 }
 
-// Value r of the window: bytes (end[r - 1], end[r]] from the four aligned LDS dwords around them.
-__device__ __forceinline__ uint64_t varint_at(const uint8_t* win, const uint16_t* ends, int r, int carry) {
-    const int e = min((int)ends[r], VWIN - 1);
-    // validated input: s >= e - 9 (the clamps only keep malformed or unused ranks inside the window)
-    const int s = max(r ? (int)ends[r - 1] + 1 : carry + 1, e - 9);
-    const int len = e - s + 1;
-    // bytes [s, s + 12) from the four aligned dwords around them (win[-16 .. 4111] are in bounds:
-    // s >= -15 and s <= 4095), then the 7-bit groups of each dword packed in 32-bit arithmetic;
-    // bytes at or past the value's length are masked out first
-    const uint32_t* wd = reinterpret_cast<const uint32_t*>(win + (s & ~3));
-    const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
-    const uint32_t sh = (uint32_t)(s & 3);
-    uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-    uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-    uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-    w0 &= len >= 4 ? 0xFFFFFFFFu : (1u << (8 * len)) - 1u;
-    w1 &= len >= 8 ? 0xFFFFFFFFu : len <= 4 ? 0u : (1u << (8 * (len - 4))) - 1u;
-    w2 &= len >= 10 ? 0xFFFFu : len == 9 ? 0xFFu : 0u;
-    return (uint64_t)pack7x4(w0) | ((uint64_t)pack7x4(w1) << 28) | ((uint64_t)(w2 & 0x7F) << 56) |
-           ((uint64_t)((w2 >> 8) & 0x7F) << 63);
-}
-
-// Ranks every lane stores unconditionally per window (512 values: ~4.7 KB of 10-byte varints).  A
-// fixed count of stores per window lets the compiler wait for the next window's prefetched bytes
-// without also waiting for this window's stores (gfx950 counts loads and stores on one counter;
-// with a data-dependent store loop it waited for every store, one HBM write round trip per
-// window).  Lanes without a value of this shard store into `sink`; denser windows (short
-// varints) finish their remaining ranks in a loop.
-constexpr int VFIXED = 2;
-
 __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, const VChunk* chunks, int64_t* row,
-                                                       SlabMap m, int64_t lo, int64_t hi, int64_t* sink) {
+                                                       SlabMap m, int64_t lo, int64_t hi) {
     __shared__ u32x4 win4[1 + 256 + 1];  // [0]: the 16 bytes before the window; [257]: slack for reads past an end
     __shared__ uint16_t ends[VWIN];      // window offsets of the value ends, by rank
     __shared__ int wsum[4];
@@ -634,18 +604,25 @@ __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, con
             tm &= tm - 1;
         }
         __syncthreads();
-        // rank r -> lane r mod 256, so consecutive lanes store consecutive int64s
-#pragma unroll
-        for (int k = 0; k < VFIXED; ++k) {
-            const int r = t + 256 * k;
-            const uint64_t val = varint_at(win, ends, min(r, max(total - 1, 0)), carry);
-            const int64_t idx = base + r;
-            const bool mine = r < total && idx >= lo && idx < hi;
-            int64_t* dst = mine ? row + m.at(idx - lo) : sink + t;
-            *dst = (int64_t)val;
-        }
-        for (int r = t + 256 * VFIXED; r < total; r += 256) {
-            const uint64_t val = varint_at(win, ends, r, carry);
+        for (int r = t; r < total; r += 256) {
+            const int e = ends[r];
+            // validated input: s >= e - 9 (the clamp only keeps malformed bytes inside the window)
+            const int s = max(r ? (int)ends[r - 1] + 1 : carry + 1, e - 9);
+            const int len = e - s + 1;
+            // bytes [s, s + 12) from the four aligned dwords around them (win[-16 .. 4111] are in
+            // bounds: s >= -15 and s <= 4095), then the 7-bit groups of each dword packed in
+            // 32-bit arithmetic; bytes at or past the value's length are masked out first
+            const uint32_t* wd = reinterpret_cast<const uint32_t*>(win + (s & ~3));
+            const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
+            const uint32_t sh = (uint32_t)(s & 3);
+            uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+            uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+            w0 &= len >= 4 ? 0xFFFFFFFFu : (1u << (8 * len)) - 1u;
+            w1 &= len >= 8 ? 0xFFFFFFFFu : len <= 4 ? 0u : (1u << (8 * (len - 4))) - 1u;
+            w2 &= len >= 10 ? 0xFFFFu : len == 9 ? 0xFFu : 0u;
+            const uint64_t val = (uint64_t)pack7x4(w0) | ((uint64_t)pack7x4(w1) << 28) |
+                                 ((uint64_t)(w2 & 0x7F) << 56) | ((uint64_t)((w2 >> 8) & 0x7F) << 63);
             const int64_t idx = base + r;
             if (idx >= lo && idx < hi) row[m.at(idx - lo)] = (int64_t)val;
         }
@@ -941,13 +918,12 @@ hipError_t launch_synth_f32(float* out, const SlabMap& m, int64_t ncols, int n_r
 }
 
 hipError_t launch_varint_decode(const uint8_t* bytes, const VChunk* chunks, int n_chunks, int64_t* row,
-                                const SlabMap& m, int64_t lo, int64_t hi, int64_t* sink, hipStream_t s) {
-    if (n_chunks < 0 || (n_chunks > 0 && (!bytes || !chunks || !row || !sink)) ||
-        (reinterpret_cast<uintptr_t>(bytes) & 15) ||
+                                const SlabMap& m, int64_t lo, int64_t hi, hipStream_t s) {
+    if (n_chunks < 0 || (n_chunks > 0 && (!bytes || !chunks || !row)) || (reinterpret_cast<uintptr_t>(bytes) & 15) ||
         m.off != 0 || !valid_map(m, 0) || lo > hi)
         return hipErrorInvalidValue;
     if (n_chunks == 0) return hipSuccess;
-    k_varint_decode<<<(unsigned)n_chunks, 256, 0, s>>>(bytes, chunks, row, m, lo, hi, sink);
+    k_varint_decode<<<(unsigned)n_chunks, 256, 0, s>>>(bytes, chunks, row, m, lo, hi);
     return hipGetLastError();
 }
 
