@@ -520,9 +520,11 @@ __global__ __launch_bounds__(BLOCK) void k_synth_shares(int64_t* out, SlabMap m,
 //   2. every lane writes the window offsets of its value ends into LDS by rank (a compacted list);
 //   3. the workgroup decodes the list rank by rank, lane = rank mod 256: value r spans
 //      (end[r - 1], end[r]] (end[-1] = the last end of the previous window, or of the 16 bytes
-//      before the chunk), its <= 10 bytes are independent LDS reads and the 7-bit groups are
-//      shifted in under a length mask -- no data-dependent loop, no divergence past the last rank;
-//      value r goes to flat index first + rank, so consecutive lanes store consecutive int64s.
+//      before the chunk), its <= 10 bytes are independent LDS reads, the 7-bit groups are packed
+//      and the next values' bytes masked off the result by length -- no data-dependent loop, no
+//      divergence past the last rank; value r goes to flat index first + rank, so consecutive
+//      lanes store consecutive int64s (one base address per window when the window's values lie
+//      in one slab block of the shard).
 // The next window's 16-byte load is issued before the current one is decoded.  Byte-level work on
 // a stream PCIe fills at ~55 GB/s; HBM traffic is ~2 bytes per byte in.
 constexpr int VWIN = 4096;
@@ -604,27 +606,36 @@ __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, con
             tm &= tm - 1;
         }
         __syncthreads();
+        // the window's values inside the shard and in one slab block (the usual case): consecutive
+        // addresses from one base, a wave-uniform test instead of a slab-map lookup per value
+        const int64_t l0 = base - lo, l1 = base + total - 1 - lo;
+        const bool flat = base >= lo && base + total <= hi && ((m.off + l0) >> m.bshift) == ((m.off + l1) >> m.bshift);
+        int64_t* const dst0 = row + (flat ? m.at(l0) : 0);
         for (int r = t; r < total; r += 256) {
             const int e = ends[r];
             // validated input: s >= e - 9 (the clamp only keeps malformed bytes inside the window)
             const int s = max(r ? (int)ends[r - 1] + 1 : carry + 1, e - 9);
             const int len = e - s + 1;
             // bytes [s, s + 12) from the four aligned dwords around them (win[-16 .. 4111] are in
-            // bounds: s >= -15 and s <= 4095), then the 7-bit groups of each dword packed in
-            // 32-bit arithmetic; bytes at or past the value's length are masked out first
+            // bounds: s >= -15 and s <= 4095), the 7-bit groups of each dword packed in 32-bit
+            // arithmetic; the bytes past the value's end (the next values') land at bits >= 7 * len
+            // and are masked off the result
             const uint32_t* wd = reinterpret_cast<const uint32_t*>(win + (s & ~3));
             const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
             const uint32_t sh = (uint32_t)(s & 3);
-            uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-            uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-            uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-            w0 &= len >= 4 ? 0xFFFFFFFFu : (1u << (8 * len)) - 1u;
-            w1 &= len >= 8 ? 0xFFFFFFFFu : len <= 4 ? 0u : (1u << (8 * (len - 4))) - 1u;
-            w2 &= len >= 10 ? 0xFFFFu : len == 9 ? 0xFFu : 0u;
-            const uint64_t val = (uint64_t)pack7x4(w0) | ((uint64_t)pack7x4(w1) << 28) |
-                                 ((uint64_t)(w2 & 0x7F) << 56) | ((uint64_t)((w2 >> 8) & 0x7F) << 63);
-            const int64_t idx = base + r;
-            if (idx >= lo && idx < hi) row[m.at(idx - lo)] = (int64_t)val;
+            const uint32_t p0 = pack7x4(__builtin_amdgcn_alignbyte(d1, d0, sh));
+            const uint32_t p1 = pack7x4(__builtin_amdgcn_alignbyte(d2, d1, sh));
+            const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+            const uint32_t lo32 = p0 | (p1 << 28);
+            const uint32_t hi32 = (p1 >> 4) | ((w2 & 0x7Fu) << 24) | ((w2 << 23) & 0x80000000u);
+            uint64_t val = ((uint64_t)hi32 << 32) | lo32;
+            val &= len >= 10 ? ~0ull : (1ull << (7 * len)) - 1ull;
+            if (flat) {
+                dst0[r] = (int64_t)val;
+            } else {
+                const int64_t idx = base + r;
+                if (idx >= lo && idx < hi) row[m.at(idx - lo)] = (int64_t)val;
+            }
         }
         carry = (total ? (int)ends[total - 1] : carry) - VWIN;
         base += total;
