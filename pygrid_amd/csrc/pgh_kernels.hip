@@ -516,7 +516,7 @@ __global__ __launch_bounds__(BLOCK) void k_synth_shares(int64_t* out, SlabMap m,
 // 64 KiB chunk, walked in 4 KiB windows staged in LDS with the 16 bytes before them (a varint is
 // at most 10 bytes, so a value ending in the window starts at offset >= -9).  Per window:
 //   1. lane t owns bytes [16t, 16t + 16): its terminators (bit 7 clear) come from its 16-byte load
-//      in registers; a wave prefix sum (shuffles) + the per-wave totals give each value's rank;
+//      in registers; a wave prefix sum (DPP) + the per-wave totals give each value's rank;
 //   2. every lane writes the window offsets of its value ends into LDS by rank (a compacted list);
 //   3. the workgroup decodes the list rank by rank, lane = rank mod 256: value r spans
 //      (end[r - 1], end[r]] (end[-1] = the last end of the previous window, or of the 16 bytes
@@ -544,6 +544,19 @@ __device__ __forceinline__ uint32_t term_mask16(const u32x4& v) {  // bit k: byt
         tm |= (((nt >> 7) & 1u) | ((nt >> 14) & 2u) | ((nt >> 21) & 4u) | ((nt >> 28) & 8u)) << (4 * w);
     }
     return tm;
+}
+
+// Inclusive prefix sum over a wave64 in DPP moves (row shifts inside each 16-lane row, then the
+// row totals broadcast into the rows after them): no LDS round trips, unlike __shfl_up's
+// ds_bpermute chain.
+__device__ __forceinline__ int wave_inclusive_sum(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
 }
 
 __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, const VChunk* chunks, int64_t* row,
@@ -586,12 +599,7 @@ __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, con
         const int lim = ch.n - w0 - p;  // bytes of mine inside the chunk
         if (lim < 16) tm &= lim > 0 ? (1u << lim) - 1u : 0u;
         const int cnt = __popc(tm);
-        int x = cnt;  // inclusive prefix over the wave
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
+        const int x = wave_inclusive_sum(cnt);
         if (lane == 63) wsum[wave] = x;
         __syncthreads();
         int rank = x - cnt, total = 0;
