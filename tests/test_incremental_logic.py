@@ -793,3 +793,63 @@ def test_lazy_skips_are_folded_by_a_timer_once_reports_pause(monkeypatch):
     assert inc.last_close["folded_before_close"] == 8
     assert eng.result == [bytes([w]) for w in range(8)]
     assert inc._timer is None
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_concurrent_reports_and_timer_folds_never_overlap_engine_calls(seed):
+    """Report handlers on several threads, the deferred-fold timer and re-reports: every engine call
+    happens under the cycle's lock (no two at once), and the close is the reference's order."""
+    import threading
+    import time as _time
+
+    class GuardedEngine(BusySpecEngine):
+        def __getattribute__(self, name):
+            attr = object.__getattribute__(self, name)
+            if callable(attr) and not name.startswith("_") and name not in ("fold_busy",):
+                def guarded(*a, **k):
+                    lock = object.__getattribute__(self, "_guard")
+                    assert lock.acquire(blocking=False), f"engine call {name} overlapped another"
+                    try:
+                        _time.sleep(0.0002)
+                        return attr(*a, **k)
+                    finally:
+                        lock.release()
+                return guarded
+            return attr
+
+    rng = np.random.default_rng(300 + seed)
+    eng = GuardedEngine()
+    object.__setattr__(eng, "_guard", threading.Lock())
+    n = 40
+    inc = IncrementalCycle(eng, [3], slots=48, min_gap_ms=1.0, mark_every=4)
+    for w in range(n):
+        inc.assigned(w)
+    reporters = [w for w in range(n) if rng.random() >= 0.2]
+    rereport = set(int(w) for w in rng.choice(reporters, size=4, replace=False))
+    order = [int(w) for w in rng.permutation(reporters)]
+    chunks = [order[i::4] for i in range(4)]
+    errors = []
+
+    def handler(ws, delays):
+        try:
+            for w, d in zip(ws, delays):
+                _time.sleep(d)
+                inc.reported(w, mk(w + 1000) if w in rereport else mk(w))
+                eng.busy = bool(rng.random() < 0.3)
+            for w in ws:
+                if w in rereport:
+                    inc.reported(w, mk(w))  # the latest diff wins
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=handler, args=(c, list(rng.uniform(0, 0.003, len(c))))) for c in chunks]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    eng.busy = False
+    _time.sleep(0.05)
+    assert not errors, errors
+    # a re-report after its diff was folded for good is read from the DB (fetch) at close
+    inc.close(b"ck", framing="template", order=sorted(reporters), fetch=mk)
+    assert eng.result == [mk(w) for w in sorted(reporters)]
