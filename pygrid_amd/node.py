@@ -199,6 +199,8 @@ class NodeEngine:
         return self
 
     def uninstall(self):
+        with self._lock:
+            self._abandon_others()  # stops their deferred-fold timers: nothing touches the engine after this
         for owner, name, old in reversed(self._patched):
             if old is _MISSING:
                 delattr(owner, name)
