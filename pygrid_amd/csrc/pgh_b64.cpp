@@ -22,7 +22,8 @@
 // Parallel form: before the first '=' the machine only decodes alphabet characters and skips the
 // rest.  A parallel count of the prefix's alphabet characters per chunk gives every chunk its
 // position in that character stream; each thread then decodes the whole quads whose first
-// character lies in its chunk, skipping non-alphabet characters in place (no compacted copy).  The
+// character lies in its chunk: their characters are compacted (stray characters dropped; AVX2 +
+// BMI2 pext) into a small thread-local buffer piece by piece and decoded as clean text.  The
 // machine itself runs only over the prefix's last 0-3 alphabet characters and the input from the
 // first '=' on.
 #include <immintrin.h>
@@ -173,6 +174,80 @@ __attribute__((target("avx2"))) bool decode_clean_avx2(const unsigned char* in, 
 bool have_avx2() {
     static const bool yes = __builtin_cpu_supports("avx2");
     return yes;
+}
+
+// The general route's inner loops (text with characters outside the alphabet, e.g. MIME line
+// breaks): AVX2 + BMI2 where the CPU has them, the scalar loops below otherwise.
+bool have_avx2_bmi2() {
+    static const bool yes = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("bmi2");
+    return yes;
+}
+
+// Bit j set when character j of the 32 at p is NOT in the alphabet.
+__attribute__((target("avx2"))) inline uint32_t bad_mask32(const unsigned char* p) {
+    PGH_B64_LUTS;
+    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p));
+    const __m256i hi = _mm256_and_si256(_mm256_srli_epi32(v, 4), nib);
+    const __m256i bad = _mm256_and_si256(_mm256_shuffle_epi8(lut_lo, _mm256_and_si256(v, nib)),
+                                         _mm256_shuffle_epi8(lut_hi, hi));
+    return ~(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(bad, _mm256_setzero_si256()));
+}
+
+// Alphabet characters in s[a, b).
+__attribute__((target("avx2,popcnt"))) size_t count_alphabet_avx2(const unsigned char* s, size_t a, size_t b) {
+    size_t g = 0, i = a;
+    for (; i + 32 <= b; i += 32) g += 32 - (size_t)__builtin_popcount(bad_mask32(s + i));
+    for (; i < b; ++i) g += kT.v[s[i]] >= 0;
+    return g;
+}
+
+size_t count_alphabet(const unsigned char* s, size_t a, size_t b) {
+    if (have_avx2_bmi2()) return count_alphabet_avx2(s, a, b);
+    size_t g = 0;
+    for (size_t i = a; i < b; ++i) g += kT.v[s[i]] >= 0;
+    return g;
+}
+
+// Copy the alphabet characters of s[i, end) to dst, in order, until `want` are copied or `end` is
+// reached; advances i, returns the count.  A 32-character block without a stray character is one
+// copy; one with strays is compacted 8 characters at a time (pext of the kept bytes).  dst needs
+// 32 bytes of slack.
+__attribute__((target("avx2,bmi2,popcnt"))) size_t compact_alphabet_avx2(const unsigned char* s, size_t& i, size_t end,
+                                                                        unsigned char* dst, size_t want) {
+    size_t got = 0;
+    while (got + 32 <= want && i + 32 <= end) {
+        const uint32_t bad = bad_mask32(s + i);
+        if (!bad) {
+            _mm256_storeu_si256(reinterpret_cast<__m256i*>(dst + got),
+                                _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i)));
+            got += 32;
+        } else {
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t keep = ~(bad >> (8 * j)) & 0xFFu;
+                uint64_t w;
+                std::memcpy(&w, s + i + 8 * j, 8);
+                const uint64_t packed = _pext_u64(w, _pdep_u64(keep, 0x0101010101010101ull) * 0xFFu);
+                std::memcpy(dst + got, &packed, 8);
+                got += (size_t)__builtin_popcountll(keep);
+            }
+        }
+        i += 32;
+    }
+    for (; got < want && i < end; ++i) {
+        dst[got] = s[i];
+        got += kT.v[s[i]] >= 0;
+    }
+    return got;
+}
+
+size_t compact_alphabet(const unsigned char* s, size_t& i, size_t end, unsigned char* dst, size_t want) {
+    if (have_avx2_bmi2()) return compact_alphabet_avx2(s, i, end, dst, want);
+    size_t got = 0;
+    for (; got < want && i < end; ++i) {
+        dst[got] = s[i];
+        got += kT.v[s[i]] >= 0;
+    }
+    return got;
 }
 
 bool decode_clean(const unsigned char* in, size_t n4, uint8_t* out) {
@@ -394,9 +469,7 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
     std::vector<size_t> good((size_t)t, 0);
     parallel(t, [&](int k) {
         const size_t a = std::min(fe, per * k), b = std::min(fe, a + per);
-        size_t g = 0;
-        for (size_t i = a; i < b; ++i) g += kT.v[s[i]] >= 0;
-        good[(size_t)k] = g;
+        good[(size_t)k] = count_alphabet(s, a, b);
     });
     // at[k]: index, among the prefix's alphabet characters, of chunk k's first one
     std::vector<size_t> at((size_t)t + 1, 0);
@@ -427,16 +500,18 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
             size_t i = std::min(fe, per * k), c = at[(size_t)k];
             const size_t c_end = std::min(at[(size_t)k + 1], 4 * n4);
             while (c % 4 && c < c_end) c += kT.v[s[i++]] >= 0;  // finishes a quad begun in an earlier chunk
-            for (; c < c_end; c += 4) {                           // may read past the chunk: never past fe
-                uint32_t x = 0;
-                for (int got = 0; got < 4; ++i) {
-                    const int v = kT.v[s[i]];
-                    if (v >= 0) { x = (x << 6) | (uint32_t)v; ++got; }
-                }
-                uint8_t* o = out + 3 * (c / 4);
-                o[0] = (uint8_t)(x >> 16);
-                o[1] = (uint8_t)(x >> 8);
-                o[2] = (uint8_t)x;
+            // its quads' characters, compacted piece by piece into a local buffer and decoded as
+            // clean text (the last quad may read past the chunk: never past fe)
+            size_t need = c < c_end ? (c_end - c + 3) / 4 * 4 : 0;
+            uint8_t* o = out + 3 * (c / 4);
+            constexpr size_t B = 16384;
+            alignas(32) unsigned char buf[B + 32];
+            while (need) {
+                const size_t got = compact_alphabet(s, i, fe, buf, std::min(need, B));
+                if (got % 4 || !got) break;  // cannot happen: the prefix holds 4 * n4 alphabet characters
+                decode_clean(buf, got / 4, o);
+                o += got / 4 * 3;
+                need -= got;
             }
         });
     }
