@@ -414,11 +414,6 @@ size_t first_eq(const unsigned char* s, size_t n) {
     return eq ? (size_t)((const unsigned char*)eq - s) : n;
 }
 
-// The general route needs the true first '=' (the machine takes over there).
-size_t first_eq_exact(const unsigned char* s, size_t n) {
-    const void* eq = n ? std::memchr(s, '=', n) : nullptr;
-    return eq ? (size_t)((const unsigned char*)eq - s) : n;
-}
 }  // namespace
 
 extern "C" {
@@ -463,14 +458,22 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
         const int rc = decode_fast(s, n, first_eq(s, n), out, pgh_b64_decoded_cap(n), written, t);
         if (rc != PGH_E_STATE) return rc;  // clean text: decoded, or a padding error
     }
-    const size_t fe = first_eq_exact(s, n);  // the machine's prefix
-    // count alphabet characters per chunk of [0, fe)
-    const size_t per = (fe + t - 1) / t;
-    std::vector<size_t> good((size_t)t, 0);
+    // per chunk of the text: its first '=' and the alphabet characters before it; the first chunk
+    // holding an '=' ends the machine's prefix [0, fe) (no serial scan of the whole text for it)
+    const size_t per = (n + t - 1) / t;
+    std::vector<size_t> good((size_t)t, 0), eqs((size_t)t, n);
     parallel(t, [&](int k) {
-        const size_t a = std::min(fe, per * k), b = std::min(fe, a + per);
-        good[(size_t)k] = count_alphabet(s, a, b);
+        const size_t a = std::min(n, per * k), b = std::min(n, a + per);
+        const void* e = b > a ? std::memchr(s + a, '=', b - a) : nullptr;
+        const size_t ek = e ? (size_t)((const unsigned char*)e - s) : b;
+        eqs[(size_t)k] = e ? ek : n;
+        good[(size_t)k] = count_alphabet(s, a, ek);
     });
+    size_t fe = n;
+    for (int k = 0; k < t; ++k) {
+        if (fe < n) good[(size_t)k] = 0;  // after the prefix
+        else fe = eqs[(size_t)k];
+    }
     // at[k]: index, among the prefix's alphabet characters, of chunk k's first one
     std::vector<size_t> at((size_t)t + 1, 0);
     for (int k = 0; k < t; ++k) at[(size_t)k + 1] = at[(size_t)k] + good[(size_t)k];
