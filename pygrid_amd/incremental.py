@@ -148,6 +148,12 @@ class IncrementalCycle:
         self._lock = threading.Lock()
         self._closed = False
         self._declined: Optional[str] = None  # why the engine cannot average this cycle
+        # one open cycle per engine: a previous one left open (dropped without close) is abandoned
+        # here, so that its deferred-fold timer cannot touch this cycle's slots
+        prev = getattr(engine, "cycle_owner", None)
+        if prev is not None and prev is not self:
+            prev.abandon()
+        engine.cycle_owner = self
         # keep the engine's slab when a cycle of the same model follows (no re-allocation)
         if tuple(getattr(engine, "numel", ())) != self._numel or getattr(engine, "max_clients", 0) != self.slots \
                 or getattr(engine, "dtype", None) != F32:
@@ -608,6 +614,8 @@ class IncrementalCycle:
         """Another user takes the engine (its slab is re-laid): nothing held here survives.  Later
         reports are ignored and ``close`` raises; the node closes this cycle from its DB rows."""
         with self._lock:
+            if self._closed:  # closed (or abandoned) already: its result may be the resident checkpoint
+                return
             self._closed = True
             self._cancel_timer()
             self._slot_of.clear()

@@ -853,3 +853,33 @@ def test_concurrent_reports_and_timer_folds_never_overlap_engine_calls(seed):
     # a re-report after its diff was folded for good is read from the DB (fetch) at close
     inc.close(b"ck", framing="template", order=sorted(reporters), fetch=mk)
     assert eng.result == [mk(w) for w in sorted(reporters)]
+
+
+def test_a_dropped_open_cycle_is_abandoned_by_the_next_one(monkeypatch):
+    """A cycle dropped without close while its deferred-fold timer is armed: the next cycle on the
+    engine abandons it (timer cancelled), so nothing of the old cycle touches the new one's slots;
+    a cycle that was closed keeps its resident checkpoint for the next one."""
+    import time as _time
+
+    eng = BusySpecEngine()
+    eng.busy = True
+    a = IncrementalCycle(eng, [3], slots=8, min_gap_ms=1.0)
+    for w in range(4):
+        a.assigned(w)
+    for w in (2, 1, 3):
+        a.reported(w, mk(w))
+    assert a._timer is not None
+    b = IncrementalCycle(eng, [3], slots=8, min_gap_ms=1.0)
+    assert a._closed and a._timer is None
+    eng.busy = False
+    for w in range(3):
+        b.assigned(w)
+    for w in (1, 0, 2):
+        b.reported(w, mk(10 + w))
+    _time.sleep(0.03)
+    b.close(b"ck", framing="template")
+    assert eng.result == [mk(10), mk(11), mk(12)]
+    with pytest.raises(AggregationError):
+        a.close(b"ck", framing="template")
+    c = IncrementalCycle(eng, [3], slots=8)  # b was closed: abandoning it is a no-op
+    assert eng.cycle_owner is c and b.last_close
