@@ -376,6 +376,10 @@ struct pgh_ctx {
     // launch costs its drain (ResNet-18 fold 7.45 ms as 4 ranges on two streams vs 6.91 ms as one,
     // r02r), about what the earlier D2H start saves in a close (report closes within noise, r02l/r02r).
     int final_split = 1;
+    // PGH_SLOT_FINAL_RANGES: the same split for the FINAL pass of a report-time close (a slot fold
+    // of the rows left at close: short, so its D2H would otherwise wait for all of it) -- on by
+    // default: 1.98 -> 1.41 ms close after a back-to-back burst at 8 ranges (profiles/r03ah/)
+    int slot_final_split = 8;
     int64_t client_base = 0;  // synthetic client k is generated as global client client_base + k
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
@@ -808,6 +812,10 @@ int join_aux(pgh_ctx* c, hipStream_t s) {
 
 // Ranges of a FINAL fold pass: 1, or final_split 4-aligned ranges of the shard.
 int final_ranges(const pgh_ctx* c) { return c->final_split > 1 && c->pg >= (1 << 20) ? c->final_split : 1; }
+int slot_final_ranges(const pgh_ctx* c) {
+    const int k = c->final_split > 1 ? c->final_split : c->slot_final_split;  // PGH_FINAL_RANGES wins
+    return k > 1 && c->pg >= (1 << 20) ? k : 1;
+}
 int64_t range_edge(const pgh_ctx* c, int k, int K) { return k >= K ? c->pg : (c->pg * k / K) & ~(int64_t)3; }
 
 // HBM bytes at `src` (after the work already on stream `s`) -> host pieces, through the pinned
@@ -1409,6 +1417,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_NT_COPY")) c->nt_copy = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_PREFAULT")) c->prefault = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_FINAL_RANGES")) c->final_split = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("PGH_SLOT_FINAL_RANGES")) c->slot_final_split = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("PGH_FINAL_STREAMS")) c->final_streams = std::atoi(e) > 1 ? 2 : 1;
     if (const char* e = std::getenv("PGH_D2H_PIECE_MB")) {
         const long long mb = std::atoll(e);
@@ -2363,7 +2372,7 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final, boo
         a.mode = mode;
         a.variant = c->variant;
         // the FINAL pass as K param ranges, each followed by its mark (pipelined close)
-        const int K = (a.flags & pgh::FL_FINAL) ? final_ranges(c) : 1;
+        const int K = (a.flags & pgh::FL_FINAL) ? slot_final_ranges(c) : 1;
         if (a.flags & pgh::FL_FINAL) clear_final_marks(c);
         if (K > 1) RC(fork_aux(c, s));
         for (int r = 0; r < K; ++r) {
@@ -2913,6 +2922,7 @@ int peek_commit(pgh_ctx* c, const uint8_t* out_frame, size_t n, uint8_t* out) {
         std::lock_guard<std::mutex> lk(c->pk_mu);
         copied = c->pk_done_gen == c->peek_gen && c->pk_done_out == out;
     }
+    clear_final_marks(c);  // they describe the fold that wrote the old checkpoint buffer
     if (copied) {  // the peek thread already put this peek's payloads into `out`
         std::swap(c->d_ckpt, c->d_peek);
         c->acc_src = nullptr;

@@ -190,3 +190,41 @@ def test_burst_then_pause_is_folded_and_peeked_by_the_timer(mode, devices):
         want = _want(mode, ckpt, rows, [weights[w] for w in reporters])
         for g, w in zip(parse_state(new), want):
             assert np.array_equal(bits(g), bits(w))
+
+
+@pytest.mark.parametrize("speculate", [False, True])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_report_time_close_of_a_large_shard_pipelines_its_final_pass(mode, speculate):
+    """Rows left at close on a shard of >= 1 M params: the FINAL pass of the slot fold runs as 8
+    param ranges with the D2H behind each (the default for report-time closes); the new checkpoint
+    bytes, the resident checkpoint and a chained second cycle are bit-exact."""
+    from pygrid_amd import Engine
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    shapes = [(1024, 1100), (77,)]
+    rng = np.random.default_rng(850 + mode)
+    numel = [int(np.prod(s)) for s in shapes]
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    ck = build_state_fast(ckpt)
+    weights = {w: float(rng.uniform(0.5, 2.0)) for w in range(6)}
+    with Engine(0) as eng:
+        want = ckpt
+        for cyc in range(2):
+            diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in range(6)}
+            inc = IncrementalCycle(eng, numel, mode=mode, slots=8, checkpoint=ck, speculate=speculate,
+                                   lazy=True, min_gap_ms=1e6, peek=False,
+                                   weights_by_worker=weights if mode == 2 else None)
+            for w in range(6):
+                inc.assigned(w)
+            for w in (3, 5, 2, 4, 1):  # worker 0 never reports: nothing is certain before close
+                inc.reported(w, build_state_fast(diffs[w]))
+            new = inc.close(ck)
+            assert not inc.last_close["peeked"]
+            rep = [1, 2, 3, 4, 5]
+            want = _want(mode, want, [diffs[w] for w in rep], [weights[w] for w in rep])
+            for g, w in zip(parse_state(new), want):
+                assert np.array_equal(bits(g), bits(w)), cyc
+            flat = eng.ckpt_download()
+            assert np.array_equal(bits(flat), bits(np.concatenate([w.reshape(-1) for w in want])))
+            ck = new
