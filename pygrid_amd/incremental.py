@@ -22,7 +22,8 @@ diff lives from WHEN it is folded:
   goes back to the last saved state before its position (``pgh_fold_rewind``) and continues; slots
   before the last saved state at the certain point are freed.  While the GPU is still busy with the
   previous fold (``pgh_fold_busy``), or reports arrive less than ``min_gap_ms`` apart, a report is
-  folded with a later one -- or by a timer once the reports pause.  Certain-only folds
+  folded with a later one -- or by a timer once no report has come for ``settle_ms``.  Certain-only
+  folds
   (``speculate=False``): the certain prefix is folded ``fold_batch`` at a time and freed
   (``pgh_fold_slots``);
 * ``close(checkpoint, order=..., fetch=...)`` takes the AUTHORITATIVE order -- the keys of the
@@ -80,7 +81,7 @@ DEFAULT_HBM_BUDGET = 64 << 30  # bytes of diffs kept in HBM per cycle when `slot
 MAX_DEFAULT_SLOTS = 4096
 DEFAULT_SPECULATION_BUDGET = 16 << 30  # bytes of HBM for saved fold states (speculative folds)
 MAX_MARKS = 256
-DEFER_LIMIT = 500  # timer re-arms after a report (min_gap each) before the close is left to fold
+DEFER_LIMIT = 200  # timer re-arms after a report (settle_ms each) before the close is left to fold
 
 log = logging.getLogger(__name__)
 
@@ -94,7 +95,7 @@ class IncrementalCycle:
                  weights_by_worker: Optional[Dict[object, float]] = None, checkpoint: Optional[bytes] = None,
                  early_fold: bool = True, speculate: Optional[bool] = None,
                  speculation_budget: int = DEFAULT_SPECULATION_BUDGET, mark_every: int = 8, lazy: bool = True,
-                 min_gap_ms: float = 2.0, peek: bool = True):
+                 min_gap_ms: float = 2.0, peek: bool = True, settle_ms: float = 5.0):
         self.engine = engine
         self.mode = mode
         self._numel = tuple(int(n) for n in numel)
@@ -113,6 +114,9 @@ class IncrementalCycle:
         # back to back would otherwise queue re-folds that the next report discards)
         self._lazy = bool(lazy) and hasattr(engine, "fold_busy")
         self.min_gap_s = max(0.0, float(min_gap_ms)) / 1e3
+        # the timer that folds what lazy skips left waits this long after a report (a close that
+        # follows the last report at once should find the cycle lock free, not a fold in progress)
+        self.settle_s = max(self.min_gap_s, float(settle_ms) / 1e3, 1e-3)
         # speculative close: the FINAL pass of the fold state peeked ahead (pgh_fold_peek) whenever
         # every reporter is folded; a close that finds nothing changed commits it
         self._peek = self.speculate and bool(peek) and hasattr(engine, "fold_peek")
@@ -362,7 +366,7 @@ class IncrementalCycle:
     def _defer(self):
         if self._timer is None and self._defer_left > 0:
             self._defer_left -= 1
-            self._timer = threading.Timer(max(self.min_gap_s, 1e-3), self._deferred)
+            self._timer = threading.Timer(self.settle_s, self._deferred)
             self._timer.daemon = True
             self._timer.start()
 
@@ -373,7 +377,7 @@ class IncrementalCycle:
             self._timer = None
             if self._closed or self._stale or self._declined:
                 return
-            if self._last_report is not None and time.monotonic() - self._last_report < self.min_gap_s:
+            if self._last_report is not None and time.monotonic() - self._last_report < self.settle_s:
                 self._defer()  # still arriving
                 return
             self._hurried = False
