@@ -20,8 +20,9 @@ def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
+@pytest.mark.parametrize("devices", [None, [0, 0]])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_random_bursts_pauses_and_rereports_stay_bit_exact(mode):
+def test_random_bursts_pauses_and_rereports_stay_bit_exact(mode, devices):
     from pygrid_amd import Engine
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast, parse_state
@@ -34,7 +35,7 @@ def test_random_bursts_pauses_and_rereports_stay_bit_exact(mode):
     ck = build_state_fast(ckpt)
     want = ckpt
     stats = {"peeked": 0, "rewinds": 0, "refold": 0}
-    with Engine(0) as eng:
+    with (Engine(devices=devices) if devices else Engine(0)) as eng:
         for cyc in range(5):
             inc = IncrementalCycle(eng, numel, mode=mode, slots=n + 2, checkpoint=ck,
                                    weights_by_worker=weights if mode == 2 else None)
@@ -64,4 +65,4 @@ def test_random_bursts_pauses_and_rereports_stay_bit_exact(mode):
             assert np.array_equal(bits(flat), bits(np.concatenate([w.reshape(-1) for w in want]))), cyc
             want = [np.asarray(w, F) for w in want]
             ck = new
-    print("soak", mode, stats)
+    print("soak", mode, devices, stats)
