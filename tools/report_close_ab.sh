@@ -9,6 +9,7 @@
 #                                                         close at once / 50 ms after the last report
 #   bash tools/report_close_ab.sh <outdir> phases         node_sim --phases: engine calls inside the close
 #   bash tools/report_close_ab.sh <outdir> trace          rocprofv3 kernel trace of the paced report bench
+#   bash tools/report_close_ab.sh <outdir> trace_burst    kernel + memory-copy trace, close after a burst
 #   bash tools/report_close_ab.sh <outdir> tests          the speculation / page-locked ingest GPU tests
 # Every step under its own time limit; stops at the first failure.
 set -o pipefail
@@ -51,5 +52,11 @@ trace)
   export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- python3 bench.py \
       --workload resnet18-report --steps 3 --warmup 1 --no-cpu-baseline --report-gap-ms 5 > "$out/trace.log" 2>&1 || { tail -5 "$out/trace.log"; exit 1; } ;;
+trace_burst)
+  # the close right after a back-to-back burst: its fold, the FINAL ranges and the D2H behind them
+  export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$out/trace_burst" -o run --output-format csv \
+      -- python3 bench.py --workload resnet18-report --steps 3 --warmup 1 --no-cpu-baseline --no-speculate \
+      > "$out/trace_burst.log" 2>&1 || { tail -5 "$out/trace_burst.log"; exit 1; } ;;
 *) echo "unknown mode $mode"; exit 2 ;;
 esac
