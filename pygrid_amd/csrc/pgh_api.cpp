@@ -380,6 +380,9 @@ struct pgh_ctx {
     // of the rows left at close: short, so its D2H would otherwise wait for all of it) -- on by
     // default: 1.98 -> 1.41 ms close after a back-to-back burst at 8 ranges (profiles/r03ah/)
     int slot_final_split = 8;
+    // PGH_D2H_NOCU (A/B): D2H into the library's page-locked buffers as hipMemcpyDeviceToDeviceNoCU
+    // (a copy engine instead of a blit kernel sharing the CUs with a fold still running)
+    bool d2h_nocu = false;
     int64_t client_base = 0;  // synthetic client k is generated as global client client_base + k
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
@@ -811,6 +814,7 @@ int join_aux(pgh_ctx* c, hipStream_t s) {
 }
 
 // Ranges of a FINAL fold pass: 1, or final_split 4-aligned ranges of the shard.
+hipMemcpyKind d2h_kind(const pgh_ctx* c) { return c->d2h_nocu ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost; }
 int final_ranges(const pgh_ctx* c) { return c->final_split > 1 && c->pg >= (1 << 20) ? c->final_split : 1; }
 int slot_final_ranges(const pgh_ctx* c) {
     const int k = c->final_split > 1 ? c->final_split : c->slot_final_split;  // PGH_FINAL_RANGES wins
@@ -850,7 +854,7 @@ int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>
                     start = m.end;
                 }
             }
-            CK(c, hipMemcpyAsync(c->h_pin[cur_slot], src + off, cur_len, hipMemcpyDeviceToHost, s));
+            CK(c, hipMemcpyAsync(c->h_pin[cur_slot], src + off, cur_len, d2h_kind(c), s));
             CK(c, hipEventRecord(c->pin_ev[cur_slot], s));
             c->pin_used[cur_slot] = true;
         }
@@ -1418,6 +1422,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_PREFAULT")) c->prefault = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_FINAL_RANGES")) c->final_split = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("PGH_SLOT_FINAL_RANGES")) c->slot_final_split = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("PGH_D2H_NOCU")) c->d2h_nocu = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_FINAL_STREAMS")) c->final_streams = std::atoi(e) > 1 ? 2 : 1;
     if (const char* e = std::getenv("PGH_D2H_PIECE_MB")) {
         const long long mb = std::atoll(e);
@@ -2643,7 +2648,7 @@ int pgh_fold_peek(pgh_ctx* c, int mode) {
     RC(record_fold(c, s));  // a checkpoint upload waits for this read of d_ckpt
     CK(c, hipEventRecord(c->peek_ev, s));
     CK(c, hipStreamWaitEvent(c->peek_stream, c->peek_ev, 0));
-    CK(c, hipMemcpyAsync(c->h_peek, c->d_peek, (size_t)c->pg * 4, hipMemcpyDeviceToHost, c->peek_stream));
+    CK(c, hipMemcpyAsync(c->h_peek, c->d_peek, (size_t)c->pg * 4, d2h_kind(c), c->peek_stream));
     CK(c, hipEventRecord(c->peek_ev, c->peek_stream));
     c->peek_gen = c->state_gen;
     return PGH_OK;
