@@ -20,6 +20,7 @@ Reference: ``CycleManager.complete_cycle`` / ``_average_plan_diffs``,
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 from typing import Callable, List, Optional, Sequence
 
@@ -383,7 +384,7 @@ def _probed_plan(*_a, **_k):  # stands in for a hosted plan whose verdict is cac
 
 
 def make_average_plan_diffs(aggregator: CycleAggregator, model_manager, process_manager, plan_manager,
-                            original: Callable) -> Callable:
+                            original: Callable, gate: Optional[Callable] = None) -> Callable:
     """Build a drop-in ``CycleManager._average_plan_diffs(self, server_config, cycle)``.
 
     DB I/O mirrors ``cycle_manager.py:234-245`` and ``:304-323``; the arithmetic slice
@@ -391,17 +392,21 @@ def make_average_plan_diffs(aggregator: CycleAggregator, model_manager, process_
     does not implement, runs the reference's ``original`` method unchanged.
     Engine errors are NOT retried on the CPU: they raise ``PyGridError`` subclasses, which
     ``tasks.complete_cycle`` logs (``tasks/cycle.py:28-37``), like any failed cycle close.
+    ``gate()``: a context manager held while the completed rows and their diffs are read (the
+    node's report gate: a re-report's DB write lands wholly before or after that read).
     """
 
     def _average_plan_diffs(self, server_config: dict, cycle):
         _model = model_manager.get(fl_process_id=cycle.fl_process_id)
         _checkpoint = model_manager.load(model_id=_model.id)
-        reports = self._worker_cycles.query(cycle_id=cycle.id, is_completed=True)
+        with gate() if gate is not None else contextlib.nullcontext():
+            reports = self._worker_cycles.query(cycle_id=cycle.id, is_completed=True)
+            diffs = [r.diff for r in reports]  # what :247-250 reads, at the query
         try:
             avg_plan, plan_key = hosted_plan(server_config, cycle, process_manager, plan_manager,
                                              getattr(aggregator, "mean_plans", None))
-            new_ckpt = aggregator.average_plan_diffs(server_config, _checkpoint.value,
-                                                     [r.diff for r in reports], avg_plan, plan_key=plan_key)
+            new_ckpt = aggregator.average_plan_diffs(server_config, _checkpoint.value, diffs, avg_plan,
+                                                     plan_key=plan_key)
         except PlanNotAcceleratedError as e:
             logging.info("engine declined (%s): running the reference averaging", e)
             return original(self, server_config, cycle)

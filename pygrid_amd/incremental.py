@@ -56,7 +56,9 @@ Report semantics (``cycle_manager.py:162-174``, ``fl_events.py:257-263``):
 
 Thread safety: the node calls ``reported`` from request handlers and ``close`` from its executor
 thread (``tasks/cycle.py``), and the deferred fold runs on a timer thread, so every method holds
-the cycle's lock (the engine context itself is single-owner).  A well-formed diff holding non-float32 tensors is accepted (the reference would
+the cycle's lock (the engine context itself is single-owner) -- except that once ``seal`` (the
+first half of ``close``) has run, ``reported`` / ``assigned`` return without taking it: a handler
+never waits for the close's fold.  A well-formed diff holding non-float32 tensors is accepted (the reference would
 average it with torch's type promotion): the cycle is then declined as a whole -- later reports
 are only recorded, and ``close`` raises ``ModelNotAcceleratedError`` so the node averages the cycle
 with its own code, from its DB.
@@ -151,6 +153,7 @@ class IncrementalCycle:
         self.last_close: dict = {}
         self._lock = threading.Lock()
         self._closed = False
+        self._close_order: Optional[List] = None  # set by seal(), taken by finish()
         self._declined: Optional[str] = None  # why the engine cannot average this cycle
         # one open cycle per engine: a previous one left open (dropped without close) is abandoned
         # here, so that its deferred-fold timer cannot touch this cycle's slots
@@ -193,6 +196,8 @@ class IncrementalCycle:
     def assigned(self, worker, key=None):
         """``worker`` was assigned to the cycle.  ``key`` orders the assignments (the WorkerCycle row
         id: the order the completed-WorkerCycle query returns rows in); default: call order."""
+        if self._closed:
+            return
         with self._lock:
             if worker in self._key_of or self._closed:
                 return
@@ -212,6 +217,9 @@ class IncrementalCycle:
     def reported(self, worker, diff: bytes):
         """The worker's (latest) diff.  Raises ``StateParseError`` for a malformed diff (see the
         module docstring); never raises for a late or repeated report."""
+        if self._closed:  # sealed: no waiting for the close's fold (set under the lock, read without)
+            log.info("worker %r reported after the cycle closed: ignored (fl_events.py:261-263)", worker)
+            return
         with self._lock:
             if self._closed:
                 log.info("worker %r reported after the cycle closed: ignored (fl_events.py:261-263)", worker)
@@ -495,7 +503,18 @@ class IncrementalCycle:
 
         ``order``: the workers of the completed-WorkerCycle query in the order the DB returned them
         (``:243-245``); ``fetch(w)``: that row's ``diff`` bytes (read only for diffs not held here).
-        Without ``order`` the assignment order of the reporters is taken as the query's."""
+        Without ``order`` the assignment order of the reporters is taken as the query's.
+        ``seal(order)`` then ``finish(checkpoint, ...)``."""
+        self.seal(order)
+        return self.finish(checkpoint, framing=framing, fetch=fetch)
+
+    def seal(self, order: Optional[Sequence[Hashable]] = None) -> bool:
+        """The close's snapshot (``cycle_manager.py:243-245``: the moment the reference's query reads
+        the completed rows): from here on reports and assignments are ignored at once, without the
+        cycle's lock, so a handler never waits for the fold.  Returns True when ``finish`` will read
+        diffs through ``fetch`` (a re-fold, diffs reported before a restart, parked diffs): the
+        caller then keeps later re-reports out of the DB rows until ``finish`` returns (the
+        reference reads every diff at its query)."""
         with self._lock:
             if self._closed:
                 raise AggregationError("cycle already closed")
@@ -520,6 +539,29 @@ class IncrementalCycle:
                 missing = [w for w in order if w not in self._weights_by_worker]
                 if missing:
                     raise AggregationError(f"workers {missing[:8]!r} have no aggregation weight")
+            self._close_order = order
+            return self._needs_fetch(order)
+
+    def _needs_fetch(self, order: List) -> bool:
+        """Whether folding ``order`` reads any diff through ``fetch``: a stale or re-folded early
+        fold, or a row whose diff is not in an HBM slot (parked, never seen; a full slab then also
+        gives up a later slot and re-reads it).  Rows between a rewind's mark and the common prefix
+        keep their slots (speculative folds free slots only before the base)."""
+        if self._stale:
+            return True
+        common = _common_prefix(self._folded, order)
+        if common < len(self._folded) and common < self._base:
+            return True
+        return any(w not in self._slot_of for w in order[common:])
+
+    def finish(self, checkpoint: bytes, framing: str = "fresh",
+               fetch: Optional[Callable[[object], bytes]] = None) -> bytes:
+        """The rest of ``close`` after ``seal``: fold, FINAL pass, new checkpoint bytes."""
+        with self._lock:
+            order = self._close_order
+            if order is None:
+                raise AggregationError("finish() without a successful seal()")
+            self._close_order = None
             folded_before = len(self._folded)
             refold = self._stale
             if not refold and not self._rewind(_common_prefix(self._folded, order)):
@@ -617,6 +659,8 @@ class IncrementalCycle:
     def abandon(self):
         """Another user takes the engine (its slab is re-laid): nothing held here survives.  Later
         reports are ignored and ``close`` raises; the node closes this cycle from its DB rows."""
+        if self._closed:  # sealed or closed: its result may be the resident checkpoint
+            return
         with self._lock:
             if self._closed:  # closed (or abandoned) already: its result may be the resident checkpoint
                 return

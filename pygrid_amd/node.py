@@ -38,6 +38,22 @@ cycle closes through the close-time path over its DB rows -- bit-identical eithe
 node restart the open cycle's state is rebuilt from its WorkerCycle rows: the diffs reported
 before the restart are read from the DB at close.
 
+Concurrency (the reference serves handlers on a gevent hub -- ``pywsgi.WSGIServer``,
+``apps/node/src/__main__.py:85``, or gunicorn's ``flask_sockets.worker``, ``entrypoint.sh:2`` -- and
+closes on Flask-Executor's thread, ``tasks/cycle.py:9-25``): a handler never waits for a close.
+
+* the **report gate** (``_Gate``): a report holds it shared across its DB write and the ingest
+  (``submit_worker_diff`` + ``on_report``); a close holds it exclusively only while it reads the
+  completed rows and seals the cycle (``IncrementalCycle.seal``) -- the moment the reference's
+  query at ``cycle_manager.py:243-250`` reads the diffs.  A re-report lands wholly before the
+  snapshot (its diff is the one averaged) or wholly after it (ignored, as by the reference's close
+  that already read the rows).  Only a close that must read diffs from the DB (a re-fold, diffs
+  reported before a restart) keeps the gate until those reads are done;
+* after the seal, reports and assignments of the closing cycle return at once (no cycle lock);
+* the **engine lock** serialises engine users: closes take it (blocking, on the executor); a
+  handler that would prepare a cycle's report-time state while a close holds it skips that
+  (``_cycle_state`` returns None) -- the diffs are then read from the DB at that cycle's close.
+
 Nothing runs at import: ``install`` is the opt-in, ``uninstall`` restores every patched name.
 """
 from __future__ import annotations
@@ -120,7 +136,9 @@ class NodeEngine:
             else None
         self._cycles: Dict[object, object] = {}  # cycle id -> IncrementalCycle | _DECLINED | _ELSEWHERE
         self._owner = None  # the cycle id whose IncrementalCycle holds the engine
-        self._lock = threading.RLock()
+        self._lock = threading.RLock()  # the maps above; held only briefly
+        self._gate = _Gate()  # reports (shared) vs a close's snapshot of the rows (exclusive)
+        self._engine_lock = threading.RLock()  # closes / cycle preparation vs each other
         self._hold = threading.local()
         self._patched: list = []
         self.stats = {"closes_report_time": 0, "closes_close_time": 0, "closes_declined": 0, "refolds": 0,
@@ -139,7 +157,8 @@ class NodeEngine:
         orig = {n: getattr(CM, n) for n in ("assign", "submit_worker_diff", "_average_plan_diffs", "create")}
         orig_run = self.mod.run_task_once
         close_time = make_average_plan_diffs(self.aggregator, self.model_manager, self.process_manager,
-                                             self.plan_manager, original=orig["_average_plan_diffs"])
+                                             self.plan_manager, original=orig["_average_plan_diffs"],
+                                             gate=self._gate.exclusive)
 
         def assign(cm, worker, cycle, hash_key):
             wc = orig["assign"](cm, worker, cycle, hash_key)
@@ -147,7 +166,7 @@ class NodeEngine:
             return wc
 
         def submit_worker_diff(cm, worker_id, request_key, diff):
-            with node._holding_triggers() as held:
+            with node._gate.shared(), node._holding_triggers() as held:
                 orig["submit_worker_diff"](cm, worker_id, request_key, diff)  # the DB write, :162-174
                 node.on_report(cm, worker_id, request_key, diff)
             for name, func, args in held:  # :176-178, after the diff is in HBM
@@ -231,26 +250,35 @@ class NodeEngine:
     # ---- report-time state -------------------------------------------------------------------
     def _cycle_state(self, cm, cycle, create: bool = True):
         """The cycle's IncrementalCycle (made on first use, from its DB rows after a restart), or a
-        marker saying why there is none."""
-        with self._lock:
-            got = self._cycles.get(cycle.id)
-            if got is not None or not create:
-                return got
-            if not self.report_time or getattr(cycle, "is_completed", False):
-                return None
-            if self._owner is not None and self._owner != cycle.id and \
-                    isinstance(self._cycles.get(self._owner), IncrementalCycle):
-                self._cycles[cycle.id] = _ELSEWHERE  # the engine serves another open cycle
-                return _ELSEWHERE
-            try:
-                inc = self._new_cycle(cm, cycle)
-            except PlanNotAcceleratedError as e:
-                log.info("cycle %s: %s -- the node averages it", cycle.id, e)
-                self._cycles[cycle.id] = _DECLINED
-                return _DECLINED
-            self._cycles[cycle.id] = inc
-            self._owner = cycle.id
-            return inc
+        marker saying why there is none.  None (nothing recorded, retried on the next call) while
+        another thread's close holds the engine: a handler does not wait for it."""
+        got = self._cycles.get(cycle.id)
+        if got is not None or not create:
+            return got
+        if not self.report_time or getattr(cycle, "is_completed", False):
+            return None
+        if not self._engine_lock.acquire(blocking=False):
+            return None
+        try:
+            with self._lock:
+                got = self._cycles.get(cycle.id)
+                if got is not None:
+                    return got
+                if self._owner is not None and self._owner != cycle.id and \
+                        isinstance(self._cycles.get(self._owner), IncrementalCycle):
+                    self._cycles[cycle.id] = _ELSEWHERE  # the engine serves another open cycle
+                    return _ELSEWHERE
+                try:
+                    inc = self._new_cycle(cm, cycle)
+                except PlanNotAcceleratedError as e:
+                    log.info("cycle %s: %s -- the node averages it", cycle.id, e)
+                    self._cycles[cycle.id] = _DECLINED
+                    return _DECLINED
+                self._cycles[cycle.id] = inc
+                self._owner = cycle.id
+                return inc
+        finally:
+            self._engine_lock.release()
 
     def _new_cycle(self, cm, cycle) -> IncrementalCycle:
         server_config, _ = self.process_manager.get_configs(id=cycle.fl_process_id)
@@ -315,34 +343,58 @@ class NodeEngine:
 
     # ---- close ---------------------------------------------------------------------------------
     def average_plan_diffs(self, cm, server_config, cycle, close_time: Callable, original: Callable):
-        with self._lock:
-            st = self._cycles.pop(cycle.id, None)
-            if self._owner == cycle.id:
-                self._owner = None
-            if st == _DECLINED:
-                self.stats["closes_declined"] += 1
-                return original(cm, server_config, cycle)
-            if not isinstance(st, IncrementalCycle):
-                self._abandon_others()  # the close-time path re-lays the engine's slab
-                self.stats["closes_close_time"] += 1
-                return close_time(cm, server_config, cycle)
-            model = self.model_manager.get(fl_process_id=cycle.fl_process_id)
-            ckpt = self.model_manager.load(model_id=model.id)
-            rows = completed_rows(cm, cycle.id)
-            by_id = {r.id: r for r in rows}
+        """The close (executor thread).  Holds the engine lock throughout, the report gate only for
+        the snapshot of the completed rows (see the module docstring)."""
+        with self._engine_lock:
+            model = ckpt = None
+            if isinstance(self._cycles.get(cycle.id), IncrementalCycle):
+                model = self.model_manager.get(fl_process_id=cycle.fl_process_id)
+                ckpt = self.model_manager.load(model_id=model.id)
+            self._gate.acquire_exclusive()  # no report is between its DB write and its ingest now
+            gated = True
             try:
-                new = st.close(ckpt.value, framing=self.framing, order=[r.id for r in rows],
-                               fetch=lambda rid: by_id[rid].diff)
+                with self._lock:
+                    st = self._cycles.pop(cycle.id, None)
+                    if self._owner == cycle.id:
+                        self._owner = None
+                    if not isinstance(st, IncrementalCycle) and st != _DECLINED:
+                        self._abandon_others()  # the close-time path re-lays the engine's slab
+                if not isinstance(st, IncrementalCycle):
+                    self._gate.release_exclusive()  # the close-time path takes it for its query
+                    gated = False
+                    if st == _DECLINED:
+                        self.stats["closes_declined"] += 1
+                        return original(cm, server_config, cycle)
+                    self.stats["closes_close_time"] += 1
+                    return close_time(cm, server_config, cycle)
+                if ckpt is None:
+                    model = self.model_manager.get(fl_process_id=cycle.fl_process_id)
+                    ckpt = self.model_manager.load(model_id=model.id)
+                rows = completed_rows(cm, cycle.id)
+                by_id = {r.id: r for r in rows}
+                if not st.seal(order=[r.id for r in rows]):
+                    self._gate.release_exclusive()  # every diff the fold needs is in HBM
+                    gated = False
+                new = st.finish(ckpt.value, framing=self.framing, fetch=lambda rid: by_id[rid].diff)
             except PlanNotAcceleratedError as e:  # incl. ModelNotAcceleratedError: a non-float32 diff
                 log.info("engine declined cycle %s (%s): running the reference averaging", cycle.id, e)
                 self.stats["closes_declined"] += 1
+                if gated:
+                    self._gate.release_exclusive()
+                    gated = False
                 return original(cm, server_config, cycle)
             except AggregationError as e:
                 log.warning("report-time close of cycle %s failed (%s): close-time path over the DB rows",
                             cycle.id, e)
                 self.aggregator._resident = None
                 self.stats["closes_close_time"] += 1
+                if gated:
+                    self._gate.release_exclusive()
+                    gated = False
                 return close_time(cm, server_config, cycle)
+            finally:
+                if gated:
+                    self._gate.release_exclusive()
             self.stats["closes_report_time"] += 1
             self.stats["refolds"] += int(st.last_close.get("refold", False))
             self.stats["diffs_from_db"] += st.last_close.get("from_db", 0)
@@ -356,6 +408,54 @@ class NodeEngine:
                 st.abandon()
                 self._cycles[cid] = _ELSEWHERE
         self._owner = None
+
+
+class _Gate:
+    """Shared (reports: DB write + ingest) / exclusive (a close's snapshot of the rows) lock.  A
+    waiting close keeps new reports out, so it waits only for the reports already in flight."""
+
+    def __init__(self):
+        self._cv = threading.Condition(threading.Lock())
+        self._shared = 0
+        self._exclusive = False
+        self._waiting = 0
+
+    @contextlib.contextmanager
+    def shared(self):
+        with self._cv:
+            while self._exclusive or self._waiting:
+                self._cv.wait()
+            self._shared += 1
+        try:
+            yield
+        finally:
+            with self._cv:
+                self._shared -= 1
+                if not self._shared:
+                    self._cv.notify_all()
+
+    def acquire_exclusive(self):
+        with self._cv:
+            self._waiting += 1
+            try:
+                while self._exclusive or self._shared:
+                    self._cv.wait()
+            finally:
+                self._waiting -= 1
+            self._exclusive = True
+
+    def release_exclusive(self):
+        with self._cv:
+            self._exclusive = False
+            self._cv.notify_all()
+
+    @contextlib.contextmanager
+    def exclusive(self):
+        self.acquire_exclusive()
+        try:
+            yield
+        finally:
+            self.release_exclusive()
 
 
 class _Base64:

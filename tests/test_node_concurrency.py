@@ -1,0 +1,205 @@
+"""CPU: the installed node under concurrency.
+
+The reference runs report handlers on a gevent hub (``apps/node/src/__main__.py:85``,
+``entrypoint.sh:2``) and the close on Flask-Executor's thread (``tasks/cycle.py:9-25``): a handler
+that waits for a close stalls every client.  These tests run the close on a real executor thread,
+block it inside the fold, and check that
+
+* a late report, a re-report and an assignment of the closing cycle, and a report of another FL
+  process's cycle, each return within milliseconds while the close is blocked;
+* a re-report whose DB write is in flight when the close starts is averaged (its DB write and its
+  ingest are atomic with respect to the close's snapshot of the rows), and a re-report that lands
+  after the snapshot is ignored -- in both cases the saved checkpoints are byte-identical to the
+  reference node run with the same events in the equivalent serial order.
+
+Node: tests/fake_node.py; engine: tests/fake_engine.py (folds by the C oracle)."""
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+from fake_engine import NumpyEngine
+from fake_node import assign, host_process, make_node
+from pygrid_amd import node as pnode
+from test_node_wiring import ckpt_bytes, diff_bytes
+
+CFG3 = {"min_diffs": 3, "max_diffs": 3, "num_cycles": 0}
+FAST_S = 0.25  # "returns at once": generous for a loaded CI box, far below a blocked close
+
+
+class NamedExecutor:
+    """``run_task_once`` as the reference has it (``tasks/cycle.py:9-25``): one named future; a
+    request while it runs is skipped."""
+
+    def __init__(self):
+        self.pool = ThreadPoolExecutor(1, thread_name_prefix="executor")
+        self.futures = {}
+
+    def run_task_once(self, name, func, *args):
+        f = self.futures.get(name)
+        if f is None or f.done():
+            self.futures[name] = self.pool.submit(func, *args)
+
+    def wait(self, timeout=10):
+        for f in list(self.futures.values()):
+            f.result(timeout)
+
+
+class BlockingEngine(NumpyEngine):
+    """The fold's FINAL pass waits for ``release`` (a close stuck on the GPU)."""
+
+    def __init__(self):
+        super().__init__()
+        self.entered = threading.Event()
+        self.release = threading.Event()
+
+    def fold_slots_finish_resident(self, mode, slots=()):
+        self.entered.set()
+        assert self.release.wait(20), "test never released the close"
+        return super().fold_slots_finish_resident(mode, slots)
+
+
+def checkpoints(mod):
+    rows = sorted(mod.model_manager._model_checkpoints.rows, key=lambda r: r.id)
+    return [(r.number, r.alias, r.value) for r in rows]
+
+
+def timed(fn, *a):
+    t0 = time.perf_counter()
+    fn(*a)
+    return time.perf_counter() - t0
+
+
+def test_handlers_never_wait_for_a_blocked_close():
+    ex = NamedExecutor()
+    mod = make_node()
+    mod.run_task_once = ex.run_task_once
+    eng = BlockingEngine()
+    node = pnode.install(mod, engine=eng, framing="template", fold_batch=1)
+    cm = mod.cycle_manager
+    proc, _, _ = host_process(mod, CFG3, ckpt_bytes())
+    other, _, _ = host_process(mod, CFG3, ckpt_bytes(1))  # a second FL process on the same node
+    keys = {w: assign(mod, w, proc) for w in range(1, 5)}
+    okey = assign(mod, 9, other)
+    for w in (1, 2, 3):
+        cm.submit_worker_diff(w, keys[w], diff_bytes(w))
+    assert eng.entered.wait(10), "the close never reached the fold"
+    try:
+        took = {
+            "late report": timed(cm.submit_worker_diff, 4, keys[4], diff_bytes(4)),
+            "re-report": timed(cm.submit_worker_diff, 1, keys[1], diff_bytes(1, version=7)),
+            "assign": timed(assign, mod, 5, proc),
+            "other process": timed(cm.submit_worker_diff, 9, okey, diff_bytes(9)),
+        }
+        assert all(t < FAST_S for t in took.values()), took
+        assert not ex.futures["complete_cycle"].done()  # the close really was blocked meanwhile
+    finally:
+        eng.release.set()
+    ex.wait()
+    node.uninstall()
+
+    # the reference with the same events, serially: the close read the rows before the late ones
+    ref = make_node()
+    rproc, _, _ = host_process(ref, CFG3, ckpt_bytes())
+    host_process(ref, CFG3, ckpt_bytes(1))
+    rkeys = {w: assign(ref, w, rproc) for w in range(1, 5)}
+    for w in (1, 2, 3):
+        ref.cycle_manager.submit_worker_diff(w, rkeys[w], diff_bytes(w))
+    assert checkpoints(mod) == checkpoints(ref)
+    assert len(checkpoints(mod)) == 3  # 2 initial + the closed cycle of process 1
+    assert node.stats["closes_report_time"] == 1
+
+
+class SlowUpdateWarehouse:
+    """Wraps the worker-cycle warehouse: ``update`` (the commit of ``submit_worker_diff``,
+    ``cycle_manager.py:174``) of a chosen thread blocks until released."""
+
+    def __init__(self, wh):
+        self.wh = wh
+        self.block_thread = None
+        self.in_update = threading.Event()
+        self.release = threading.Event()
+
+    def __getattr__(self, name):
+        return getattr(self.wh, name)
+
+    def update(self):
+        if threading.current_thread() is self.block_thread:
+            self.in_update.set()
+            assert self.release.wait(20)
+        return self.wh.update()
+
+
+def test_rereport_in_flight_at_the_close_is_averaged():
+    """the re-report's DB write has landed (the row holds the new diff) but its
+    ingest has not, when the last report triggers the close.  The close must average the new diff,
+    as the reference's query at :243-250 -- which reads the committed row -- does."""
+    ex = NamedExecutor()
+    mod = make_node()
+    mod.run_task_once = ex.run_task_once
+    node = pnode.install(mod, engine=NumpyEngine(), framing="template", fold_batch=1)
+    cm = mod.cycle_manager
+    slow = SlowUpdateWarehouse(cm._worker_cycles)
+    cm._worker_cycles = slow
+    proc, _, _ = host_process(mod, CFG3, ckpt_bytes())
+    keys = {w: assign(mod, w, proc) for w in range(1, 4)}
+    cm.submit_worker_diff(1, keys[1], diff_bytes(1))
+    cm.submit_worker_diff(2, keys[2], diff_bytes(2))
+
+    t = threading.Thread(target=cm.submit_worker_diff, args=(1, keys[1], diff_bytes(1, version=5)))
+    slow.block_thread = t
+    t.start()
+    assert slow.in_update.wait(10)
+    cm.submit_worker_diff(3, keys[3], diff_bytes(3))  # triggers the close on the executor
+    deadline = time.monotonic() + 10
+    while node._gate._waiting == 0 and time.monotonic() < deadline:  # the close waits for the gate
+        time.sleep(0.005)
+    assert node._gate._waiting == 1
+    slow.release.set()
+    t.join(10)
+    ex.wait()
+    node.uninstall()
+
+    ref = make_node()
+    rproc, _, _ = host_process(ref, CFG3, ckpt_bytes())
+    rkeys = {w: assign(ref, w, rproc) for w in range(1, 4)}
+    rcm = ref.cycle_manager
+    rcm.submit_worker_diff(1, rkeys[1], diff_bytes(1))
+    rcm.submit_worker_diff(2, rkeys[2], diff_bytes(2))
+    rcm.submit_worker_diff(1, rkeys[1], diff_bytes(1, version=5))
+    rcm.submit_worker_diff(3, rkeys[3], diff_bytes(3))
+    assert checkpoints(mod) == checkpoints(ref)
+    assert len(checkpoints(mod)) == 2
+
+
+def test_gate_close_waits_only_for_reports_in_flight():
+    g = pnode._Gate()
+    order = []
+    entered = threading.Event()
+    go = threading.Event()
+
+    def report():
+        with g.shared():
+            entered.set()
+            go.wait(10)
+            order.append("report")
+
+    t = threading.Thread(target=report)
+    t.start()
+    entered.wait(10)
+
+    def close():
+        with g.exclusive():
+            order.append("close")
+
+    c = threading.Thread(target=close)
+    c.start()
+    while g._waiting == 0:
+        time.sleep(0.001)
+    late = threading.Thread(target=lambda: (g.shared().__enter__(), order.append("late")))
+    late.start()
+    time.sleep(0.05)
+    assert order == []  # the late report queues behind the waiting close
+    go.set()
+    for th in (t, c, late):
+        th.join(10)
+    assert order == ["report", "close", "late"]
