@@ -1148,13 +1148,20 @@ def e2e_close(ctx, args, eng, n_clients: int, steps: int = 2):
                           "State bytes in host memory -> new checkpoint bytes (BASELINE.md cycle close; PCIe-inclusive)"}
 
 
-def report_close(ctx, args, eng, cycles: int = 4, gap_ms: float = 5.0, assigned: int = 100):
-    """The close as a node running report-time aggregation sees it: per cycle
-    `assigned` ResNet-18 workers, ~20 % never report (worker 0 among them, routes.py:314), the rest in
-    shuffled order `gap_ms` apart (a node decodes each report's base64 for 4-5 ms anyway,
-    tools/node_sim.py); each State diff goes to HBM and is folded when reported; the close
-    (cycle_manager.py:217 -> :240-303) = what the DB order still changes + the new checkpoint bytes.
-    Wall time of IncrementalCycle.close after the last report returned; 1 warm-up cycle."""
+def report_close(ctx, args, eng, cycles: int = 4, assigned: int = 100):
+    """The close as a node running report-time aggregation sees it, triggered
+    the way the reference triggers it: the report that completes the cycle requests the close
+    (``submit_worker_diff`` -> ``run_task_once("complete_cycle", ...)``, cycle_manager.py:176-178)
+    and Flask-Executor runs it on its own thread (tasks/cycle.py:9-25).  Per cycle `assigned`
+    ResNet-18 workers, ~20 % never report (worker 0 among them, routes.py:314), the rest in shuffled
+    order, each State diff to HBM (and folded) when reported.  Timed: from the last report's
+    ``reported`` returning to the new checkpoint bytes ready on the executor thread -- nothing
+    waits between the two, nothing syncs the GPU before the clock starts.  Two arrival patterns
+    (reports `paced` 5 ms apart -- a node decodes each report's base64 for a few ms anyway,
+    tools/node_sim.py -- and `back_to_back`) x speculative / certain-only early folds; the headline
+    is the product default (`IncrementalCycle(speculate=None)`), paced.  1 warm-up cycle each."""
+    from concurrent.futures import ThreadPoolExecutor
+
     import numpy as np
 
     from pygrid_amd.incremental import IncrementalCycle
@@ -1167,26 +1174,38 @@ def report_close(ctx, args, eng, cycles: int = 4, gap_ms: float = 5.0, assigned:
     distinct = [build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2)
                                   for s in RESNET18_SHAPES]) for _ in range(4)]
     reporters = [w for w in range(assigned) if w != 0 and rng.random() >= 0.2]
-    closes, left = [], []
-    for cyc in range(cycles + 1):
-        inc = IncrementalCycle(eng, numel, slots=assigned, checkpoint=ck_pb)
-        for w in range(assigned):
-            inc.assigned(w)
-        for w in rng.permutation(reporters):
-            inc.reported(int(w), distinct[int(w) % 4])
-            time.sleep(gap_ms / 1e3)
-        t0 = time.perf_counter()
-        ck_pb = inc.close(ck_pb)
-        if cyc:
-            closes.append((time.perf_counter() - t0) * 1e3)
-            left.append(inc.last_close["n"] - inc.last_close["early"])
-    return {"close_ms_after_last_report": round(float(np.median(closes)), 3),
-            "closes_ms": [round(c, 3) for c in closes], "assigned": assigned, "reporters": len(reporters),
-            "rows_left_to_fold_at_close": int(np.median(left)), "report_gap_ms": gap_ms,
-            "speculative_folds": inc.speculate, "gpus": ctx.n_gpus,
-            "definition": "wall time of IncrementalCycle.close after the last report (report-time aggregation, "
-                          "cycles chained through the resident checkpoint): fold what the DB order still changes "
-                          "+ new checkpoint bytes (PCIe-inclusive D2H)"}
+    arms = {}
+    with ThreadPoolExecutor(1, thread_name_prefix="executor") as executor:
+        for arrival, gap_ms in (("paced", 5.0), ("back_to_back", 0.0)):
+            for speculate in (None, False):
+                closes, left = [], []
+                for cyc in range(cycles + 1):
+                    inc = IncrementalCycle(eng, numel, slots=assigned, checkpoint=ck_pb, speculate=speculate)
+                    for w in range(assigned):
+                        inc.assigned(w)
+                    for i, w in enumerate(rng.permutation(reporters)):
+                        if i and gap_ms:
+                            time.sleep(gap_ms / 1e3)  # between reports; none after the last one
+                        inc.reported(int(w), distinct[int(w) % 4])
+                    t0 = time.perf_counter()
+                    ck_pb = executor.submit(inc.close, ck_pb).result()
+                    if cyc:
+                        closes.append((time.perf_counter() - t0) * 1e3)
+                        left.append(inc.last_close["n"] - inc.last_close["early"])
+                arm = "speculative" if inc.speculate else "certain_only"
+                if speculate is None:
+                    default = inc.speculate
+                arms[f"{arrival}_{arm}"] = {"close_ms": round(float(np.median(closes)), 3),
+                                            "closes_ms": [round(c, 3) for c in closes],
+                                            "rows_left_to_fold_at_close": int(np.median(left))}
+    head = arms["paced_" + ("speculative" if default else "certain_only")]
+    return {"close_ms_after_last_report": head["close_ms"], "arms": arms, "default_speculative": default,
+            "assigned": assigned, "reporters": len(reporters), "gpus": ctx.n_gpus,
+            "definition": "the reference's trigger: the last report's handler returns, the close runs at once on "
+                          "an executor thread (run_task_once, cycle_manager.py:176-178); timed from that return "
+                          "to the new checkpoint bytes (fold what the DB order still changes + FINAL pass + "
+                          "PCIe D2H + State framing), no pause and no GPU sync in between; headline = product "
+                          "default, reports paced 5 ms apart; cycles chained through the resident checkpoint"}
 
 
 def group_exchange(eng) -> str:

@@ -84,18 +84,29 @@ def completed_rows(cm, cycle_id):
     return _rows(cm, cycle_id=cycle_id, is_completed=True)
 
 
-def _rows(cm, **filters):
-    wh = cm._worker_cycles
-    schema = getattr(wh, "_schema", None)
+def _deferred(cm):
+    """``WorkerCycle.query`` with the ``diff`` blob deferred (SQLAlchemy), or None."""
+    schema = getattr(cm._worker_cycles, "_schema", None)
     q = getattr(schema, "query", None)
     if q is not None and hasattr(schema, "diff"):
         try:
             from sqlalchemy.orm import defer
 
-            return q.options(defer(schema.diff)).filter_by(**filters).all()
+            return q.options(defer(schema.diff))
         except ImportError:
             pass
-    return wh.query(**filters)
+    return None
+
+
+def _rows(cm, **filters):
+    q = _deferred(cm)
+    return q.filter_by(**filters).all() if q is not None else cm._worker_cycles.query(**filters)
+
+
+def _first_row(cm, **filters):
+    """``Warehouse.first`` without reading the row's diff back (the handler just wrote it)."""
+    q = _deferred(cm)
+    return q.filter_by(**filters).first() if q is not None else cm._worker_cycles.first(**filters)
 
 
 class NodeEngine:
@@ -327,7 +338,7 @@ class NodeEngine:
         """After the reference's DB write.  Never raises: the response stays the reference's, and a
         diff the engine could not take is read from the DB at close."""
         try:
-            wc = cm._worker_cycles.first(worker_id=worker_id, request_key=request_key)
+            wc = _first_row(cm, worker_id=worker_id, request_key=request_key)
             st = self._cycles.get(wc.cycle_id)
             if st is None and self.report_time:
                 cycle = cm._cycles.first(id=wc.cycle_id)

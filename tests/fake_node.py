@@ -1,5 +1,7 @@
 """Test infrastructure: an in-memory stand-in for the PyGrid Node pieces the engine's wiring
-touches (the reference node itself is not importable here: flask, sqlalchemy and syft are absent).
+touches.  The reference node itself is not importable here (syft, flask_sqlalchemy, flask_executor,
+gevent are absent; flask and sqlalchemy are present): tests/sql_node.py puts the same bookkeeping
+on real SQLAlchemy tables (``make_node(warehouse=...)``).
 
 * ``Warehouse`` -- ``core/warehouse.py`` over a list of rows: ``register`` (autoincrement id),
   ``query`` / ``first`` / ``count`` / ``last`` / ``modify`` / ``update``.  ``query`` returns rows
@@ -75,9 +77,9 @@ class ModelNotFoundError(Exception):
 
 
 class ModelManager:
-    def __init__(self):
-        self._models = Warehouse("model")
-        self._model_checkpoints = Warehouse("checkpoint")
+    def __init__(self, warehouse=Warehouse):
+        self._models = warehouse("model")
+        self._model_checkpoints = warehouse("checkpoint")
         self.db_loads = 0
 
     def create(self, model, process):  # model_manager.py:19-28
@@ -148,11 +150,12 @@ def complete_cycle(cycle_manager, cycle_id):  # tasks/cycle.py:28-37
         return e
 
 
-def make_node():
+def make_node(warehouse=Warehouse):
     """A fresh node: a module-like namespace holding what cycle_manager.py holds (CycleManager,
-    run_task_once, complete_cycle, model_manager, process_manager, PlanManager)."""
+    run_task_once, complete_cycle, model_manager, process_manager, PlanManager).  ``warehouse(name)``
+    makes the tables ("model", "checkpoint", "cycle", "worker_cycle")."""
     mod = types.SimpleNamespace()
-    mod.model_manager = ModelManager()
+    mod.model_manager = ModelManager(warehouse)
     mod.process_manager = ProcessManager()
     mod.PlanManager = PlanManager
     mod.run_task_once = run_task_once
@@ -160,8 +163,8 @@ def make_node():
 
     class CycleManager:
         def __init__(self):
-            self._cycles = Warehouse("cycle")
-            self._worker_cycles = Warehouse("worker_cycle")
+            self._cycles = warehouse("cycle")
+            self._worker_cycles = warehouse("worker_cycle")
             self.task_errors = []
 
         def create(self, fl_process_id, version, cycle_time):  # :28-54

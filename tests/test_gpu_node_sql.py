@@ -1,0 +1,52 @@
+"""GPU: the installed node on the real engine against the reference's storage types and report
+handler -- tests/test_node_sql.py's scenario with MNIST-sized diffs (784-392-10,
+1.2 MB State messages: the handler's clean base64 route) decoded into the library's page-locked
+blocks (``PinnedPool``), bound into SQLAlchemy's ``LargeBinary`` column, DMA'd to HBM as they lie
+(``pgh_ingest_state``) and folded at report time.  The saved checkpoints must be byte-identical to
+the reference node's torch close over the same DB rows; every block must come back to its pool."""
+import gc
+
+import numpy as np
+import pytest
+
+from test_node_sql import CFG, SqlScenario, run_both, script_three_cycles
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+MNIST = [(392, 784), (392,), (10, 392), (10,)]
+
+
+def mnist_ckpt():
+    from pygrid_amd.state_schema import build_state_fast
+
+    rng = np.random.default_rng(71)
+    return build_state_fast([(rng.standard_normal(s) * 0.05).astype(F) for s in MNIST])
+
+
+def mnist_diff(worker, version=0):
+    import zlib
+
+    from pygrid_amd.state_schema import build_state_fast
+
+    rng = np.random.default_rng([version, zlib.crc32(str(worker).encode()), 72])
+    return build_state_fast([(rng.standard_normal(s) * 10.0 ** rng.integers(-4, 0)).astype(F) for s in MNIST])
+
+
+@pytest.mark.parametrize("slots", [None, 2], ids=["slots-default", "slots-2"])
+@pytest.mark.parametrize("speculate", [False, True], ids=["certain-only", "speculative"])
+@pytest.mark.parametrize("threaded", [False, True], ids=["sync", "executor"])
+def test_installed_sql_node_with_pinned_reports_on_the_gpu(tmp_path, engine, speculate, slots, threaded):
+    def fresh_engine():  # a (re)started node process has nothing resident in HBM
+        engine.reset()
+        engine.ckpt_owner = None
+        return engine
+
+    eng = run_both(tmp_path, script_three_cycles, engine=fresh_engine, ckpt=mnist_ckpt(), diff_fn=mnist_diff,
+                   threaded=threaded, pinned_reports=4, speculate=speculate, slots=slots)
+    st = eng.stats
+    assert st["closes_report_time"] == 3 and st["closes_close_time"] == 0 and st["report_errors"] == 0, st
+    gc.collect()
+    pools = [(p.hits, p.misses, p.blocks) for p in eng.pools]
+    # every report decoded into a page-locked block; every block freed once its views were gone
+    assert pools == [(12, 0, 0), (2, 0, 0)], pools
+    assert CFG["num_cycles"] == 3

@@ -1,0 +1,236 @@
+"""CPU: ``pygrid_amd.node.install`` against the reference node's real storage types and report
+handler code.
+
+The node's tables live in SQLAlchemy on a SQLite file (tests/sql_node.py: the reference's columns,
+``WorkerCycle.diff`` a ``LargeBinary``, ``Model.query`` from a thread-scoped session, the
+reference's ``Warehouse``); clients report through the reference's handler restated
+(tests/ref_fl_events.py: ``base64.b64decode(data.get(CYCLE.DIFF).encode())``, fl_events.py:257).
+Each script runs on two fresh nodes -- as shipped, and after ``install(..., report_module=
+ref_fl_events)`` -- and the saved ``ModelCheckPoint`` rows, read back through a session of their
+own, must be byte-identical.  Also checked:
+
+* the installed handler's decoded diffs are read-only memoryviews over pool blocks, SQLAlchemy binds
+  them into the ``LargeBinary`` column, and every row reads back byte-identical to the decoded diff
+  after commit (and expire-on-commit) -- and every block comes back to the pool;
+* the close reads the completed rows with ``defer(WorkerCycle.diff)`` (``node._rows``): the blobs
+  of diffs already in HBM are never loaded;
+* the close running on an executor thread (its own session) reads what the handler threads
+  committed.
+
+Engine: tests/fake_engine.py (folds by the C oracle); the GPU version of this test is
+tests/test_gpu_node_sql.py."""
+import base64
+import collections
+import gc
+import types
+
+import pytest
+import sqlalchemy.orm
+from sqlalchemy import inspect
+
+import ref_fl_events
+from fake_engine import NumpyEngine
+from fake_node import assign, host_process
+from pygrid_amd import node as pnode
+from sql_node import HeapPool, make_sql_node
+from test_node_concurrency import NamedExecutor
+from test_node_wiring import ckpt_bytes, diff_bytes
+
+CFG = {"min_diffs": 3, "max_diffs": 4, "num_cycles": 3}
+
+
+class SqlScenario:
+    def __init__(self, path, installed: bool, threaded: bool = False, pool: bool = False, engine=None,
+                 cfg=CFG, ckpt=None, diff_fn=diff_bytes, **opts):
+        self.mod, self.store = make_sql_node(f"sqlite:///{path}")
+        self.ex = NamedExecutor() if threaded else None
+        if self.ex:
+            self.mod.run_task_once = self.ex.run_task_once
+        self.installed = installed
+        self.engine_factory = engine or NumpyEngine
+        self.opts = {"framing": "template", "report_module": ref_fl_events, "pinned_reports": 0, **opts}
+        self.use_pool = pool
+        self.pools = []  # one per (re)start of the node process
+        self.node = None
+        self.before_restart = collections.Counter()
+        self.sent = {}  # (worker) -> the latest diff bytes it reported
+        self.diff_fn = diff_fn
+        if installed:
+            self._install()
+        ref_fl_events.processes = types.SimpleNamespace(
+            submit_diff=lambda *a: self.mod.cycle_manager.submit_worker_diff(*a))
+        self.proc, _, _ = host_process(self.mod, cfg, ckpt if ckpt is not None else ckpt_bytes())
+        self.keys = {}
+
+    def _install(self):
+        self.node = pnode.install(self.mod, engine=self.engine_factory(), **self.opts)
+        if self.use_pool:  # the handler's pool: ordinary memory on a CPU box
+            self.node.pinned = HeapPool(max_blocks=4)
+            ref_fl_events.base64._pool = self.node.pinned
+        if self.node.pinned is not None:
+            self.pools.append(self.node.pinned)
+
+    @property
+    def pool(self):
+        return self.pools[-1]
+
+    def restart(self):
+        if self.installed:
+            self.node.uninstall()
+            self.before_restart.update(self.node.stats)
+            self._install()
+
+    @property
+    def stats(self):
+        """The node's counters summed over its restarts."""
+        return self.before_restart + collections.Counter(self.node.stats)
+
+    def assign(self, *workers):
+        for w in workers:
+            self.keys[w] = assign(self.mod, w, self.proc)
+
+    def report(self, w, version=0, payload=None):
+        diff = payload if payload is not None else self.diff_fn(w, version)
+        msg = {"data": {"worker_id": w, "request_key": self.keys[w], "diff": base64.b64encode(diff).decode()}}
+        resp = ref_fl_events.report(msg)
+        assert resp["data"] == {"status": "success"}, resp
+        self.sent[w] = diff
+        if self.ex:
+            self.ex.wait()
+        return resp
+
+    def checkpoints(self):
+        s = self.store.fresh_session()
+        try:
+            rows = s.query(self.store.ModelCheckPoint).order_by(self.store.ModelCheckPoint.id).all()
+            return [(r.number, r.alias, bytes(r.value)) for r in rows]
+        finally:
+            s.close()
+
+    def diffs_in_db(self):
+        s = self.store.fresh_session()
+        try:
+            return {(r.cycle_id, r.worker_id): r.diff for r in s.query(self.store.WorkerCycle).all()
+                    if r.diff is not None}
+        finally:
+            s.close()
+
+    def finish(self):
+        if self.node is not None:
+            self.node.uninstall()
+        self.store.close()
+
+
+def script_three_cycles(sc: SqlScenario):
+    """Re-report, late report, a restart mid-cycle, workers that never report."""
+    sc.assign("w1", "w2", "w3", "w4", "w5", "w6")
+    sc.report("w2")
+    sc.report("w1")
+    sc.report("w5")
+    sc.report("w2", version=1)  # re-report: the latest diff is averaged at w2's row position
+    sc.report("w6")  # 4 = max_diffs: the close
+    sc.report("w3")  # late: stored, ignored (cycle_manager.py:186-188)
+    sc.assign("w1", "w2", "w3", "w4", "w5")
+    for w in ("w5", "w4", "w3", "w1"):
+        sc.report(w, version=2)
+    sc.assign("w1", "w2", "w3", "w4")
+    sc.report("w1", version=3)
+    sc.report("w2", version=3)
+    sc.restart()  # the node process restarts: the DB stays
+    sc.report("w3", version=3)
+    sc.report("w4", version=3)
+
+
+def run_both(tmp_path, script, **kw):
+    out = []
+    for installed in (False, True):
+        sc = SqlScenario(tmp_path / f"node_{int(installed)}.db", installed, **kw)
+        try:
+            script(sc)
+            out.append((sc.checkpoints(), sc.diffs_in_db(), sc))
+        finally:
+            sc.finish()
+    (ref_ck, ref_db, _), (eng_ck, eng_db, eng) = out
+    assert len(ref_ck) == 4  # the initial checkpoint + three closed cycles
+    assert eng_ck == ref_ck
+    assert eng_db == ref_db
+    return eng
+
+
+@pytest.mark.parametrize("threaded", [False, True], ids=["sync", "executor"])
+@pytest.mark.parametrize("pool", [False, True], ids=["bytes", "pooled-views"])
+def test_installed_sql_node_saves_the_reference_bytes(tmp_path, monkeypatch, threaded, pool):
+    deferred = []
+    real_defer = sqlalchemy.orm.defer
+    monkeypatch.setattr(sqlalchemy.orm, "defer", lambda *a, **k: deferred.append(a) or real_defer(*a, **k))
+    eng = run_both(tmp_path, script_three_cycles, threaded=threaded, pool=pool)
+    st = eng.stats
+    assert st["closes_report_time"] == 3 and st["closes_close_time"] == 0, st
+    assert st["report_errors"] == 0
+    assert st["diffs_from_db"] >= 2  # the two cycle-3 reports made before the restart
+    assert deferred, "the close never read the completed rows with defer(WorkerCycle.diff)"
+    if pool:
+        gc.collect()
+        hits = [(p.hits, p.misses, p.outstanding) for p in eng.pools]
+        assert hits == [(12, 0, 0), (2, 0, 0)], hits  # every report decoded into a block, all given back
+
+
+def test_pooled_view_binds_into_largebinary_and_reads_back(tmp_path):
+    """The installed handler's diff: a read-only memoryview over a pool block, stored by
+    submit_worker_diff into WorkerCycle.diff; after the commit the row reads back (this session,
+    after expire-on-commit, and a fresh one) byte-identical."""
+    sc = SqlScenario(tmp_path / "n.db", installed=True, pool=True)
+    try:
+        seen = []
+        orig = sc.mod.CycleManager.submit_worker_diff
+
+        def spy(cm, worker_id, request_key, diff):
+            seen.append(diff)
+            return orig(cm, worker_id, request_key, diff)
+        sc.mod.CycleManager.submit_worker_diff = spy
+        sc.assign("a", "b")
+        wc = sc.mod.cycle_manager._worker_cycles.first(worker_id="a")  # the handler's session's row
+        sc.report("a", version=4)
+        assert isinstance(seen[0], memoryview) and seen[0].readonly
+        assert bytes(seen[0]) == sc.sent["a"]
+        # expired on commit; the reference's own ``_worker_cycle.cycle_id`` (cycle_manager.py:178)
+        # then refreshed the row: what the session holds now is the DB's copy, not the view
+        assert isinstance(inspect(wc).dict.get("diff"), bytes)
+        assert wc.diff == sc.sent["a"]
+        assert sc.diffs_in_db()[(wc.cycle_id, "a")] == sc.sent["a"]
+        del seen[:], wc
+        gc.collect()
+        assert sc.pool.outstanding == 0
+    finally:
+        sc.finish()
+
+
+def test_completed_rows_defer_the_diff_blobs(tmp_path):
+    sc = SqlScenario(tmp_path / "n.db", installed=True)
+    try:
+        sc.assign("a", "b", "c")
+        sc.report("b")
+        sc.report("a")
+        cm = sc.mod.cycle_manager
+        sc.store.session.expire_all()
+        rows = pnode.completed_rows(cm, sc.mod.cycle_manager.last(sc.proc.id).id)
+        assert [r.worker_id for r in rows] == ["a", "b"]  # row (assignment) order, not report order
+        assert all("diff" not in inspect(r).dict for r in rows)
+        assert [r.diff for r in rows] == [sc.sent["a"], sc.sent["b"]]  # loaded on access
+    finally:
+        sc.finish()
+
+
+def test_malformed_report_answers_like_the_reference(tmp_path):
+    """A bad base64 body: the installed decoder raises binascii.Error as base64 does, so the
+    handler's error response (its text up to the traceback) is the reference's."""
+    answers = []
+    for installed in (False, True):
+        sc = SqlScenario(tmp_path / f"m{int(installed)}.db", installed, pool=installed)
+        try:
+            sc.assign("a")
+            resp = ref_fl_events.report({"data": {"worker_id": "a", "request_key": sc.keys["a"], "diff": "QUJ"}})
+            answers.append(resp["data"]["error"].split("\n")[0])
+        finally:
+            sc.finish()
+    assert answers[0] == answers[1] and answers[0]

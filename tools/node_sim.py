@@ -1,130 +1,218 @@
 #!/usr/bin/env python3
-"""What a PyGrid node sees per cycle with the engine wired in: the
-report handler's work for each client (fl_events.py:257-261: the JSON's base64 diff text ->
-bytes -> submit), here `report.b64decode` + `IncrementalCycle.reported` (the diff straight into
-an HBM slot), and the close when the cycle ends (cycle_manager.py:217).  ResNet-18, 100 workers
-assigned per cycle, ~20 % never report (routes.py:314), shuffled arrival, several cycles chained
-through the resident checkpoint.
+"""What a PyGrid node sees per cycle with the engine installed, through
+the reference's own storage types and report handler code:
 
-    python tools/node_sim.py [cycles] [--pinned] [--tune] [--phases] [--no-speculate] [--close-gap-ms=50]
+* the node's tables in SQLAlchemy on SQLite (tests/sql_node.py: ``WorkerCycle.diff`` a
+  ``LargeBinary``, the reference's ``Warehouse``), in memory by default (``--db=PATH``: a file);
+* each client's report through the reference's handler restated (tests/ref_fl_events.py:
+  ``base64.b64decode(data.get(CYCLE.DIFF).encode())``, fl_events.py:257 -- the ``.encode()`` copy
+  of the 62 MB text included) -> ``submit_worker_diff`` (the DB write + commit) -> the engine's
+  ``on_report`` (the diff into an HBM slot, folded);
+* the close requested the reference's way: the report that reaches ``max_diffs`` calls
+  ``run_task_once("complete_cycle", ...)`` (cycle_manager.py:176-178), run on an executor thread
+  (tasks/cycle.py:9-25).
 
-Prints one JSON line: per-report handler latency (decode, ingest, total: p50 / p99 / max), the host
-bytes copied into the library's staging ring per report, and the close latency per cycle.
-``--pinned``: the report is decoded into a page-locked block (``report.PinnedPool``) and DMA'd as
-it lies.  ``--tune``: ``pygrid_amd.tune_process()`` first (glibc thresholds;
-the engine's own share of the close is the untuned run).  ``--no-speculate``: fold only certain
-positions early.  ``--close-gap-ms``: pause between the last report and the close (0: at once, as
-when the report that reaches ``max_diffs`` triggers ``complete_cycle``; 50 by default, a
-``cycle.end`` close).
+ResNet-18, 100 workers assigned per cycle, 80 report (worker 0 and 19 others never do,
+routes.py:314; ``max_diffs`` = 80), shuffled arrival.  Four arms: reports ``paced`` ``--gap-ms``
+apart (default 5) or back to back, x speculative / certain-only early folds.
+
+    python tools/node_sim.py [cycles] [--gap-ms=5] [--no-pinned] [--db=PATH] [--arms=paced_spec,...] [--cpu]
+
+Prints one JSON line: per arm the report handler latency (p50 / p99 / max) and its phases (the
+handler's base64 decode including ``.encode()``, the DB write + commit, the engine's ingest), and
+``close_ms``: from the last report's handler returning to the new checkpoint committed in the DB
+and the next cycle open (the executor's ``complete_cycle``), with the engine's share
+(``IncrementalCycle.finish``).  Dev tool: imports tests/ infrastructure; never a product path.
 """
 import base64
+import functools
 import json
 import sys
+import threading
 import time
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
 import numpy as np  # noqa: E402
 
-from pygrid_amd import Engine  # noqa: E402
-from pygrid_amd.incremental import IncrementalCycle  # noqa: E402
-from pygrid_amd.report import b64decode  # noqa: E402
+import ref_fl_events  # noqa: E402
+from fake_node import assign, host_process  # noqa: E402
+from pygrid_amd import Engine, incremental  # noqa: E402
+from pygrid_amd import node as pnode  # noqa: E402
 from pygrid_amd.state_schema import build_state_fast  # noqa: E402
 from pygrid_amd.workloads import RESNET18_SHAPES  # noqa: E402
+from sql_node import make_sql_node  # noqa: E402
+
+ASSIGNED, REPORTERS = 100, 80
 
 
 def pct(xs, q):
-    return round(float(np.percentile(xs, q)), 3)
+    return round(float(np.percentile(xs, q)), 3) if xs else None
+
+
+class Executor:
+    """``run_task_once`` (tasks/cycle.py:9-25): one named future on a worker thread."""
+
+    def __init__(self):
+        self.pool = ThreadPoolExecutor(1, thread_name_prefix="executor")
+        self.futures = {}
+
+    def run_task_once(self, name, func, *args):
+        f = self.futures.get(name)
+        if f is None or f.done():
+            self.futures[name] = self.pool.submit(func, *args)
+
+
+class Timer:
+    """Wraps callables to add their wall time (ms) to a per-thread bucket."""
+
+    def __init__(self):
+        self.local = threading.local()
+
+    def bucket(self):
+        b = getattr(self.local, "b", None)
+        if b is None:
+            b = self.local.b = {}
+        return b
+
+    def wrap(self, owner, name, key):
+        f = getattr(owner, name)
+
+        @functools.wraps(f)
+        def g(*a, **k):
+            t0 = time.perf_counter()
+            try:
+                return f(*a, **k)
+            finally:
+                b = self.bucket()
+                b[key] = b.get(key, 0.0) + (time.perf_counter() - t0) * 1e3
+        setattr(owner, name, g)
+        return f
+
+
+def run_arm(eng, cycles, gap_ms, speculate, pinned, db, rng, ckpt, texts, framing="fresh"):
+    mod, store = make_sql_node(db)
+    ex = Executor()
+    mod.run_task_once = ex.run_task_once
+    node = pnode.install(mod, engine=eng, report_module=ref_fl_events, pinned_reports=16 if pinned else 0,
+                         speculate=speculate, framing=framing)
+    ref_fl_events.processes = type("P", (), {"submit_diff": staticmethod(
+        lambda *a: mod.cycle_manager.submit_worker_diff(*a))})
+    timer = Timer()
+    timer.wrap(ref_fl_events.base64, "b64decode", "decode")
+    timer.wrap(node, "on_report", "ingest")
+    finish = incremental.IncrementalCycle.finish
+    engine_close = []
+
+    def timed_finish(self, *a, **k):
+        t0 = time.perf_counter()
+        try:
+            return finish(self, *a, **k)
+        finally:
+            engine_close.append((time.perf_counter() - t0) * 1e3)
+    incremental.IncrementalCycle.finish = timed_finish
+    try:
+        cfg = {"min_diffs": REPORTERS, "max_diffs": REPORTERS, "num_cycles": 0}
+        proc, _, _ = host_process(mod, cfg, ckpt)
+        handler, encode, decode, write, ingest, closes, engine_share = [], [], [], [], [], [], []
+        for cyc in range(cycles + 1):  # cycle 0 warms up
+            keys = {w: assign(mod, f"w{w}", proc) for w in range(ASSIGNED)}
+            reporters = [w for w in rng.permutation(ASSIGNED) if w != 0][:REPORTERS]
+            engine_close.clear()
+            for i, w in enumerate(reporters):
+                if i and gap_ms:
+                    time.sleep(gap_ms / 1e3)
+                text = texts[w % len(texts)]
+                msg = {"data": {"worker_id": f"w{w}", "request_key": keys[w], "diff": text}}
+                e0 = time.perf_counter()
+                text.encode()  # the handler's .encode() copy, timed apart (it runs before b64decode)
+                enc = (time.perf_counter() - e0) * 1e3
+                timer.bucket().clear()
+                t0 = time.perf_counter()
+                resp = ref_fl_events.report(msg)
+                t1 = time.perf_counter()
+                if resp["data"] != {"status": "success"}:
+                    raise SystemExit(f"report failed: {resp}")
+                if cyc:
+                    b = timer.bucket()
+                    total = (t1 - t0) * 1e3
+                    handler.append(total)
+                    encode.append(enc)
+                    decode.append(b.get("decode", 0.0))
+                    ingest.append(b.get("ingest", 0.0))
+                    write.append(total - enc - b.get("decode", 0.0) - b.get("ingest", 0.0))
+            fut = ex.futures["complete_cycle"]
+            fut.result(120)
+            if mod.cycle_manager.task_errors:
+                raise SystemExit(f"close failed: {mod.cycle_manager.task_errors!r}")
+            t2 = time.perf_counter()
+            if cyc:
+                closes.append((t2 - t1) * 1e3)
+                engine_share.append(engine_close[-1] if engine_close else None)
+            # untimed: the closed cycle's blobs are not needed again (bounds the DB's size)
+            cid = store.session.query(store.Cycle.id).filter_by(is_completed=True).order_by(store.Cycle.id.desc()).first()[0]
+            store.session.query(store.WorkerCycle).filter_by(cycle_id=cid).update({"diff": None})
+            store.session.commit()
+        stats = dict(node.stats)
+        pools = {"hits": node.pinned.hits, "misses": node.pinned.misses} if node.pinned else None
+    finally:
+        incremental.IncrementalCycle.finish = finish
+        node.uninstall()
+        ex.pool.shutdown()
+        store.close()
+    return {"report_handler_ms": {"p50": pct(handler, 50), "p99": pct(handler, 99), "max": round(max(handler), 3)},
+            "handler_phases_p50_ms": {"str_encode": pct(encode, 50), "b64decode": pct(decode, 50),
+                                      "submit_worker_diff_db_write_commit": pct(write, 50),
+                                      "engine_on_report_ingest": pct(ingest, 50)},
+            "close_ms": pct(closes, 50), "closes_ms": [round(c, 3) for c in closes],
+            "engine_close_ms": pct([e for e in engine_share if e is not None], 50),
+            "node_stats": stats, "pinned_pool": pools}
+
+
+class _nullctx:
+    def __init__(self, x):
+        self.x = x
+
+    def __enter__(self):
+        return self.x
+
+    def __exit__(self, *a):
+        return False
 
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    cycles = int(args[0]) if args else 4
-    speculate = False if "--no-speculate" in sys.argv else None
-    gap_ms = next((float(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--close-gap-ms=")), 50.0)
-    tuned = None
-    if "--tune" in sys.argv:
-        import pygrid_amd
-
-        tuned = pygrid_amd.tune_process(hw_queues=False)
-    pool = None
-    if "--pinned" in sys.argv:
-        from pygrid_amd.report import PinnedPool
-
-        pool = PinnedPool(max_blocks=8)
+    opt = dict(a[2:].split("=", 1) for a in sys.argv[1:] if a.startswith("--") and "=" in a)
+    cycles = int(args[0]) if args else 3
+    gap = float(opt.get("gap-ms", 5.0))
+    pinned = "--no-pinned" not in sys.argv
+    db = f"sqlite:///{opt['db']}" if "db" in opt else "sqlite://"
+    want = opt.get("arms", "paced_spec,paced_certain,b2b_spec,b2b_certain").split(",")
     rng = np.random.default_rng(2024)
-    numel = [int(np.prod(s)) for s in RESNET18_SHAPES]
     ckpt = build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in RESNET18_SHAPES])
-    # the report payload as the JSON carries it: base64 text of the State diff (4 distinct diffs, re-sent)
     texts = [base64.b64encode(build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2)
                                                 for s in RESNET18_SHAPES])).decode("ascii") for _ in range(4)]
-    eng = Engine(0)
-    phases = {}
-    if "--phases" in sys.argv:  # time the engine calls inside close (as tools/time_report_close.py)
-        import functools
-
-        from pygrid_amd import state as st
-
-        def wrap(obj, name):
-            f = getattr(obj, name)
-
-            @functools.wraps(f)
-            def g(*a, **k):
-                t0 = time.perf_counter()
-                r = f(*a, **k)
-                phases[name] = round(phases.get(name, 0) + (time.perf_counter() - t0) * 1e3, 3)
-                return r
-            setattr(obj, name, g)
-        for nm in ("fold_slots_finish_resident", "ckpt_patch_into", "fold_slots"):
-            wrap(eng, nm)
-        wrap(st, "fresh_frame_bytes")
-    dec, ing, tot, closes, close_phases, staged = [], [], [], [], [], []
-    for cyc in range(cycles + 1):  # cycle 0 warms up
-        n = 100
-        reporters = [w for w in range(n) if rng.random() >= 0.2]
-        inc = IncrementalCycle(eng, numel, slots=n, fold_batch=8, checkpoint=ckpt, speculate=speculate)
-        for w in range(n):
-            inc.assigned(w)
-        for w in rng.permutation(reporters):
-            s0 = eng.stats()["h2d_staged_bytes_total"]
-            t0 = time.perf_counter()
-            diff = b64decode(texts[int(w) % 4], into=pool)  # fl_events.py:257
-            t1 = time.perf_counter()
-            inc.reported(int(w), diff)           # submit_worker_diff, cycle_manager.py:151-178
-            t2 = time.perf_counter()
-            del diff                             # the handler returns (its pinned block goes back)
-            if cyc:
-                dec.append((t1 - t0) * 1e3)
-                ing.append((t2 - t1) * 1e3)
-                tot.append((t2 - t0) * 1e3)
-                staged.append(eng.stats()["h2d_staged_bytes_total"] - s0)
-        if gap_ms:
-            time.sleep(gap_ms / 1e3)  # the cycle ends some time after the last report (cycle.end timer)
-        phases.clear()
-        t0 = time.perf_counter()
-        new = inc.close(ckpt)
-        t1 = time.perf_counter()
-        ckpt = new  # the previous checkpoint's bytes are freed here (the node drops them after the save)
-        t2 = time.perf_counter()
-        if cyc:
-            closes.append((t2 - t0) * 1e3)
-            close_phases.append(dict(phases, close_call=round((t1 - t0) * 1e3, 3), free_old=round((t2 - t1) * 1e3, 3),
-                                     folded_before_close=inc.folded_early))
-    eng.close()
-    if pool is not None:
-        pool.close()
+    arms = {}
+    if "--cpu" in sys.argv:  # dev check of this tool on a GPU-less box: the tests' numpy engine
+        from fake_engine import NumpyEngine
+    with (Engine(0) if "--cpu" not in sys.argv else _nullctx(NumpyEngine())) as eng:
+        for name in want:
+            pace, kind = name.split("_")
+            arms[name] = run_arm(eng, cycles, gap if pace == "paced" else 0.0, None if kind == "spec" else False,
+                                 pinned, db, rng, ckpt, texts, framing="template" if "--cpu" in sys.argv else "fresh")
+            print(f"# {name}: close {arms[name]['close_ms']} ms, handler p50 {arms[name]['report_handler_ms']['p50']} ms",
+                  file=sys.stderr, flush=True)
     print(json.dumps({
-        "pinned_reports": pool is not None, "process_tuning": tuned, "speculative_folds": inc.speculate,
-        "close_gap_ms": gap_ms,
-        "pinned_pool": {"hits": pool.hits, "misses": pool.misses} if pool is not None else None,
-        "host_staging_bytes_per_report": {"mean": round(float(np.mean(staged)), 1), "max": int(max(staged))},
-        "workload": "ResNet-18 (62 tensors), 100 assigned per cycle, ~20 % never report, shuffled arrival, "
-                    "base64 text -> report.b64decode -> IncrementalCycle.reported; close close_gap_ms after the last report",
-        "cycles": cycles, "reports": len(tot),
-        "report_b64decode_ms": {"p50": pct(dec, 50), "p99": pct(dec, 99), "max": round(max(dec), 3)},
-        "report_ingest_ms": {"p50": pct(ing, 50), "p99": pct(ing, 99), "max": round(max(ing), 3)},
-        "report_handler_ms": {"p50": pct(tot, 50), "p99": pct(tot, 99), "max": round(max(tot), 3)},
-        "close_ms": [round(c, 3) for c in closes], "close_phases_ms": close_phases}))
+        "workload": f"ResNet-18 (62 tensors), {ASSIGNED} assigned per cycle, {REPORTERS} report (max_diffs) in "
+                    "shuffled order; JSON base64 text -> restated fl_events.report (.encode() + b64decode) -> "
+                    "submit_worker_diff (SQLAlchemy LargeBinary write + commit) -> engine ingest; close by "
+                    "run_task_once on an executor thread",
+        "db": db, "pinned_reports": pinned, "cycles": cycles, "gap_ms": gap,
+        "close_definition": "last report handler returned -> new checkpoint committed + next cycle open "
+                            "(complete_cycle on the executor thread)",
+        "arms": arms}))
 
 
 if __name__ == "__main__":
