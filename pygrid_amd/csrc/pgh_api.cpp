@@ -62,10 +62,9 @@ constexpr int KIND_SECAGG = 3;  // stream kind besides the three fedavg modes
 // drain the pinned staging slots, where payload pieces are many and mostly small.
 // memcpy with non-temporal 16-byte stores for big copies into staging / output buffers (no
 // read-for-ownership of the destination, which is written once and then read by the DMA engine or
-// handed to the caller).  g_nt_copy = PGH_NT_COPY (default on).
-bool g_nt_copy = true;
+// handed to the caller; r01ab).
 void copy_stream(uint8_t* dst, const uint8_t* src, size_t n) {
-    if (!g_nt_copy || n < (256u << 10)) { std::memcpy(dst, src, n); return; }
+    if (n < (256u << 10)) { std::memcpy(dst, src, n); return; }
     const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
     std::memcpy(dst, src, head);
     dst += head; src += head; n -= head;
@@ -297,13 +296,6 @@ struct pgh_ctx {
     int64_t bmask = 0;
     size_t block_bytes = 256u << 10;  // PGH_BLOCK_BYTES; 0 = one block (plain row-major rows)
     int synth_kind = 0;        // pgh_set_synth_kind: generator of synthetic diffs (0 Irwin-Hall, 1 fast)
-    int64_t synth_wgs = 8192;  // PGH_SYNTH_WGS: STREAM synthetic fill grid cap (0 = a grid row per row; r01t)
-    // STREAM synthetic fills run on the fold stream, generator and fold alternating with the whole
-    // GPU each (PGH_SYNTH_SERIAL=0: beside the fold on the copy stream; the write-heavy fill and the
-    // read-only fold then share HBM 13 % worse, r02p), with non-temporal stores (PGH_SYNTH_NT)
-    bool synth_serial = true;
-    int final_streams = 2;         // PGH_FINAL_STREAMS: 1 = the split FINAL pass on one stream
-    bool synth_nt = true;
 
     int slots = 0, dtype = PGH_F32, parties = 1;
     void* d_slab = nullptr;
@@ -333,7 +325,6 @@ struct pgh_ctx {
     int copy_threads = 8;
     std::vector<int> local_cpus;  // PGH_NUMA (default on): the GPU's socket, for the copy pool + pinned ring
     std::unique_ptr<CopyPool> pool_copy;
-    bool register_ingest = false;  // PGH_REGISTER_INGEST=1: page-lock State messages instead of staging
 
     // secagg shares as State bytes: varint payloads in HBM + their chunk table (k_varint_decode)
     uint8_t* d_vbytes = nullptr;
@@ -352,16 +343,6 @@ struct pgh_ctx {
     hipEvent_t gdma_ev = nullptr;    // the last message DMA (the caller's buffer is free after it)
     bool gtab_used = false;
     bool pinned_gather = true;
-    // PGH_SHARE_FILL_MB: cap on one pinned fill of share payloads (default: the whole slot; r01z:
-    // 8 / 16 / 32 / 128 MiB fills gave 29.6 / 30.8 / 34.7 / 41.6 wire GB/s at ResNet-18 x 16 x 2)
-    size_t share_fill = ~(size_t)0;
-    bool nt_copy = true;  // PGH_NT_COPY: non-temporal staging copies (host side)
-    // PGH_D2H_PIECE_MB: HBM -> host results move in pieces of at most this size, the DMA of piece
-    // i + 1 beside the host copy-out of piece i (0: one pinned slot per piece).  r01ac: 4, 8, 16 MiB
-    // within the noise of the 47 MB report-time close while the copy-out took page faults; with
-    // the parallel pre-fault (r01ak) 8 MiB pieces close in 2.3-2.4 ms vs 2.6-2.7 for one piece.
-    size_t d2h_piece = 8u << 20;
-    bool prefault = true;  // PGH_PREFAULT: pre-fault big fresh checkpoint outputs in parallel (patch)
     bool warmup_skipped = false;  // pgh_create's warm-up failed (e.g. no device memory left): skipped
     int64_t vec_min = 0;      // [P_shard] device vectors at least this long (group collectives)
     // Pipelined close: a resident fold's FINAL pass runs as final_split param ranges, each followed by
@@ -380,9 +361,6 @@ struct pgh_ctx {
     // of the rows left at close: short, so its D2H would otherwise wait for all of it) -- on by
     // default: 1.98 -> 1.41 ms close after a back-to-back burst at 8 ranges (profiles/r03ah/)
     int slot_final_split = 8;
-    // PGH_D2H_NOCU (A/B): D2H into the library's page-locked buffers as hipMemcpyDeviceToDeviceNoCU
-    // (a copy engine instead of a blit kernel sharing the CUs with a fold still running)
-    bool d2h_nocu = false;
     int64_t client_base = 0;  // synthetic client k is generated as global client client_base + k
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
@@ -759,17 +737,7 @@ void prefault_parallel(uint8_t* p, size_t n, CopyPool& pool) {
     static const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
     const uintptr_t a = (uintptr_t)p & ~(page - 1), b = ((uintptr_t)p + n + page - 1) & ~(page - 1);
     if (all_resident(a, b, page)) return;
-    // PGH_THP=1: the 2 MiB-aligned interior on transparent huge pages.  Off by default: this
-    // populate already runs beside the fold and the first D2H, and the report-time close measured
-    // the same either way (2.0-2.3 vs 2.1-2.3 ms medians, profiles/r02ad/).
-    static const bool thp = [] {
-        const char* e = std::getenv("PGH_THP");
-        return e && std::atoi(e) != 0;
-    }();
-    if (thp) {
-        const uintptr_t h = (uintptr_t)2 << 20, ha = (a + h - 1) & ~(h - 1), hb = b & ~(h - 1);
-        if (hb > ha) (void)madvise((void*)ha, hb - ha, MADV_HUGEPAGE);
-    }
+    // (transparent huge pages for this range measured neutral, profiles/r02ad/: 4 KiB pages)
     const int k = pool.threads();
     const uintptr_t per = ((b - a) / k + page - 1) & ~(page - 1);
     pool.run_items(k, true, [&](int i) {
@@ -793,34 +761,36 @@ int add_final_mark(pgh_ctx* c, hipStream_t s, int64_t end) {
     return PGH_OK;
 }
 
-// The ranges of a split FINAL pass alternate over `s` and the aux stream (final_streams == 2), so
-// range k + 1 starts while range k drains its last workgroups instead of after (one stream costs
-// the drain once per range: r02n group line, 4 launches 7.38 ms vs one 6.80 ms).  fork: aux after
-// everything issued on s; join: s after everything issued on aux.
+// The ranges of a split FINAL pass alternate over `s` and the aux stream, so range k + 1 starts
+// while range k drains its last workgroups instead of after (one stream costs the drain once per
+// range: r02n group line, 4 launches 7.38 ms vs one 6.80 ms).  fork: aux after everything issued
+// on s; join: s after everything issued on aux.
 hipStream_t range_stream(const pgh_ctx* c, hipStream_t s, int k) {
-    return (c->final_streams > 1 && (k & 1)) ? c->aux : s;
+    return (k & 1) ? c->aux : s;
 }
 int fork_aux(pgh_ctx* c, hipStream_t s) {
-    if (c->final_streams < 2) return PGH_OK;
     CK(c, hipEventRecord(c->aux_ev, s));
     CK(c, hipStreamWaitEvent(c->aux, c->aux_ev, 0));
     return PGH_OK;
 }
 int join_aux(pgh_ctx* c, hipStream_t s) {
-    if (c->final_streams < 2) return PGH_OK;
     CK(c, hipEventRecord(c->aux_ev, c->aux));
     CK(c, hipStreamWaitEvent(s, c->aux_ev, 0));
     return PGH_OK;
 }
 
 // Ranges of a FINAL fold pass: 1, or final_split 4-aligned ranges of the shard.
-hipMemcpyKind d2h_kind(const pgh_ctx* c) { return c->d2h_nocu ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost; }
 int final_ranges(const pgh_ctx* c) { return c->final_split > 1 && c->pg >= (1 << 20) ? c->final_split : 1; }
 int slot_final_ranges(const pgh_ctx* c) {
     const int k = c->final_split > 1 ? c->final_split : c->slot_final_split;  // PGH_FINAL_RANGES wins
     return k > 1 && c->pg >= (1 << 20) ? k : 1;
 }
 int64_t range_edge(const pgh_ctx* c, int k, int K) { return k >= K ? c->pg : (c->pg * k / K) & ~(int64_t)3; }
+
+// HBM -> host results move in pieces of at most D2H_PIECE, the DMA of piece i + 1 beside the host
+// copy-out of piece i (r01ac: 4, 8, 16 MiB within the noise of the 47 MB report-time close; with the
+// parallel pre-fault, r01ak, 8 MiB pieces closed in 2.3-2.4 ms vs 2.6-2.7 for one piece).
+constexpr size_t D2H_PIECE = 8u << 20;
 
 // HBM bytes at `src` (after the work already on stream `s`) -> host pieces, through the pinned
 // ring: the DMA of one slot overlaps the host copy-out of the previous one.  `overlap`, if given,
@@ -843,7 +813,7 @@ int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>
             cur_slot = c->pin_next;
             c->pin_next ^= 1;
             if (c->pin_used[cur_slot]) CK(c, hipEventSynchronize(c->pin_ev[cur_slot]));
-            cur_len = std::min({total - off, c->pin_slot, c->d2h_piece});
+            cur_len = std::min({total - off, c->pin_slot, D2H_PIECE});
             if (piped) {  // wait for EVERY fold range the piece's floats come from: the ranges
                           // alternate over two streams, so the last one's mark orders nothing else
                 const int64_t first = (int64_t)(off / 4), last = (int64_t)((off + cur_len + 3) / 4);
@@ -854,7 +824,7 @@ int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>
                     start = m.end;
                 }
             }
-            CK(c, hipMemcpyAsync(c->h_pin[cur_slot], src + off, cur_len, d2h_kind(c), s));
+            CK(c, hipMemcpyAsync(c->h_pin[cur_slot], src + off, cur_len, hipMemcpyDeviceToHost, s));
             CK(c, hipEventRecord(c->pin_ev[cur_slot], s));
             c->pin_used[cur_slot] = true;
         }
@@ -1411,24 +1381,10 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
         if (!nu || std::atoi(nu) != 0) c->local_cpus = gpu_local_cpus(device);
     }
     c->pool_copy.reset(new CopyPool(c->copy_threads, c->local_cpus));
-    if (const char* e = std::getenv("PGH_REGISTER_INGEST")) c->register_ingest = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_PINNED_GATHER")) c->pinned_gather = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PGH_SYNTH_WGS")) c->synth_wgs = std::max(0LL, std::atoll(e));
-    if (const char* e = std::getenv("PGH_SYNTH_SERIAL")) c->synth_serial = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PGH_SYNTH_NT")) c->synth_nt = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_BLOCK_BYTES")) c->block_bytes = (size_t)std::max(0LL, std::atoll(e));
-    if (const char* e = std::getenv("PGH_SHARE_FILL_MB")) c->share_fill = (size_t)std::max(1LL, std::atoll(e)) << 20;
-    if (const char* e = std::getenv("PGH_NT_COPY")) c->nt_copy = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PGH_PREFAULT")) c->prefault = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_FINAL_RANGES")) c->final_split = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("PGH_SLOT_FINAL_RANGES")) c->slot_final_split = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("PGH_D2H_NOCU")) c->d2h_nocu = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PGH_FINAL_STREAMS")) c->final_streams = std::atoi(e) > 1 ? 2 : 1;
-    if (const char* e = std::getenv("PGH_D2H_PIECE_MB")) {
-        const long long mb = std::atoll(e);
-        c->d2h_piece = mb > 0 ? (size_t)mb << 20 : ~(size_t)0;
-    }
-    g_nt_copy = c->nt_copy;
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming) == hipSuccess &&
@@ -1700,26 +1656,6 @@ int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
         c->st.h2d_bytes_total += off;
         return mark_ingested(c, client, slot);
     }
-    if (c->register_ingest && n >= (8u << 20) &&
-        hipHostRegister((void*)pb, n, hipHostRegisterDefault) == hipSuccess) {
-        // page-lock the message for the duration of the call and DMA the spans directly
-        const double t0 = now_ms();
-        const Dest d = row_dest(c, slot, 0);
-        size_t off = 0;
-        int rc = PGH_OK;
-        for (auto& p : pieces) {
-            if (rc == PGH_OK) rc = h2d_range(c, d, (int64_t)(off / 4), p.src, (int64_t)(p.n / 4), c->copy);
-            off += p.n;
-        }
-        hipError_t e = rc == PGH_OK ? hipStreamSynchronize(c->copy) : hipSuccess;
-        (void)hipHostUnregister((void*)pb);
-        if (rc) return rc;
-        if (e != hipSuccess) return fail(c, PGH_E_HIP, "registered ingest failed: %s", hipGetErrorString(e));
-        c->st.h2d_ms_total += now_ms() - t0;
-        c->st.h2d_bytes_total += off;
-        return mark_ingested(c, client, slot);
-    }
-    (void)hipGetLastError();
     RC(stage_pieces_h2d(c, row_dest(c, slot, 0), pieces));
     return mark_ingested(c, client, slot);
 }
@@ -1827,7 +1763,7 @@ int stage_share_msg(pgh_ctx* c, ShareMsg& m) {
         c->pin_next ^= 1;
         if (c->pin_used[ps]) CK(c, hipEventSynchronize(c->pin_ev[ps]));
         const size_t s0 = (size_t)m.chunks[k].off;
-        const size_t cap = std::min(c->pin_slot, c->share_fill);  // smaller fills: DMA i beside fill i + 1
+        const size_t cap = c->pin_slot;  // whole-slot fills (r01z: smaller fills were slower)
         size_t k1 = k;
         while (k1 < nk && (size_t)m.chunks[k1].off + (size_t)m.chunks[k1].n - s0 <= cap) ++k1;
         if (k1 == k) return fail(c, PGH_E_STATE, "pinned slot smaller than one varint chunk");
@@ -1836,9 +1772,7 @@ int stage_share_msg(pgh_ctx* c, ShareMsg& m) {
         c->pool_copy->run_items((int)(k1 - k), fill >= (4u << 20), [&](int i) {
             const size_t q = k + (size_t)i;
             uint8_t* dst = pin + ((size_t)m.chunks[q].off - s0);
-            m.st[q] = c->nt_copy ? pgh_state::varint_copy_stats(dst, m.src[q], (size_t)m.chunks[q].n)
-                                 : (std::memcpy(dst, m.src[q], (size_t)m.chunks[q].n),
-                                    pgh_state::varint_stats(dst, (size_t)m.chunks[q].n));
+            m.st[q] = pgh_state::varint_copy_stats(dst, m.src[q], (size_t)m.chunks[q].n);
         });
         CK(c, hipMemcpyAsync(c->d_vbytes + s0, pin, fill, hipMemcpyHostToDevice, c->copy));
         CK(c, hipEventRecord(c->pin_ev[ps], c->copy));
@@ -2000,11 +1934,14 @@ int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
         }
         if (c->streaming && run > 1) RC(order_stream_overwrite(c, client + run - 1));
         hipError_t e;
-        const hipStream_t gs = c->streaming && c->synth_serial ? c->stream : c->copy;
+        // STREAM fills run on the fold stream, generator and fold alternating with the whole GPU each
+        // (beside the fold on the copy stream, the write-heavy fill and the read-only fold shared
+        // HBM 13 % worse, r02p), grid capped at 8192 workgroups (r01t), non-temporal stores
+        const hipStream_t gs = c->streaming ? c->stream : c->copy;
         if (c->dtype == PGH_F32)
             e = pgh::launch_synth_f32((float*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->pg, seed,
                                       pgh::STREAM_DIFF, c->client_base + client, c->lo, pgh::DIFF_SCALE, gs,
-                                      c->streaming ? c->synth_wgs : 0, c->synth_kind, c->synth_nt);
+                                      c->streaming ? 8192 : 0, c->synth_kind, true);
         else
             e = pgh::launch_synth_shares((int64_t*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->parties,
                                          c->pg, seed, c->client_base + client, c->lo, 1000.0f, gs);
@@ -2254,8 +2191,7 @@ int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out
     // the framing copy and the pre-fault of the output run while the first slot's DMA flies (in
     // place, out == tmpl, is how a freshly framed checkpoint is filled: its pages are fresh too)
     RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, pieces, c->stream, [&] {
-        if (c->prefault) prefault_parallel(out, n, *c->pool_copy);
-        else prefault_small(out, n);
+        prefault_parallel(out, n, *c->pool_copy);
         if (!gaps.empty()) c->pool_copy->run(gaps);
     }, true));
     return collect_timings(c);
@@ -2648,7 +2584,7 @@ int pgh_fold_peek(pgh_ctx* c, int mode) {
     RC(record_fold(c, s));  // a checkpoint upload waits for this read of d_ckpt
     CK(c, hipEventRecord(c->peek_ev, s));
     CK(c, hipStreamWaitEvent(c->peek_stream, c->peek_ev, 0));
-    CK(c, hipMemcpyAsync(c->h_peek, c->d_peek, (size_t)c->pg * 4, d2h_kind(c), c->peek_stream));
+    CK(c, hipMemcpyAsync(c->h_peek, c->d_peek, (size_t)c->pg * 4, hipMemcpyDeviceToHost, c->peek_stream));
     CK(c, hipEventRecord(c->peek_ev, c->peek_stream));
     c->peek_gen = c->state_gen;
     return PGH_OK;
@@ -3039,7 +2975,7 @@ int patch_payloads(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out) {
     for (auto& sp : spans) pieces.push_back(OutPiece{out + sp.first, sp.second});
     RC(order_after_ingest(c, c->stream));
     RC(stage_d2h_pieces(c, (const uint8_t*)c->d_ckpt, pieces, c->stream, [&] {
-        if (c->prefault && !spans.empty()) {  // this shard's part of the (fresh) output
+        if (!spans.empty()) {  // this shard's part of the (fresh) output
             const size_t a = spans.front().first, b = spans.back().first + spans.back().second;
             if (b > a) prefault_parallel(out + a, b - a, *c->pool_copy);
         }

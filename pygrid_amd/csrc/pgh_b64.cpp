@@ -267,11 +267,7 @@ void populate(uint8_t* p, size_t n) {
 #ifndef MADV_POPULATE_WRITE
 #define MADV_POPULATE_WRITE 23
 #endif
-    static const bool on = [] {
-        const char* e = std::getenv("PGH_B64_POPULATE");  // A/B knob: 0 = let the decode fault pages in
-        return !e || std::atoi(e) != 0;
-    }();
-    if (!on || !p || n < (1u << 20)) return;
+    if (!p || n < (1u << 20)) return;
     static const uintptr_t page = (uintptr_t)sysconf(_SC_PAGESIZE);
     const uintptr_t a = ((uintptr_t)p + page - 1) & ~(page - 1), b = ((uintptr_t)p + n) & ~(page - 1);
     if (b > a) (void)madvise((void*)a, b - a, MADV_POPULATE_WRITE);
@@ -280,13 +276,9 @@ void populate(uint8_t* p, size_t n) {
 // The 2 MiB-aligned interior of a big fresh output on transparent huge pages (one fault per 2 MiB
 // instead of 512): a 47 MB diff decodes in 7-9 ms instead of 11-12 (profiles/r02ad/).  One call
 // over the whole output on the caller's thread, before the threads populate their parts (the
-// hint changes the mapping's flags: one writer, not one per thread).  PGH_B64_THP=0 turns it off.
+// hint changes the mapping's flags: one writer, not one per thread).
 void hugepage_hint(uint8_t* p, size_t n) {
-    static const bool thp = [] {
-        const char* e = std::getenv("PGH_B64_THP");
-        return !e || std::atoi(e) != 0;
-    }();
-    if (!thp || !p || n < (4u << 20)) return;
+    if (!p || n < (4u << 20)) return;
     const uintptr_t h = (uintptr_t)2 << 20, ha = ((uintptr_t)p + h - 1) & ~(h - 1), hb = ((uintptr_t)p + n) & ~(h - 1);
     if (hb > ha) (void)madvise((void*)ha, hb - ha, MADV_HUGEPAGE);
 }
@@ -454,7 +446,7 @@ int pgh_b64_decode(const char* in, size_t n, uint8_t* out, size_t* written, int 
     if ((!in && n) || !written) return PGH_E_ARG;
     const unsigned char* s = (const unsigned char*)in;
     const int t = threads_for(n, threads);
-    if (std::getenv("PGH_B64_GENERAL") == nullptr) {
+    {
         const int rc = decode_fast(s, n, first_eq(s, n), out, pgh_b64_decoded_cap(n), written, t);
         if (rc != PGH_E_STATE) return rc;  // clean text: decoded, or a padding error
     }

@@ -1,0 +1,81 @@
+"""GPU: every environment knob the library still reads, at a
+non-default value, closes bit-exact against the oracle.  PGH_BLOCK_BYTES,
+PGH_FINAL_RANGES and PGH_PINNED_GATHER have their own tests (test_gpu_parity.py,
+test_gpu_pipelined_close.py, test_gpu_pinned_report.py).  The library reads the environment when
+a context is created, so each case creates its own."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+SHAPES = [(1100, 1000), (1000,), (10, 1000), (10,)]  # > 1 M params: the split FINAL pass applies
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _case(seed, n=5):
+    from pygrid_amd.state_schema import build_state_fast
+
+    rng = np.random.default_rng(seed)
+    ckpt = [rng.standard_normal(s).astype(F) for s in SHAPES]
+    diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES] for _ in range(n)]
+    return ckpt, diffs, build_state_fast(ckpt), [build_state_fast(d) for d in diffs]
+
+
+def _check(new_pb, want):
+    from pygrid_amd.state_schema import parse_state
+
+    for g, w in zip(parse_state(new_pb), want):
+        assert np.array_equal(bits(g), bits(w))
+
+
+@pytest.mark.parametrize("env", [{"PGH_COPY_THREADS": "1"}, {"PGH_NUMA": "0"}, {"PGH_WARMUP": "0"}],
+                         ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+def test_close_time_knobs(monkeypatch, env):
+    from pygrid_amd import Engine
+    from pygrid_amd.cycle import CycleAggregator
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    ckpt, diffs, ck_pb, d_pbs = _case(900)
+    with Engine(0) as eng:
+        for _ in range(2):  # the first close after create (no warm-up) and a second one
+            _check(CycleAggregator(eng).average_plan_diffs({}, ck_pb, d_pbs), O.fedavg_mean(ckpt, diffs))
+
+
+@pytest.mark.parametrize("ranges", ["1", "3"])
+@pytest.mark.parametrize("speculate", [False, True])
+def test_slot_final_ranges(monkeypatch, ranges, speculate):
+    """PGH_SLOT_FINAL_RANGES (default 8): the report-time close's FINAL pass as one launch, or as
+    3 ranges (not a divisor of anything here), with the D2H behind them."""
+    from pygrid_amd import Engine
+    from pygrid_amd.incremental import IncrementalCycle
+
+    monkeypatch.setenv("PGH_SLOT_FINAL_RANGES", ranges)
+    ckpt, diffs, ck_pb, d_pbs = _case(910 + int(ranges), n=6)
+    with Engine(0) as eng:
+        inc = IncrementalCycle(eng, [int(np.prod(s)) for s in SHAPES], slots=8, checkpoint=ck_pb,
+                               speculate=speculate, lazy=False)
+        for w in range(7):
+            inc.assigned(w)
+        for w in (5, 1, 3, 0, 2, 4):  # worker 6 never reports
+            inc.reported(w, d_pbs[w])
+        _check(inc.close(ck_pb), O.fedavg_mean(ckpt, diffs))
+
+
+def test_group_copy_threads_and_rccl_off(monkeypatch):
+    """PGH_COPY_THREADS=2 split over a two-child group on GPU 0, PGH_RCCL=0 (peer copies)."""
+    from pygrid_amd import Engine
+    from pygrid_amd.cycle import CycleAggregator
+
+    monkeypatch.setenv("PGH_COPY_THREADS", "2")
+    monkeypatch.setenv("PGH_RCCL", "0")
+    ckpt, diffs, ck_pb, d_pbs = _case(920)
+    with Engine(devices=[0, 0]) as grp:
+        _check(CycleAggregator(grp).average_plan_diffs({}, ck_pb, d_pbs), O.fedavg_mean(ckpt, diffs))
+        grp.allgather_resident()
+        assert grp.group_backend() == 0  # peer copies, never RCCL

@@ -100,14 +100,12 @@ def test_report_time_close_ranges(piped, mode):
             assert np.array_equal(bits(g), bits(w_)), cyc
 
 
-@pytest.mark.parametrize("streams", ["1", "2"])
-def test_group_pipelined_close(monkeypatch, streams):
+def test_group_pipelined_close(monkeypatch):
     """Two children on GPU 0, each shard >= 1 M params: every child pipelines its own slice (ranges
-    on one stream or alternating over two)."""
+    alternating over two streams)."""
     from pygrid_amd import Engine
 
     monkeypatch.setenv("PGH_FINAL_RANGES", "4")
-    monkeypatch.setenv("PGH_FINAL_STREAMS", streams)
     from pygrid_amd.cycle import CycleAggregator
     from pygrid_amd.state_schema import build_state_fast, parse_state
 
@@ -130,9 +128,7 @@ def test_one_d2h_piece_spanning_every_range(monkeypatch, mode):
     from pygrid_amd import Engine
     from pygrid_amd.state_schema import build_state_fast, parse_state
 
-    monkeypatch.setenv("PGH_FINAL_RANGES", "4")
-    monkeypatch.setenv("PGH_FINAL_STREAMS", "2")
-    monkeypatch.setenv("PGH_D2H_PIECE_MB", "64")  # the whole 6.2 MB checkpoint is one piece
+    monkeypatch.setenv("PGH_FINAL_RANGES", "4")  # the whole 6.2 MB checkpoint is one 8 MiB D2H piece
     rng = np.random.default_rng(430 + mode)
     shapes = [(1024, 1500), (1500,), (7, 1024), (7,)]
     numel = [int(np.prod(s)) for s in shapes]

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Host base64 decode of a ResNet-18-sized diff (fl_events.py:257): Python vs native, by threads.
-(A/B knobs read by the library: PGH_B64_GENERAL=1 forces the general path, PGH_B64_POPULATE=0 skips the
+(r02 A/B knobs, since removed from the library: PGH_B64_GENERAL=1 forced the general path, PGH_B64_POPULATE=0 skipped the
 output pre-population.)"""
 import base64
 import sys

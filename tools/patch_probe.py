@@ -4,7 +4,7 @@ were left to fold).  ResNet-18 resident checkpoint, one FINAL fold, then the fre
 written from HBM, timed over --reps for: a fresh output (framed now), a prepared output (framed and
 faulted in beforehand), and the D2H alone into a page-locked buffer (``ckpt_download``).
 
-    python tools/patch_probe.py [--reps 10]      (PGH_PREFAULT / PGH_D2H_PIECE_MB apply)
+    python tools/patch_probe.py [--reps 10]      (r01 knobs PGH_PREFAULT / PGH_D2H_PIECE_MB: now fixed defaults)
 """
 import argparse
 import json

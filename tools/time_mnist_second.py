@@ -5,7 +5,7 @@ scan and the fresh-checkpoint steps timed inside the real call.
 
     python tools/time_mnist_second.py [closes]
 Environment knobs worth comparing: MALLOC_MMAP_THRESHOLD_ (fixes glibc's dynamic mmap threshold),
-PGH_PREFAULT=0."""
+(PGH_PREFAULT=0 was the r01 arm; the pre-fault is now always on)."""
 import functools
 import sys
 import time
