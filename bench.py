@@ -126,6 +126,13 @@ def parse():
                     help="leave glibc's allocator thresholds alone (pygrid_amd.tune_process(malloc=...))")
     ap.add_argument("--dry-run", action="store_true",
                     help="form the world (gloo, no GPU), print the world size on rank 0 and exit")
+    ap.add_argument("--check", action="store_true",
+                    help="c4-stream / c5-ingest: after the timed steps, every rank samples params of its shard, "
+                         "the oracle computes them from that rank's inputs, rank 0 compares the all-gathered "
+                         "new checkpoint bit for bit (a checker leg outside the timed region)")
+    ap.add_argument("--no-config-lines", action="store_true",
+                    help="default workload: skip the config-4 / config-5 lines (c4-stream, c5-ingest --check over "
+                         "the same --gpus, each in a fresh child world) attached under `config4` / `config5`")
     return ap.parse_args()
 
 
@@ -199,11 +206,23 @@ def spawn_ranks(args) -> int:
     rec = json.loads(lines[-1])
     if wants_group_line(args):
         rec["group"] = group_line(args)
+    attach_config_lines(args, rec)
     print(json.dumps(rec), flush=True)
     return 0
 
 
 GROUP_WORKLOADS = {"resnet18-fedavg", "resnet18-iterative", "resnet18-weighted", "resnet18-secagg", "secagg-clients"}
+
+
+LAUNCHER_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "GROUP_RANK",
+                "ROLE_RANK", "GROUP_WORLD_SIZE", "ROLE_WORLD_SIZE", "ROLE_NAME", "PGH_BENCH_SPAWNED")
+
+
+def child_env() -> dict:
+    """This environment without the launcher's rank variables (torch.distributed.run's, including
+    every TORCHELASTIC_* one: a child world that inherited TORCHELASTIC_USE_AGENT_STORE would wait
+    on the launcher's store), so a child forms its own world or none."""
+    return {k: v for k, v in os.environ.items() if k not in LAUNCHER_ENV and not k.startswith("TORCHELASTIC_")}
 
 
 def wants_group_line(args) -> bool:
@@ -227,9 +246,7 @@ def group_line(args, limit_s: int = 300) -> dict:
         cmd += ["--clients", str(args.clients)]
     if args.params:
         cmd += ["--params", str(args.params)]
-    env = {k: v for k, v in os.environ.items()
-           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
-                        "PGH_BENCH_SPAWNED", "TORCHELASTIC_RUN_ID", "GROUP_RANK", "ROLE_RANK")}
+    env = child_env()
     print(f"bench.py: one-process group over {args.gpus} GPUs in a fresh child ({limit_s} s limit)", file=sys.stderr,
           flush=True)
     try:  # stderr passes through: the child's progress stays visible
@@ -255,6 +272,86 @@ def group_line(args, limit_s: int = 300) -> dict:
         if k in g:
             out[k] = g[k]
     return out
+
+
+CONFIG_LINES = {"config4": "c4-stream", "config5": "c5-ingest"}
+
+
+def wants_config_lines(args) -> bool:
+    return args.workload == "resnet18-fedavg" and not args.group and not args.no_config_lines
+
+
+def config_line(args, workload: str, limit_s: int = 420) -> dict:
+    """BASELINE configs 4 and 5 over the same --gpus as this run, each a fresh child world
+    (``bench.py --gpus N --workload <w> --check``: it forms its own N ranks; no process that touched a
+    GPU re-execs), summarised for this line: what ran (ranks, backend), its throughput and the
+    sampled bit-exact check of the sharded result after the all-gather."""
+    import subprocess
+
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--gpus", str(args.gpus), "--workload", workload,
+           "--steps", str(min(args.steps, 5)), "--warmup", "1", "--seed", str(args.seed), "--no-cpu-baseline",
+           "--no-live-traffic", "--no-group-line", "--no-config-lines", "--check"]
+    if args.dry_run:
+        cmd.append("--dry-run")
+    env = child_env()
+    print(f"bench.py: {workload} over {args.gpus} GPU(s) in a fresh child world ({limit_s} s limit)", file=sys.stderr,
+          flush=True)
+    try:
+        r = subprocess.run(["timeout", "-k", "10", str(limit_s)] + cmd, cwd=str(ROOT), env=env,
+                           stdout=subprocess.PIPE, text=True)
+    except OSError as e:
+        return {"error": f"{workload} child did not start: {e}"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"{workload} child exited {r.returncode} (limit {limit_s} s; its stderr is above)",
+                "command": " ".join(cmd[1:])}
+    g = json.loads(lines[-1])
+    if g.get("dry_run"):
+        return g
+    keep = ("value", "unit", "n_gpus", "steps", "ms_per_step", "pct_hbm_peak_per_gpu", "dist_backend", "rccl_ranks",
+            "check", "fold_kernel_client_diff_GBps_aggregated", "fold_kernel_client_diff_GBps_per_gpu",
+            "ingest_GBps_per_gpu", "bound_by")
+    out = {k: g[k] for k in keep if k in g}
+    out["workload"] = (g.get("config") or {}).get("workload")
+    out["parallelism"] = (g.get("config") or {}).get("parallelism")
+    out["frac"] = (g.get("roofline") or {}).get("frac")
+    out["command"] = " ".join(cmd[1:])
+    return out
+
+
+def attach_config_lines(args, rec: dict):
+    if wants_config_lines(args):
+        for key, wl in CONFIG_LINES.items():
+            rec[key] = config_line(args, wl)
+
+
+def check_sampled(ctx, args, full, lo: int, hi: int, expected) -> dict:
+    """``--check``: a checker leg outside the timed region (like cpu_baseline, the only other place
+    this script runs the oracle).  Every rank samples global param indices of its own shard [lo, hi)
+    (both edges included) and computes the oracle's new-checkpoint values for them from its own
+    inputs (``expected(idx)``); rank 0 gathers them and compares ``full`` -- the all-gathered new
+    checkpoint, or the one shard at N = 1 -- at every rank's indices, bit for bit."""
+    import numpy as np
+
+    torch = ctx.torch
+    rng = np.random.default_rng(args.seed + 7919 * ctx.rank)
+    idx = np.unique(np.concatenate([[lo, hi - 1], rng.integers(lo, hi, 62)])).astype(np.int64)
+    want = np.ascontiguousarray(expected(idx), np.float32)
+    mine = (idx.tolist(), want.view(np.uint32).tolist())
+    if ctx.world > 1:
+        got = [None] * ctx.world
+        ctx.dist.all_gather_object(got, mine)
+    else:
+        got = [mine]
+    if ctx.rank != 0:
+        return None
+    all_idx = np.array([i for g in got for i in g[0]], np.int64)
+    all_want = np.array([w for g in got for w in g[1]], np.uint32)
+    have = full[torch.from_numpy(all_idx).to(full.device)].float().cpu().numpy().view(np.uint32)
+    bad = int((have != all_want).sum())
+    return {"bit_exact": bad == 0, "mismatches": bad, "params_checked": int(all_idx.size), "ranks": ctx.world,
+            "against": "oracle (coracle.fedavg over the sampled params of every client, from each rank's own inputs)",
+            "after": "all-gather of the sharded new checkpoint" if ctx.world > 1 else "one GPU (no exchange)"}
 
 
 def cpu_baseline(kind: str, P: int, seed: int, budget_s: float, n: int = 32, all_cores: int = 0):
@@ -776,14 +873,28 @@ def run_c4(ctx, args, eng, N, pg, P):
     eng.synth_ckpt_device(args.seed, ckpt.data_ptr(), sp)
     torch.cuda.synchronize()
 
+    full = [out]
+
     def step():
         eng.stream_begin(0, chunk)
         for c0 in range(0, N, chunk):
             eng.synth_ingest(args.seed, c0, min(chunk, N - c0))
         eng.stream_finish_device(ckpt.data_ptr(), out.data_ptr(), sp)
         if ctx.world > 1:
-            gather_flat(out, P, ctx.world, ctx.rank)
+            full[0] = gather_flat(out, P, ctx.world, ctx.rank)
     el, st = timed(ctx, step, args.steps, args.warmup, eng)
+    checked = None
+    if args.check:
+        def expected(idx):
+            import numpy as np
+
+            from oracle import coracle
+            from oracle import oracle as O
+
+            u = idx.astype(np.uint64)
+            gen = O.synth_diff_fast if args.synth == "fast" else O.synth_diff
+            return coracle.fedavg(0, np.stack([gen(args.seed, k, u) for k in range(N)]), O.synth_ckpt(args.seed, u))
+        checked = check_sampled(ctx, args, full[0], eng.lo, eng.hi, expected)
     diff_bytes = 4 * N * pg
     value = diff_bytes * ctx.world * args.steps / el / 1e9
     kern_gbs = ctx.sum_over_ranks(4 * N * pg * args.steps / (st["kernel_ms_total"] / 1e3) / 1e9)
@@ -795,6 +906,8 @@ def run_c4(ctx, args, eng, N, pg, P):
     extra = {"fold_kernel_client_diff_GBps_aggregated": round(kern_gbs, 1),
              "note": "value includes on-device generation of every chunk (writes 4 B/param/client, "
                      "alternating with the fold); the fold kernels alone are fold_kernel_*"}
+    if args.check:
+        extra["check"] = checked
     rec = record(ctx, args, "c4-stream", value, el, "f32", cfg,
                  roofline_of(st, "c4-stream", cfg["kernel_variant"], "k_fedavg"), extra)
     return attach_cpu_baseline(ctx, args, rec, "mean", pg, n=8,
@@ -823,14 +936,27 @@ def run_c5(ctx, args, eng, N, pg, P):
     eng.synth_ckpt_device(args.seed, ckpt.data_ptr(), sp)
     torch.cuda.synchronize()
 
+    full = [out]
+
     def step():
         eng.stream_begin(1, 2)
         for k in range(N):
             eng.ingest(k, bufs[k % n_host].array)
         eng.stream_finish_device(ckpt.data_ptr(), out.data_ptr(), sp)
         if ctx.world > 1:
-            gather_flat(out, P, ctx.world, ctx.rank)
+            full[0] = gather_flat(out, P, ctx.world, ctx.rank)
     el, st = timed(ctx, step, args.steps, args.warmup, eng)
+    checked = None
+    if args.check:
+        lo = eng.lo
+
+        def expected(idx):
+            from oracle import coracle
+            from oracle import oracle as O
+
+            d = np.stack([bufs[k % n_host].array[idx - lo] for k in range(N)])
+            return coracle.fedavg(1, d, O.synth_ckpt(args.seed, idx.astype(np.uint64)))
+        checked = check_sampled(ctx, args, full[0], eng.lo, eng.hi, expected)
     diff_bytes = 4 * N * pg
     value = diff_bytes * ctx.world * args.steps / el / 1e9
     kern_gbs = 4 * N * pg * args.steps / (st["kernel_ms_total"] / 1e3) / 1e9
@@ -843,6 +969,8 @@ def run_c5(ctx, args, eng, N, pg, P):
     extra = {"bound_by": "PCIe host->device (Gen5 x16, 63 GB/s spec per GPU)",
              "ingest_GBps_per_gpu": round(ingest_gbs, 2) if ingest_gbs else None,
              "fold_kernel_client_diff_GBps_per_gpu": round(kern_gbs, 1)}
+    if args.check:
+        extra["check"] = checked
     rec = record(ctx, args, "c5-ingest", value, el, "f32", cfg,
                  roofline_of(st, "c5-ingest", cfg["kernel_variant"], "k_fedavg"), extra)
     attach_cpu_baseline(ctx, args, rec, "iterative", pg, n=4,
@@ -1342,11 +1470,15 @@ def main():
         LIVE_TRAFFIC = measure_live_traffic(args)  # child processes; this one has not touched the GPU yet
     ctx = Ctx(args)
     if args.dry_run:
-        rec = {"dry_run": True, "n_gpus": ctx.n_gpus, "backend": ctx.backend, "group": ctx.group}
+        rec = {"dry_run": True, "n_gpus": ctx.n_gpus, "backend": ctx.backend, "group": ctx.group,
+               "workload": args.workload, "dist_backend": ctx.dist_backend, "rccl_ranks": ctx.rccl_ranks,
+               "check": args.check}
         ctx.close()
         if ctx.rank == 0:
             if launched_elsewhere() and wants_group_line(args):
                 rec["group"] = group_line(args)
+            if ctx.world == 1 or launched_elsewhere():
+                attach_config_lines(args, rec)
             print(json.dumps(rec), flush=True)
         return
     if ctx.group:
@@ -1395,6 +1527,8 @@ def main():
     if ctx.rank == 0:
         if launched_elsewhere() and wants_group_line(args):
             rec["group"] = group_line(args)  # a fresh child: this process never re-execs
+        if ctx.world == 1 or launched_elsewhere():
+            attach_config_lines(args, rec)  # fresh child worlds over the same GPUs
         print(json.dumps(rec), flush=True)
 
 

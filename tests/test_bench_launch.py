@@ -25,29 +25,52 @@ def _json_line(out: str) -> dict:
     return json.loads(lines[0])
 
 
-GROUP_DRY = {"dry_run": True, "n_gpus": 2, "backend": "gloo", "group": True}
+GROUP_DRY = {"dry_run": True, "n_gpus": 2, "backend": "gloo", "group": True, "workload": "resnet18-fedavg"}
+
+
+def _has(rec: dict, sub: dict):
+    assert {k: rec.get(k) for k in sub} == sub, rec
+
+
+def _config_lines(rec: dict, n: int):
+    """Configs 4 and 5 ran as their own N-rank worlds: the ranks, the
+    collective backend and the --check request are on the line."""
+    for key, wl in (("config4", "c4-stream"), ("config5", "c5-ingest")):
+        _has(rec[key], {"dry_run": True, "n_gpus": n, "workload": wl, "dist_backend": "gloo" if n > 1 else None,
+                        "rccl_ranks": 0, "check": True, "group": False})
 
 
 def test_plain_bench_forms_two_ranks():
     """The per-rank world's line, with the one-process group over the same GPUs (what the node
-    deploys, VERDICT r2 next #3) run after the ranks exit, in a fresh child, under `group`."""
+    deploys) run after the ranks exit, in a fresh child, under `group`, and
+    the config-4 / config-5 worlds over the same GPUs under `config4` / `config5`."""
     r = _run(["--gpus", "2", "--dry-run"])
     assert r.returncode == 0, r.stderr
     rec = _json_line(r.stdout)
-    assert rec == {"dry_run": True, "n_gpus": 2, "backend": "gloo", "group": GROUP_DRY}
+    _has(rec, {"dry_run": True, "n_gpus": 2, "backend": "gloo", "dist_backend": "gloo", "rccl_ranks": 0})
+    _has(rec["group"], GROUP_DRY)
+    _config_lines(rec, 2)
 
 
-def test_group_line_can_be_skipped_and_is_skipped_for_per_rank_only_workloads():
-    r = _run(["--gpus", "2", "--dry-run", "--no-group-line"])
+def test_config4_and_5_dry_runs_carry_ranks_backend_and_check():
+    for wl in ("c4-stream", "c5-ingest"):
+        r = _run(["--gpus", "2", "--dry-run", "--workload", wl, "--check"])
+        assert r.returncode == 0, r.stderr
+        rec = _json_line(r.stdout)
+        _has(rec, {"workload": wl, "n_gpus": 2, "dist_backend": "gloo", "rccl_ranks": 0, "check": True,
+                   "group": False})  # no group record: c4 / c5 run per rank only
+        assert "config4" not in rec and "config5" not in rec
+
+
+def test_group_line_can_be_skipped():
+    r = _run(["--gpus", "2", "--dry-run", "--no-group-line", "--no-config-lines"])
     assert r.returncode == 0, r.stderr
-    assert "group" not in {k for k, v in _json_line(r.stdout).items() if isinstance(v, dict)}
-    r = _run(["--gpus", "2", "--dry-run", "--workload", "c4-stream"])
-    assert r.returncode == 0, r.stderr
-    assert _json_line(r.stdout)["group"] is False  # no group record: c4 runs per rank only
+    rec = _json_line(r.stdout)
+    assert not isinstance(rec["group"], dict) and "config4" not in rec
 
 
 def test_plain_bench_forms_three_ranks():
-    r = _run(["--gpus", "3", "--dry-run"])
+    r = _run(["--gpus", "3", "--dry-run", "--no-config-lines"])
     assert r.returncode == 0, r.stderr
     assert _json_line(r.stdout)["n_gpus"] == 3
 
@@ -55,12 +78,14 @@ def test_plain_bench_forms_three_ranks():
 def test_single_rank_dry_run():
     r = _run(["--dry-run"])
     assert r.returncode == 0, r.stderr
-    assert _json_line(r.stdout)["n_gpus"] == 1
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 1
+    _config_lines(rec, 1)
 
 
 def test_launcher_world_mismatch_fails_loudly():
     # a launcher that formed 1 rank while --gpus says 2: exit non-zero, print no result line
-    r = _run(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    r = _run(["--gpus", "2", "--dry-run", "--no-config-lines"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert "WORLD_SIZE 1" in r.stderr
@@ -75,7 +100,8 @@ def test_torchrun_launch_forms_two_ranks():
     assert r.returncode == 0, r.stderr
     rec = _json_line(r.stdout)
     assert rec["n_gpus"] == 2 and rec["backend"] == "gloo"
-    assert rec["group"] == GROUP_DRY  # rank 0 ran the group child itself after the world closed
+    _has(rec["group"], GROUP_DRY)  # rank 0 ran the group child itself after the world closed
+    _config_lines(rec, 2)  # ... and the config-4 / config-5 worlds
 
 
 def test_usable_cores_reports_a_positive_count():
@@ -90,7 +116,8 @@ def test_usable_cores_reports_a_positive_count():
 def test_group_mode_is_one_process_over_n_gpus():
     r = _run(["--gpus", "4", "--group", "--dry-run"])
     assert r.returncode == 0, r.stderr
-    assert _json_line(r.stdout) == {"dry_run": True, "n_gpus": 4, "backend": "gloo", "group": True}
+    _has(_json_line(r.stdout), {"dry_run": True, "n_gpus": 4, "backend": "gloo", "group": True})
+    assert "config4" not in _json_line(r.stdout)
 
 
 def test_roofline_quotes_live_traffic_over_the_committed_file(monkeypatch):
@@ -118,3 +145,28 @@ def test_live_traffic_is_skipped_under_a_profiler(monkeypatch):
     bench = importlib.import_module("bench")
     monkeypatch.setenv("ROCPROF_COUNTERS", "FETCH_SIZE")
     assert bench.under_profiler()
+
+
+def test_check_leg_compares_bit_for_bit(monkeypatch):
+    """bench.check_sampled (the --check leg) on one rank: equal values pass, one flipped low bit of
+    one sampled param fails."""
+    import importlib
+    import types
+
+    import numpy as np
+    import torch
+
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    bench = importlib.import_module("bench")
+    ctx = types.SimpleNamespace(torch=torch, world=1, rank=0, dist=None)
+    args = types.SimpleNamespace(seed=3)
+    full = torch.arange(1000, dtype=torch.float32) * 0.5
+    ok = bench.check_sampled(ctx, args, full, 0, 1000, lambda idx: idx.astype(np.float32) * np.float32(0.5))
+    assert ok["bit_exact"] and ok["mismatches"] == 0 and ok["params_checked"] >= 2
+
+    def off_by_one_ulp(idx):
+        v = idx.astype(np.float32) * np.float32(0.5)
+        v.view(np.uint32)[-1] ^= 1
+        return v
+    bad = bench.check_sampled(ctx, args, full, 0, 1000, off_by_one_ulp)
+    assert not bad["bit_exact"] and bad["mismatches"] == 1
