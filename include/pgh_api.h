@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PGH_ABI_VERSION 6
+#define PGH_ABI_VERSION 7
 
 typedef struct pgh_ctx pgh_ctx;
 
@@ -249,6 +249,10 @@ int pgh_fold_peek(pgh_ctx* ctx, int mode);
  * copy). */
 int pgh_fold_peek_into(pgh_ctx* ctx, int mode, uint8_t* out, size_t n);
 int pgh_peek_patch_state(pgh_ctx* ctx, uint8_t* out, size_t n, int* ok);
+/* ABI 7: *valid = 1 when a peek of the fold state as it stands now exists (the last pgh_fold_peek
+ * took one and nothing changed since; a group: every GPU's), else 0 -- e.g. the peek was skipped
+ * because the previous one's copy was still running.  Never blocks. */
+int pgh_peek_valid(pgh_ctx* ctx, int* valid);
 
 /* Z_2^64 share sum over all clients x parties, then decode float32(sum) / base**prec.
  * sum_out (int64) and dec_out (float32) are host arrays of P_shard; either may be NULL. */

@@ -2634,6 +2634,13 @@ int pgh_peek_patch_state(pgh_ctx* c, uint8_t* out, size_t n, int* ok) {
     return PGH_OK;
 }
 
+int pgh_peek_valid(pgh_ctx* c, int* valid) {
+    if (c && c->grp) return pgh_group_api::peek_valid(c, valid);
+    if (!c || !valid) return PGH_E_ARG;
+    *valid = pgh_int::peek_valid(c) ? 1 : 0;
+    return PGH_OK;
+}
+
 int pgh_fold_busy(pgh_ctx* c, int* busy) {
     if (c && c->grp) return pgh_group_api::fold_busy(c, busy);
     if (!c || !busy) return PGH_E_ARG;

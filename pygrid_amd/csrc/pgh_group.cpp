@@ -837,6 +837,14 @@ int fold_peek_into(pgh_ctx* c, int mode, uint8_t* out, size_t n) {
     return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_peek_into(k, mode, out, n); });
 }
 
+int peek_valid(pgh_ctx* c, int* valid) {
+    RC(need_slab(c));
+    if (!valid) return fail(c, PGH_E_ARG, "valid is NULL");
+    *valid = 1;
+    for (pgh_ctx* k : G(c)->kids) *valid &= pgh_int::peek_valid(k) ? 1 : 0;
+    return PGH_OK;
+}
+
 // All children's peeks must still hold, or none is committed (the group's checkpoint stays whole).
 int peek_patch_state(pgh_ctx* c, uint8_t* out, size_t n, int* ok) {
     RC(need_slab(c));

@@ -79,6 +79,7 @@ int fold_busy(pgh_ctx* c, int* busy);
 int fold_peek(pgh_ctx* c, int mode);
 int fold_peek_into(pgh_ctx* c, int mode, uint8_t* out, size_t n);
 int peek_patch_state(pgh_ctx* c, uint8_t* out, size_t n, int* ok);
+int peek_valid(pgh_ctx* c, int* valid);
 int secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out);
 int stream_begin(pgh_ctx* c, int kind, int fold_batch);
 int stream_flush(pgh_ctx* c);

@@ -349,6 +349,12 @@ class Engine:
         self._check(self._lib.pgh_peek_patch_state(self._h, C.c_void_p(ptr), n, C.byref(ok)), "peek_patch_state")
         return bool(ok.value)
 
+    def peek_valid(self) -> bool:
+        """A peek of the fold state as it stands now exists (the last fold_peek was not skipped)."""
+        v = C.c_int(0)
+        self._check(self._lib.pgh_peek_valid(self._h, C.byref(v)), "peek_valid")
+        return bool(v.value)
+
     def fold_busy(self) -> bool:
         """The last slot fold issued is still running (non-blocking)."""
         b = C.c_int(0)

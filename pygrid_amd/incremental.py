@@ -366,10 +366,14 @@ class IncrementalCycle:
                 # every reporter so far is folded: take the close's FINAL pass now, in the background
                 try:
                     self.engine.fold_peek(self.mode, into=self._prepared[1] if self._prepared[1][1] else None)
-                    self._peeked = (len(self._folded), self.rewinds)
                 except AggregationError as e:  # e.g. no HBM for the peek buffer: close the usual way
                     log.warning("speculative close disabled for this cycle: %s", e)
                     self._peek = False
+                    return
+                if not hasattr(self.engine, "peek_valid") or self.engine.peek_valid():
+                    self._peeked = (len(self._folded), self.rewinds)
+                else:  # skipped (the previous peek's copy still running): try again once reports pause
+                    self._defer()
 
     def _defer(self):
         if self._timer is None and self._defer_left > 0:

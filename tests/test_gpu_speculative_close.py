@@ -228,3 +228,40 @@ def test_report_time_close_of_a_large_shard_pipelines_its_final_pass(mode, specu
             flat = eng.ckpt_download()
             assert np.array_equal(bits(flat), bits(np.concatenate([w.reshape(-1) for w in want])))
             ck = new
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_peek_valid_tracks_the_fold_state(devices):
+    """pgh_peek_valid (ABI 7): true after a peek of the fold state as it stands, false
+    once a later fold changed it, true again after the next peek -- for a group only when every
+    GPU's peek holds.  IncrementalCycle records a peek only when it was taken (a skipped one is
+    retried by the settle timer), so a close after a burst still commits a peek."""
+    import time
+
+    from pygrid_amd import Engine
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(860)
+    numel = [int(np.prod(s)) for s in SHAPES]
+    ckpt = [rng.standard_normal(s).astype(F) for s in SHAPES]
+    ck = build_state_fast(ckpt)
+    diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES] for w in range(4)}
+    with (Engine(0) if devices is None else Engine(devices=devices)) as eng:
+        inc = IncrementalCycle(eng, numel, slots=6, checkpoint=ck, lazy=False)
+        for w in range(4):
+            inc.assigned(w)
+        inc.reported(0, build_state_fast(diffs[0]))  # folded and peeked at once
+        eng.sync()
+        assert eng.peek_valid()
+        inc.reported(1, build_state_fast(diffs[1]))
+        inc.reported(2, build_state_fast(diffs[2]))
+        inc.reported(3, build_state_fast(diffs[3]))
+        deadline = time.monotonic() + 5
+        while not eng.peek_valid() and time.monotonic() < deadline:  # a skipped peek is retried
+            time.sleep(0.01)
+        assert eng.peek_valid()
+        new = inc.close(ck)
+        assert inc.last_close["peeked"]
+        for g, w in zip(parse_state(new), O.fedavg_mean(ckpt, [diffs[w] for w in range(4)])):
+            assert np.array_equal(bits(g), bits(w))
