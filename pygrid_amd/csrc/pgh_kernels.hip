@@ -415,18 +415,41 @@ __global__ __launch_bounds__(TB) void k_secagg(SecaggArgs a, int64_t ncol) {
 }
 
 // Page-locked report ingest (pgh_ingest_state): one workgroup per chunk of a float payload that
-// sits at an arbitrary byte offset of the DMA'd message; lanes read the two aligned dwords around
-// their float and funnel-shift it out (v_alignbyte), then store into the blocked slab row.  Bound by
-// HBM like a copy (4 B read + 4 B written per param; the message is read once).
+// sits at an arbitrary byte offset of the DMA'd message.  After a head that brings the slab column
+// to a multiple of 4, each lane moves 4 floats: one 16-byte load of the 4 dwords around them (plus
+// the dword after, for an unaligned payload) funnel-shifted out (v_alignbyte), one 16-byte store
+// into the blocked slab row (blocks are multiples of 64 columns, so 4 aligned columns never straddle
+// one).  Bound by HBM like a copy: 4 B read + 4 B written per param, the message read once.
 __global__ __launch_bounds__(BLOCK) void k_gather_f32(const uint8_t* bytes, const GChunk* tab, float* row,
                                                       SlabMap m) {
     const GChunk ch = tab[blockIdx.x];
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(bytes + (ch.src & ~int64_t(3)));
+    const int head = (int)min((int64_t)ch.n, (4 - (ch.dst & 3)) & 3);
+    const int body = (ch.n - head) & ~3;
     const uint32_t sh = (uint32_t)(ch.src & 3);
-    for (int t = threadIdx.x; t < ch.n; t += BLOCK) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(bytes + (ch.src & ~int64_t(3)));
+    auto one = [&](int t) {
         const uint32_t lo = w[t];
         const uint32_t v = sh ? __builtin_amdgcn_alignbyte(w[t + 1], lo, sh) : lo;
         row[m.at(ch.dst + t)] = __uint_as_float(v);
+    };
+    if ((int)threadIdx.x < head) one((int)threadIdx.x);
+    const int tail0 = head + body;
+    if ((int)threadIdx.x < ch.n - tail0) one(tail0 + (int)threadIdx.x);
+    for (int q = (int)threadIdx.x * 4; q < body; q += BLOCK * 4) {
+        const int t = head + q;
+        uint4 a;
+        __builtin_memcpy(&a, w + t, 16);  // 4-byte aligned: a dwordx4 load (unaligned access is legal)
+        float4 o;
+        if (sh) {
+            const uint32_t e = w[t + 4];
+            o.x = __uint_as_float(__builtin_amdgcn_alignbyte(a.y, a.x, sh));
+            o.y = __uint_as_float(__builtin_amdgcn_alignbyte(a.z, a.y, sh));
+            o.z = __uint_as_float(__builtin_amdgcn_alignbyte(a.w, a.z, sh));
+            o.w = __uint_as_float(__builtin_amdgcn_alignbyte(e, a.w, sh));
+        } else {
+            o = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
+        }
+        *reinterpret_cast<float4*>(row + m.at(ch.dst + t)) = o;
     }
 }
 
@@ -948,7 +971,9 @@ hipError_t launch_varint_decode(const uint8_t* bytes, const VChunk* chunks, int 
 
 hipError_t launch_gather_f32(const uint8_t* bytes, const GChunk* chunks, int n_chunks, float* row, const SlabMap& m,
                              hipStream_t s) {
-    if (n_chunks < 0 || (n_chunks > 0 && (!bytes || !chunks || !row)) || (reinterpret_cast<uintptr_t>(bytes) & 3))
+    // 16-byte row stores: the row and the map's column offset 4-aligned (blocks are multiples of 4)
+    if (n_chunks < 0 || (n_chunks > 0 && (!bytes || !chunks || !row)) || (reinterpret_cast<uintptr_t>(bytes) & 3) ||
+        (reinterpret_cast<uintptr_t>(row) & 15) || (m.off & 3) || (m.ld & 3) || (m.bstride & 3))
         return hipErrorInvalidValue;
     if (n_chunks == 0) return hipSuccess;
     k_gather_f32<<<(unsigned)n_chunks, BLOCK, 0, s>>>(bytes, chunks, row, m);
