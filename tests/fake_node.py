@@ -21,6 +21,7 @@ on real SQLAlchemy tables (``make_node(warehouse=...)``).
 """
 from __future__ import annotations
 
+import threading
 import types
 from datetime import datetime, timedelta
 from functools import reduce
@@ -38,15 +39,17 @@ class Warehouse:
         self.rows = []
         self.next_id = 1
         self.row_order = None  # callable(list of rows) -> list in "physical" order, or None (id order)
+        self._lock = threading.Lock()  # autoincrement ids under concurrent handlers
 
     def register(self, **kw):
-        r = Row(id=self.next_id, **kw)
-        self.next_id += 1
-        self.rows.append(r)
+        with self._lock:
+            r = Row(id=self.next_id, **kw)
+            self.next_id += 1
+            self.rows.append(r)
         return r
 
     def _match(self, kw):
-        return [r for r in self.rows if all(getattr(r, k, None) == v for k, v in kw.items())]
+        return [r for r in list(self.rows) if all(getattr(r, k, None) == v for k, v in kw.items())]
 
     def query(self, **kw):
         got = self._match(kw)

@@ -203,3 +203,88 @@ def test_gate_close_waits_only_for_reports_in_flight():
     for th in (t, c, late):
         th.join(10)
     assert order == ["report", "close", "late"]
+
+
+class JitterWarehouse(SlowUpdateWarehouse):
+    """Every commit of submit_worker_diff takes 0-2 ms (a DB write), so a close's snapshot often
+    lands between a report's DB write and its ingest -- where only the report gate keeps them
+    consistent."""
+
+    def __init__(self, wh):
+        super().__init__(wh)
+        import random
+
+        self.rng = random.Random(7)
+
+    def update(self):
+        time.sleep(self.rng.random() * 0.002)
+        return self.wh.update()
+
+
+def test_concurrent_handlers_and_closes_equal_the_reference_over_each_snapshot(monkeypatch):
+    """Linearizability under load: 4 handler threads assign, report and re-report workers of
+    whatever cycle is open (late reports included) while closes run on the executor.  Each close's
+    snapshot of the completed rows (taken under the report gate) is recorded with the diffs the
+    rows held then; the reference node, replayed serially over exactly those rows, must save the
+    same checkpoint bytes, cycle after cycle."""
+    import random
+
+    ex = NamedExecutor()
+    mod = make_node()
+    mod.run_task_once = ex.run_task_once
+    node = pnode.install(mod, engine=NumpyEngine(), framing="template", fold_batch=1)
+    cm = mod.cycle_manager
+    cm._worker_cycles = JitterWarehouse(cm._worker_cycles)  # widen the write -> ingest window
+    cfg = {"min_diffs": 5, "max_diffs": 5, "num_cycles": 4}
+    snaps = []
+    real_rows = pnode.completed_rows
+
+    def recording_rows(cm_, cycle_id):
+        rows = real_rows(cm_, cycle_id)
+        snaps.append([(r.id, r.diff) for r in rows])  # under the exclusive gate: the DB as read
+        return rows
+    monkeypatch.setattr(pnode, "completed_rows", recording_rows)
+    proc, _, _ = host_process(mod, cfg, ckpt_bytes())
+    stop = threading.Event()
+    errors = []
+
+    def handler(seed):
+        rng = random.Random(seed)
+        v = 0
+        try:
+            while not stop.is_set():
+                w = f"h{seed}-{rng.randrange(4)}"
+                try:
+                    key = assign(mod, w, proc)
+                except AttributeError:  # every cycle done: cycle_manager.last() found none
+                    return
+                for _ in range(rng.choice((1, 1, 2))):  # sometimes a re-report
+                    v += 1
+                    cm.submit_worker_diff(w, key, diff_bytes(w, v))
+                    time.sleep(rng.random() * 0.003)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    threads = [threading.Thread(target=handler, args=(s,)) for s in range(4)]
+    for t in threads:
+        t.start()
+    deadline = time.monotonic() + 60
+    while len(checkpoints(mod)) < 5 and time.monotonic() < deadline:
+        time.sleep(0.01)
+    stop.set()
+    for t in threads:
+        t.join(10)
+    ex.wait()
+    node.uninstall()
+    assert not errors, errors
+    assert cm.task_errors == []
+    saved = checkpoints(mod)
+    assert len(saved) == 5 and len(snaps) == 4, (len(saved), len(snaps))
+    # replay each close on a fresh reference node: the previous checkpoint, the snapshot's rows
+    for k, rows in enumerate(snaps):
+        ref = make_node()
+        rp, _, _ = host_process(ref, {"min_diffs": len(rows), "max_diffs": len(rows), "num_cycles": 1}, saved[k][2])
+        keys = [assign(ref, i, rp) for i in range(len(rows))]
+        for i, (_, d) in enumerate(rows):
+            ref.cycle_manager.submit_worker_diff(i, keys[i], d)
+        assert checkpoints(ref)[-1][2] == saved[k + 1][2], f"close {k}"
