@@ -423,33 +423,42 @@ class NodeEngine:
 
 class _Gate:
     """Shared (reports: DB write + ingest) / exclusive (a close's snapshot of the rows) lock.  A
-    waiting close keeps new reports out, so it waits only for the reports already in flight."""
+    waiting close keeps new reports out, so it waits only for the reports already in flight.  A
+    close requested synchronously from inside a report (a node that runs ``complete_cycle`` inline
+    instead of through the patched ``run_task_once``) upgrades: it waits for the OTHER reports in
+    flight, never for its own handler."""
 
     def __init__(self):
         self._cv = threading.Condition(threading.Lock())
         self._shared = 0
         self._exclusive = False
         self._waiting = 0
+        self._mine = threading.local()  # shared holds of this thread
 
     @contextlib.contextmanager
     def shared(self):
         with self._cv:
-            while self._exclusive or self._waiting:
+            while (self._exclusive or self._waiting) and not getattr(self._mine, "n", 0):
                 self._cv.wait()
             self._shared += 1
+        self._mine.n = getattr(self._mine, "n", 0) + 1
         try:
             yield
         finally:
+            self._mine.n -= 1
             with self._cv:
                 self._shared -= 1
                 if not self._shared:
                     self._cv.notify_all()
+                elif self._waiting:
+                    self._cv.notify_all()
 
     def acquire_exclusive(self):
+        mine = getattr(self._mine, "n", 0)
         with self._cv:
             self._waiting += 1
             try:
-                while self._exclusive or self._shared:
+                while self._exclusive or self._shared - mine:
                     self._cv.wait()
             finally:
                 self._waiting -= 1

@@ -153,11 +153,13 @@ def complete_cycle(cycle_manager, cycle_id):  # tasks/cycle.py:28-37
         return e
 
 
-def make_node(warehouse=Warehouse):
+def make_node(warehouse=Warehouse, mod=None):
     """A fresh node: a module-like namespace holding what cycle_manager.py holds (CycleManager,
     run_task_once, complete_cycle, model_manager, process_manager, PlanManager).  ``warehouse(name)``
-    makes the tables ("model", "checkpoint", "cycle", "worker_cycle")."""
-    mod = types.SimpleNamespace()
+    makes the tables ("model", "checkpoint", "cycle", "worker_cycle"); ``mod``: fill this object
+    (e.g. a module) instead of a new namespace -- its ``run_task_once`` is what submit_worker_diff
+    calls, as the reference's module global is."""
+    mod = types.SimpleNamespace() if mod is None else mod
     mod.model_manager = ModelManager(warehouse)
     mod.process_manager = ProcessManager()
     mod.PlanManager = PlanManager

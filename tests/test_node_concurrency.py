@@ -288,3 +288,26 @@ def test_concurrent_handlers_and_closes_equal_the_reference_over_each_snapshot(m
         for i, (_, d) in enumerate(rows):
             ref.cycle_manager.submit_worker_diff(i, keys[i], d)
         assert checkpoints(ref)[-1][2] == saved[k + 1][2], f"close {k}"
+
+
+def test_close_run_inline_from_a_report_does_not_deadlock():
+    """A node whose submit_worker_diff runs complete_cycle inline (not through the patched
+    run_task_once): the close's exclusive gate upgrades the report's shared hold instead of waiting
+    for it forever; the close reads the triggering diff from the DB (its ingest has not run yet)."""
+    mod = make_node()
+    node = pnode.install(mod, engine=NumpyEngine(), framing="template", fold_batch=1)
+    mod.run_task_once = lambda name, func, *args: func(*args)  # bypasses install's hold-and-dispatch
+    proc, _, _ = host_process(mod, CFG3, ckpt_bytes())
+    keys = {w: assign(mod, w, proc) for w in range(1, 4)}
+    t = threading.Thread(target=lambda: [mod.cycle_manager.submit_worker_diff(w, keys[w], diff_bytes(w))
+                                         for w in (1, 2, 3)])
+    t.start()
+    t.join(10)
+    assert not t.is_alive(), "deadlock: the inline close waited for its own report's gate"
+    node.uninstall()
+    ref = make_node()
+    rproc, _, _ = host_process(ref, CFG3, ckpt_bytes())
+    rkeys = {w: assign(ref, w, rproc) for w in range(1, 4)}
+    for w in (1, 2, 3):
+        ref.cycle_manager.submit_worker_diff(w, rkeys[w], diff_bytes(w))
+    assert checkpoints(mod) == checkpoints(ref) and len(checkpoints(mod)) == 2

@@ -234,3 +234,43 @@ def test_malformed_report_answers_like_the_reference(tmp_path):
         finally:
             sc.finish()
     assert answers[0] == answers[1] and answers[0]
+
+
+def test_install_into_node_by_package_name(tmp_path, monkeypatch):
+    """``install_into_node("src.app")`` imports the node's modules by the reference's layout
+    (``src/app/main/model_centric/cycles/cycle_manager.py``, ``src/app/main/events/model_centric/
+    fl_events.py``, ``src/app.executor``): here a throwaway package with that layout over
+    tests/fake_node.py and the restated handler.  The handler's ``base64`` is replaced, the close
+    runs on the engine, and uninstall restores both."""
+    import importlib
+    import shutil
+    import sys
+
+    pkg = tmp_path / "nodepkg"
+    (pkg / "main" / "model_centric" / "cycles").mkdir(parents=True)
+    (pkg / "main" / "events" / "model_centric").mkdir(parents=True)
+    for d in (pkg, pkg / "main", pkg / "main" / "model_centric", pkg / "main" / "model_centric" / "cycles",
+              pkg / "main" / "events", pkg / "main" / "events" / "model_centric"):
+        (d / "__init__.py").write_text("")
+    (pkg / "__init__.py").write_text("executor = None\n")
+    (pkg / "main" / "model_centric" / "cycles" / "cycle_manager.py").write_text(
+        "import sys\nimport fake_node\nfake_node.make_node(mod=sys.modules[__name__])\n")
+    shutil.copy(ref_fl_events.__file__, pkg / "main" / "events" / "model_centric" / "fl_events.py")
+    monkeypatch.syspath_prepend(str(tmp_path))
+    try:
+        node = pnode.install_into_node("nodepkg", engine=NumpyEngine(), framing="template", pinned_reports=0)
+        cmm = importlib.import_module("nodepkg.main.model_centric.cycles.cycle_manager")
+        fle = importlib.import_module("nodepkg.main.events.model_centric.fl_events")
+        assert isinstance(fle.base64, pnode._Base64)
+        fle.processes = types.SimpleNamespace(submit_diff=lambda *a: cmm.cycle_manager.submit_worker_diff(*a))
+        proc, _, _ = host_process(cmm, {"min_diffs": 2, "max_diffs": 2}, ckpt_bytes())
+        keys = {w: assign(cmm, w, proc) for w in ("a", "b")}
+        for w in ("a", "b"):
+            msg = {"data": {"worker_id": w, "request_key": keys[w], "diff": base64.b64encode(diff_bytes(w)).decode()}}
+            assert fle.report(msg)["data"] == {"status": "success"}
+        assert node.stats["closes_report_time"] == 1
+        node.uninstall()
+        assert fle.base64 is base64
+    finally:
+        for m in [m for m in sys.modules if m == "nodepkg" or m.startswith("nodepkg.")]:
+            del sys.modules[m]
