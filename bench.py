@@ -1285,9 +1285,10 @@ def report_close(ctx, args, eng, cycles: int = 4, assigned: int = 100):
     order, each State diff to HBM (and folded) when reported.  Timed: from the last report's
     ``reported`` returning to the new checkpoint bytes ready on the executor thread -- nothing
     waits between the two, nothing syncs the GPU before the clock starts.  Two arrival patterns
-    (reports `paced` 5 ms apart -- a node decodes each report's base64 for a few ms anyway,
-    tools/node_sim.py -- and `back_to_back`) x speculative / certain-only early folds; the headline
-    is the product default (`IncrementalCycle(speculate=None)`), paced.  1 warm-up cycle each."""
+    (reports `paced` 5 ms apart -- a node handles each report for tens of ms anyway, its DB write
+    included, tools/node_sim.py -- and `back_to_back`) x the product default and the alternatives
+    (speculative folds with / without the peeked close, certain-only folds); the headline is the
+    product default, paced.  1 warm-up cycle each."""
     from concurrent.futures import ThreadPoolExecutor
 
     import numpy as np
@@ -1303,12 +1304,15 @@ def report_close(ctx, args, eng, cycles: int = 4, assigned: int = 100):
                                   for s in RESNET18_SHAPES]) for _ in range(4)]
     reporters = [w for w in range(assigned) if w != 0 and rng.random() >= 0.2]
     arms = {}
+    # (arm, IncrementalCycle options): the product default first, then the alternatives
+    kinds = (("default", {}), ("speculative_peek", {"speculate": True, "peek": True}),
+             ("speculative_no_peek", {"speculate": True, "peek": False}), ("certain_only", {"speculate": False}))
     with ThreadPoolExecutor(1, thread_name_prefix="executor") as executor:
         for arrival, gap_ms in (("paced", 5.0), ("back_to_back", 0.0)):
-            for speculate in (None, False):
+            for kind, opts in kinds:
                 closes, left = [], []
                 for cyc in range(cycles + 1):
-                    inc = IncrementalCycle(eng, numel, slots=assigned, checkpoint=ck_pb, speculate=speculate)
+                    inc = IncrementalCycle(eng, numel, slots=assigned, checkpoint=ck_pb, **opts)
                     for w in range(assigned):
                         inc.assigned(w)
                     for i, w in enumerate(rng.permutation(reporters)):
@@ -1320,14 +1324,13 @@ def report_close(ctx, args, eng, cycles: int = 4, assigned: int = 100):
                     if cyc:
                         closes.append((time.perf_counter() - t0) * 1e3)
                         left.append(inc.last_close["n"] - inc.last_close["early"])
-                arm = "speculative" if inc.speculate else "certain_only"
-                if speculate is None:
-                    default = inc.speculate
-                arms[f"{arrival}_{arm}"] = {"close_ms": round(float(np.median(closes)), 3),
+                if kind == "default":
+                    default = {"speculate": inc.speculate, "peek": inc.peek_enabled}
+                arms[f"{arrival}_{kind}"] = {"close_ms": round(float(np.median(closes)), 3),
                                             "closes_ms": [round(c, 3) for c in closes],
                                             "rows_left_to_fold_at_close": int(np.median(left))}
-    head = arms["paced_" + ("speculative" if default else "certain_only")]
-    return {"close_ms_after_last_report": head["close_ms"], "arms": arms, "default_speculative": default,
+    head = arms["paced_default"]
+    return {"close_ms_after_last_report": head["close_ms"], "arms": arms, "default": default,
             "assigned": assigned, "reporters": len(reporters), "gpus": ctx.n_gpus,
             "definition": "the reference's trigger: the last report's handler returns, the close runs at once on "
                           "an executor thread (run_task_once, cycle_manager.py:176-178); timed from that return "

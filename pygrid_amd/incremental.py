@@ -677,6 +677,11 @@ class IncrementalCycle:
                 self.engine.ckpt_owner = None
 
     @property
+    def peek_enabled(self) -> bool:
+        """The speculative close (pgh_fold_peek_into) is on for this cycle."""
+        return bool(self._peek)
+
+    @property
     def declined(self) -> Optional[str]:
         """Why the engine will not average this cycle (``close`` raises ``ModelNotAcceleratedError``),
         or None."""

@@ -117,7 +117,7 @@ class NodeEngine:
                  report_time: bool = True, close_trigger: str = "reference", deadline: bool = False,
                  keep_checkpoints: int = 4, slots: Optional[int] = None, fold_batch: int = 8,
                  mean_plans: Optional[str] = None, framing: str = "fresh", report_module=None,
-                 pinned_reports: int = 16, speculate: Optional[bool] = None):
+                 pinned_reports: int = 16, speculate: Optional[bool] = None, peek: Optional[bool] = None):
         if close_trigger not in ("reference", "replay"):
             raise AggregationError(f"close_trigger must be 'reference' or 'replay', not {close_trigger!r}")
         if deadline and close_trigger != "replay":
@@ -135,6 +135,7 @@ class NodeEngine:
         self.slots = slots
         self.fold_batch = fold_batch
         self.speculate = speculate
+        self.peek = peek
         self.framing = framing
         self.store = CheckpointStore(keep=keep_checkpoints) if keep_checkpoints else None
         self.report_module = report_module
@@ -308,7 +309,8 @@ class NodeEngine:
                            shapes=lambda: _shapes(ckpt))
         self.aggregator._resident = None  # the report-time cycle takes over the engine's slab
         inc = IncrementalCycle(self.engine, numel, mode=mode, slots=self.slots, fold_batch=self.fold_batch,
-                               checkpoint=ckpt, speculate=self.speculate)
+                               checkpoint=ckpt, speculate=self.speculate,
+                               **({} if self.peek is None else {"peek": self.peek}))
         for row in _rows(cm, cycle_id=cycle.id):  # after a restart: the rows assigned before it
             inc.assigned(row.id, key=row.id)
         return inc

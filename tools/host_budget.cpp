@@ -6,7 +6,7 @@
 //   stage    T threads copy pageable -> page-locked with non-temporal stores: the library's
 //            staging copy pool (pgh_api.cpp copy_stream) alone, no DMA
 //   register hipHostRegister + hipHostUnregister of fresh pageable buffers of one diff's size
-//            (page-locking a message in place instead of copying it)
+//            (page-locking a message in place instead of copying it); register_parallel: T threads
 //   h2d      page-locked -> GPU 0 DMA (hipMemcpyAsync)
 //   stage+h2d  the staging copy with T threads while GPU 0's DMA reads the other page-locked half
 //            (the two compete for DRAM as in a close)
@@ -150,6 +150,26 @@ int main(int argc, char** argv) {
         std::snprintf(buf, sizeof buf, ", \"register_GBps\": %.1f, \"unregister_GBps\": %.1f, \"register_ms_per_47MB\": %.3f",
                       k * m / reg / 1e9, k * m / unreg / 1e9, reg / k * 1e3);
         js += buf;
+        for (auto* p : bufs) std::free(p);
+    }
+    // page-locking in parallel: T threads each register + unregister their own 47 MB buffers (does
+    // pinning scale with threads, as a group's per-GPU ingest threads would need?)
+    {
+        const size_t m = 46758048;
+        const int per = 4;
+        std::vector<uint8_t*> bufs;
+        for (int i = 0; i < 16 * per; ++i) bufs.push_back(pageable(m));
+        series("register_parallel", [&](int t) {
+            const double t0 = now_s();
+            run_threads(t, [&](int k) {
+                for (int i = 0; i < per; ++i) HIPCK(hipHostRegister(bufs[(size_t)(k * per + i)], m, hipHostRegisterDefault));
+            });
+            const double dt = now_s() - t0;
+            run_threads(t, [&](int k) {
+                for (int i = 0; i < per; ++i) HIPCK(hipHostUnregister(bufs[(size_t)(k * per + i)]));
+            });
+            return (double)t * per * m / dt / 1e9;
+        });
         for (auto* p : bufs) std::free(p);
     }
     // DMA alone, then the staging copy beside it

@@ -13,8 +13,9 @@ the reference's own storage types and report handler code (VERDICT r3 next #1-#2
   (tasks/cycle.py:9-25).
 
 ResNet-18, 100 workers assigned per cycle, 80 report (worker 0 and 19 others never do,
-routes.py:314; ``max_diffs`` = 80), shuffled arrival.  Four arms: reports ``paced`` ``--gap-ms``
-apart (default 5) or back to back, x speculative / certain-only early folds.
+routes.py:314; ``max_diffs`` = 80), shuffled arrival.  Arms: reports ``paced`` ``--gap-ms`` apart
+(default 5) or back to back (``b2b``), x the product default / speculative folds with the peeked
+close (``peek``) / without (``spec``) / certain-only folds (``certain``).
 
     python tools/node_sim.py [cycles] [--gap-ms=5] [--no-pinned] [--db=PATH] [--arms=paced_spec,...] [--cpu]
 
@@ -92,12 +93,12 @@ class Timer:
         return f
 
 
-def run_arm(eng, cycles, gap_ms, speculate, pinned, db, rng, ckpt, texts, framing="fresh"):
+def run_arm(eng, cycles, gap_ms, opts, pinned, db, rng, ckpt, texts, framing="fresh"):
     mod, store = make_sql_node(db)
     ex = Executor()
     mod.run_task_once = ex.run_task_once
     node = pnode.install(mod, engine=eng, report_module=ref_fl_events, pinned_reports=16 if pinned else 0,
-                         speculate=speculate, framing=framing)
+                         framing=framing, **opts)
     ref_fl_events.processes = type("P", (), {"submit_diff": staticmethod(
         lambda *a: mod.cycle_manager.submit_worker_diff(*a))})
     timer = Timer()
@@ -189,7 +190,7 @@ def main():
     gap = float(opt.get("gap-ms", 5.0))
     pinned = "--no-pinned" not in sys.argv
     db = f"sqlite:///{opt['db']}" if "db" in opt else "sqlite://"
-    want = opt.get("arms", "paced_spec,paced_certain,b2b_spec,b2b_certain").split(",")
+    want = opt.get("arms", "paced_default,paced_peek,paced_spec,paced_certain,b2b_default,b2b_certain").split(",")
     rng = np.random.default_rng(2024)
     ckpt = build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in RESNET18_SHAPES])
     texts = [base64.b64encode(build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2)
@@ -200,7 +201,9 @@ def main():
     with (Engine(0) if "--cpu" not in sys.argv else _nullctx(NumpyEngine())) as eng:
         for name in want:
             pace, kind = name.split("_")
-            arms[name] = run_arm(eng, cycles, gap if pace == "paced" else 0.0, None if kind == "spec" else False,
+            opts = {"default": {}, "peek": {"speculate": True, "peek": True}, "spec": {"speculate": True, "peek": False},
+                    "certain": {"speculate": False}}[kind]
+            arms[name] = run_arm(eng, cycles, gap if pace == "paced" else 0.0, opts,
                                  pinned, db, rng, ckpt, texts, framing="template" if "--cpu" in sys.argv else "fresh")
             print(f"# {name}: close {arms[name]['close_ms']} ms, handler p50 {arms[name]['report_handler_ms']['p50']} ms",
                   file=sys.stderr, flush=True)
