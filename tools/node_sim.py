@@ -107,12 +107,15 @@ def run_arm(eng, cycles, gap_ms, opts, pinned, db, rng, ckpt, texts, framing="fr
     finish = incremental.IncrementalCycle.finish
     engine_close = []
 
+    close_info = []
+
     def timed_finish(self, *a, **k):
         t0 = time.perf_counter()
         try:
             return finish(self, *a, **k)
         finally:
             engine_close.append((time.perf_counter() - t0) * 1e3)
+            close_info.append({k_: self.last_close.get(k_) for k_ in ("peeked", "early", "n", "from_db", "refold")})
     incremental.IncrementalCycle.finish = timed_finish
     try:
         cfg = {"min_diffs": REPORTERS, "max_diffs": REPORTERS, "num_cycles": 0}
@@ -169,6 +172,7 @@ def run_arm(eng, cycles, gap_ms, opts, pinned, db, rng, ckpt, texts, framing="fr
                                       "engine_on_report_ingest": pct(ingest, 50)},
             "close_ms": pct(closes, 50), "closes_ms": [round(c, 3) for c in closes],
             "engine_close_ms": pct([e for e in engine_share if e is not None], 50),
+            "engine_closes": close_info[1:],
             "node_stats": stats, "pinned_pool": pools}
 
 
