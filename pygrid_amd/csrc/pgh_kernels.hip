@@ -435,35 +435,21 @@ __global__ __launch_bounds__(BLOCK) void k_gather_f32(const uint8_t* bytes, cons
     if ((int)threadIdx.x < head) one((int)threadIdx.x);
     const int tail0 = head + body;
     if ((int)threadIdx.x < ch.n - tail0) one(tail0 + (int)threadIdx.x);
-    // a chunk is at most GATHER_CHUNK = 16 x BLOCK floats: each lane's (up to) 4 float4s, all loads
-    // issued before the first store (16 B x 5 in flight per lane instead of one)
-    static_assert(GATHER_CHUNK <= 16 * BLOCK, "k_gather_f32: a lane moves at most 4 float4 per chunk");
-    uint4 a[4];
-    uint32_t e[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int q = ((int)threadIdx.x + k * BLOCK) * 4;
-        if (q < body) {
-            __builtin_memcpy(&a[k], w + head + q, 16);  // 4-byte aligned dwordx4 (unaligned access is legal)
-            e[k] = sh ? w[head + q + 4] : 0u;
+    for (int q = (int)threadIdx.x * 4; q < body; q += BLOCK * 4) {
+        const int t = head + q;
+        uint4 a;
+        __builtin_memcpy(&a, w + t, 16);  // 4-byte aligned: a dwordx4 load (unaligned access is legal)
+        float4 o;
+        if (sh) {
+            const uint32_t e = w[t + 4];
+            o.x = __uint_as_float(__builtin_amdgcn_alignbyte(a.y, a.x, sh));
+            o.y = __uint_as_float(__builtin_amdgcn_alignbyte(a.z, a.y, sh));
+            o.z = __uint_as_float(__builtin_amdgcn_alignbyte(a.w, a.z, sh));
+            o.w = __uint_as_float(__builtin_amdgcn_alignbyte(e, a.w, sh));
+        } else {
+            o = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
         }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int q = ((int)threadIdx.x + k * BLOCK) * 4;
-        if (q < body) {
-            float4 o;
-            if (sh) {
-                o.x = __uint_as_float(__builtin_amdgcn_alignbyte(a[k].y, a[k].x, sh));
-                o.y = __uint_as_float(__builtin_amdgcn_alignbyte(a[k].z, a[k].y, sh));
-                o.z = __uint_as_float(__builtin_amdgcn_alignbyte(a[k].w, a[k].z, sh));
-                o.w = __uint_as_float(__builtin_amdgcn_alignbyte(e[k], a[k].w, sh));
-            } else {
-                o = make_float4(__uint_as_float(a[k].x), __uint_as_float(a[k].y), __uint_as_float(a[k].z),
-                                __uint_as_float(a[k].w));
-            }
-            *reinterpret_cast<float4*>(row + m.at(ch.dst + head + q)) = o;
-        }
+        *reinterpret_cast<float4*>(row + m.at(ch.dst + t)) = o;
     }
 }
 

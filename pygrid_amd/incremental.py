@@ -15,17 +15,17 @@ diff lives from WHEN it is folded:
   order);
 * the fold follows the assignment order (``assigned(w, key)``, ``key`` = the WorkerCycle row id),
   reporters only, through the slots where the diffs landed (the kernel reads them through a row
-  table).  A position is CERTAIN once every worker assigned before it has reported.  Speculative
-  folds (default): every reported diff is folded at once (``pgh_fold_slots_keep``: its slot is kept)
+  table).  A position is CERTAIN once every worker assigned before it has reported.  Certain-only
+  folds (default): the certain prefix is folded ``fold_batch`` at a time and freed
+  (``pgh_fold_slots``).  Speculative folds (opt-in, ``speculate=True``: under the reference's
+  trigger, a close right after the last report, they measured slower, profiles/r04b): every
+  reported diff is folded at once (``pgh_fold_slots_keep``: its slot is kept)
   and the fold state is saved every ``mark_every`` rows and at the certain point
   (``pgh_fold_mark``); when an earlier worker reports after all, or a kept one re-reports, the fold
   goes back to the last saved state before its position (``pgh_fold_rewind``) and continues; slots
   before the last saved state at the certain point are freed.  While the GPU is still busy with the
   previous fold (``pgh_fold_busy``), or reports arrive less than ``min_gap_ms`` apart, a report is
-  folded with a later one -- or by a timer once no report has come for ``settle_ms``.  Certain-only
-  folds
-  (``speculate=False``): the certain prefix is folded ``fold_batch`` at a time and freed
-  (``pgh_fold_slots``);
+  folded with a later one -- or by a timer once no report has come for ``settle_ms``;
 * ``close(checkpoint, order=..., fetch=...)`` takes the AUTHORITATIVE order -- the keys of the
   completed-WorkerCycle query, as the node's DB returns them -- keeps the early fold up to the last
   saved state inside its common prefix with that order, and folds the rest of the order from HBM
@@ -34,7 +34,7 @@ diff lives from WHEN it is folded:
   prefix, a freed worker re-reported, an assignment arrived behind it) the fold restarts
   (``pgh_fold_slots_restart``) and re-folds the whole order, the folded diffs fetched from the DB:
   bit-identical to the reference in every case, early folding is only ever a speedup;
-* speculative close (``peek=True``): whenever every reporter is folded, the close's FINAL pass,
+* speculative close (with speculative folds, ``peek=True``): whenever every reporter is folded, the close's FINAL pass,
   its D2H and the copy of the payloads into the cycle's prepared output bytes run ahead
   (``pgh_fold_peek_into``); a close whose order and fold state match that peek only commits it
   (``pgh_peek_patch_state``), any other close folds and copies as usual.
@@ -110,7 +110,9 @@ class IncrementalCycle:
         # saved fold states the speculation may hold in HBM (each P floats); < 2 turns it off
         self.max_marks = int(min(MAX_MARKS, speculation_budget // max(4 * P, 1)))
         can = all(hasattr(engine, f) for f in ("fold_slots_keep", "fold_mark", "fold_rewind", "fold_unmark"))
-        self.speculate = bool(can and self.max_marks >= 2 and (speculate is None or speculate))
+        # opt-in (r04): under the reference's trigger -- the close right after the last report -- a
+        # certain-only close was faster (profiles/r04b: 2.09 vs 3.7-4.0 ms with the peek, 2.5 without)
+        self.speculate = bool(can and self.max_marks >= 2 and speculate)
         self.mark_every = max(1, int(mark_every))
         # speculative folds wait while the GPU is still busy with the previous one (reports arriving
         # back to back would otherwise queue re-folds that the next report discards)

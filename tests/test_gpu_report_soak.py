@@ -37,7 +37,7 @@ def test_random_bursts_pauses_and_rereports_stay_bit_exact(mode, devices):
     stats = {"peeked": 0, "rewinds": 0, "refold": 0}
     with (Engine(devices=devices) if devices else Engine(0)) as eng:
         for cyc in range(5):
-            inc = IncrementalCycle(eng, numel, mode=mode, slots=n + 2, checkpoint=ck,
+            inc = IncrementalCycle(eng, numel, mode=mode, slots=n + 2, checkpoint=ck, speculate=True,
                                    weights_by_worker=weights if mode == 2 else None)
             for w in range(n):
                 inc.assigned(w)

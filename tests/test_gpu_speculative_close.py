@@ -44,7 +44,7 @@ def test_committed_peek_is_bit_exact_and_chains(devices, mode):
         for cyc in range(3):
             diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES] for w in range(12)}
             reporters = [w for w in range(12) if w % 4 != 1]
-            inc = IncrementalCycle(eng, numel, mode=mode, slots=16, checkpoint=ck, lazy=False,
+            inc = IncrementalCycle(eng, numel, speculate=True, mode=mode, slots=16, checkpoint=ck, lazy=False,
                                    weights_by_worker=weights if mode == 2 else None)
             for w in range(12):
                 inc.assigned(w)
@@ -72,7 +72,7 @@ def test_stale_peek_falls_back_bit_exact(case):
     ck = build_state_fast(ckpt)
     diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES] for w in range(8)}
     with Engine(0) as eng:
-        inc = IncrementalCycle(eng, numel, slots=10, checkpoint=ck, lazy=False, peek=case != "no_peek")
+        inc = IncrementalCycle(eng, numel, speculate=True, slots=10, checkpoint=ck, lazy=False, peek=case != "no_peek")
         for w in range(8):
             inc.assigned(w)
         for w in (5, 2, 0, 3):
@@ -111,7 +111,7 @@ def test_abandoned_cycle_peek_copy_finishes_before_the_next_peek():
     with Engine(0) as eng:
         for cyc in range(3):
             diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in range(4)}
-            inc = IncrementalCycle(eng, numel, slots=6, checkpoint=ck, lazy=False)
+            inc = IncrementalCycle(eng, numel, speculate=True, slots=6, checkpoint=ck, lazy=False)
             for w in range(4):
                 inc.assigned(w)
             for w in (2, 0, 3, 1):
@@ -142,7 +142,7 @@ def test_peek_into_another_output_while_a_copy_runs():
     ck = build_state_fast(ckpt)
     diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in range(3)}
     with Engine(0) as eng:
-        inc = IncrementalCycle(eng, numel, slots=5, checkpoint=ck, lazy=False)
+        inc = IncrementalCycle(eng, numel, speculate=True, slots=5, checkpoint=ck, lazy=False)
         for w in range(3):
             inc.assigned(w)
         for w in (1, 2, 0):
@@ -174,7 +174,7 @@ def test_burst_then_pause_is_folded_and_peeked_by_the_timer(mode, devices):
     diffs = {w: build_state_fast([(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES]) for w in range(10)}
     reporters = [w for w in range(10) if w != 4]
     with (Engine(devices=devices) if devices else Engine(0)) as eng:
-        inc = IncrementalCycle(eng, numel, mode=mode, slots=12, checkpoint=ck, min_gap_ms=50.0,
+        inc = IncrementalCycle(eng, numel, speculate=True, mode=mode, slots=12, checkpoint=ck, min_gap_ms=50.0,
                                weights_by_worker=weights if mode == 2 else None)
         for w in range(10):
             inc.assigned(w)
@@ -248,7 +248,7 @@ def test_peek_valid_tracks_the_fold_state(devices):
     ck = build_state_fast(ckpt)
     diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES] for w in range(4)}
     with (Engine(0) if devices is None else Engine(devices=devices)) as eng:
-        inc = IncrementalCycle(eng, numel, slots=6, checkpoint=ck, lazy=False)
+        inc = IncrementalCycle(eng, numel, speculate=True, slots=6, checkpoint=ck, lazy=False)
         for w in range(4):
             inc.assigned(w)
         inc.reported(0, build_state_fast(diffs[0]))  # folded and peeked at once

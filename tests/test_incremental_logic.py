@@ -552,7 +552,7 @@ def test_speculation_folds_every_report_and_closes_with_nothing_left():
     rng = np.random.default_rng(11)
     eng = SpecEngine()
     n = 40
-    inc = IncrementalCycle(eng, [3], slots=n, fold_batch=8)
+    inc = IncrementalCycle(eng, [3], speculate=True, slots=n, fold_batch=8)
     assert inc.speculate
     for w in range(n):
         inc.assigned(w)
@@ -571,7 +571,7 @@ def test_speculation_folds_every_report_and_closes_with_nothing_left():
 
 def test_speculation_frees_certain_slots_and_rewinds_only_after_the_base():
     eng = SpecEngine()
-    inc = IncrementalCycle(eng, [3], slots=6)
+    inc = IncrementalCycle(eng, [3], speculate=True, slots=6)
     for w in "abcdefgh":
         inc.assigned(w)
     for w in "abd":            # a, b certain; d speculative (c outstanding)
@@ -589,7 +589,7 @@ def test_speculation_frees_certain_slots_and_rewinds_only_after_the_base():
 
 def test_speculative_re_report_rewinds_and_folds_the_latest_diff():
     eng = SpecEngine()
-    inc = IncrementalCycle(eng, [3], slots=8)
+    inc = IncrementalCycle(eng, [3], speculate=True, slots=8)
     for w in range(6):
         inc.assigned(w)
     for w, v in ((2, b"2a"), (4, b"4a"), (3, b"3a"), (4, b"4b"), (2, b"2b")):
@@ -604,7 +604,7 @@ def test_close_rewinds_to_the_db_order():
     """The DB returns another order than assignment: the close goes back to the last saved state
     inside the common prefix and folds the rest from the kept slots -- no DB reads."""
     eng = SpecEngine()
-    inc = IncrementalCycle(eng, [3], slots=8, mark_every=1)
+    inc = IncrementalCycle(eng, [3], speculate=True, slots=8, mark_every=1)
     for w in range(6):
         inc.assigned(w)
     for w in (5, 1, 2, 4):
@@ -619,7 +619,7 @@ def test_mark_budget_thins_saved_states():
     rng = np.random.default_rng(12)
     eng = SpecEngine()
     n = 60
-    inc = IncrementalCycle(eng, [1000], slots=n, speculation_budget=5 * 4000)
+    inc = IncrementalCycle(eng, [1000], speculate=True, slots=n, speculation_budget=5 * 4000)
     assert inc.max_marks == 5
     for w in range(n):
         inc.assigned(w)
@@ -632,7 +632,9 @@ def test_mark_budget_thins_saved_states():
 
 
 def test_no_speculation_without_budget():
-    assert not IncrementalCycle(SpecEngine(), [1000], slots=4, speculation_budget=4000).speculate
+    with pytest.raises(AggregationError):  # room for one saved state only
+        IncrementalCycle(SpecEngine(), [1000], slots=4, speculation_budget=4000, speculate=True)
+    assert not IncrementalCycle(SpecEngine(), [10], slots=4).speculate  # opt-in (r04)
     assert not IncrementalCycle(SpecEngine(), [10], slots=4, speculate=False).speculate
     with pytest.raises(AggregationError):
         IncrementalCycle(RecordingEngine(), [10], slots=4, speculate=True)
@@ -648,7 +650,7 @@ def test_randomised_speculation_matches_the_reference_order(seed):
     n = int(rng.integers(3, 30))
     slots = int(rng.integers(2, n + 3))
     eng = SpecEngine(fail_on=b"bad")
-    inc = IncrementalCycle(eng, [3], slots=slots, fold_batch=int(rng.integers(1, 4)),
+    inc = IncrementalCycle(eng, [3], speculate=True, slots=slots, fold_batch=int(rng.integers(1, 4)),
                            speculation_budget=int(rng.integers(2, 12)) * 12)
     late = set(int(x) for x in rng.choice(n, size=int(rng.integers(0, n // 3 + 1)), replace=False))
     for w in range(n):
@@ -694,7 +696,7 @@ def test_speculation_under_slot_pressure_closes_without_the_db(slots, seed):
     rng = np.random.default_rng(50 + seed)
     eng = SpecEngine()
     n = 24
-    inc = IncrementalCycle(eng, [3], slots=slots, fold_batch=2, mark_every=3)
+    inc = IncrementalCycle(eng, [3], speculate=True, slots=slots, fold_batch=2, mark_every=3)
     for w in range(n):
         inc.assigned(w)
     reporters = [w for w in range(n) if w % 5 != 3]
@@ -726,7 +728,7 @@ def test_lazy_speculation_waits_for_slow_reports_and_an_idle_gpu(monkeypatch, ga
     monkeypatch.setattr(inc_mod.time, "monotonic", lambda: clock[0])
     eng = BusySpecEngine()
     eng.busy = busy
-    inc = IncrementalCycle(eng, [3], slots=16)
+    inc = IncrementalCycle(eng, [3], speculate=True, slots=16)
     assert inc.speculate and inc._lazy
     for w in range(8):
         inc.assigned(w)
@@ -749,7 +751,7 @@ def test_out_of_hbm_for_saved_states_degrades_not_fails():
 
     rng = np.random.default_rng(77)
     eng = TightEngine()
-    inc = IncrementalCycle(eng, [3], slots=40, mark_every=2)
+    inc = IncrementalCycle(eng, [3], speculate=True, slots=40, mark_every=2)
     for w in range(40):
         inc.assigned(w)
     reporters = [w for w in range(1, 40) if rng.random() >= 0.2]
@@ -772,7 +774,7 @@ def test_lazy_skips_are_folded_by_a_timer_once_reports_pause(monkeypatch):
     monkeypatch.setattr(inc_mod.time, "monotonic", lambda: clock[0])
     eng = BusySpecEngine()
     eng.busy = True
-    inc = IncrementalCycle(eng, [3], slots=16, min_gap_ms=2.0)
+    inc = IncrementalCycle(eng, [3], speculate=True, slots=16, min_gap_ms=2.0)
     for w in range(8):
         inc.assigned(w)
     for w in (3, 1, 0, 6, 2, 5, 7, 4):
@@ -821,7 +823,7 @@ def test_concurrent_reports_and_timer_folds_never_overlap_engine_calls(seed):
     eng = GuardedEngine()
     object.__setattr__(eng, "_guard", threading.Lock())
     n = 40
-    inc = IncrementalCycle(eng, [3], slots=48, min_gap_ms=1.0, mark_every=4)
+    inc = IncrementalCycle(eng, [3], speculate=True, slots=48, min_gap_ms=1.0, mark_every=4)
     for w in range(n):
         inc.assigned(w)
     reporters = [w for w in range(n) if rng.random() >= 0.2]
@@ -863,13 +865,13 @@ def test_a_dropped_open_cycle_is_abandoned_by_the_next_one(monkeypatch):
 
     eng = BusySpecEngine()
     eng.busy = True
-    a = IncrementalCycle(eng, [3], slots=8, min_gap_ms=1.0)
+    a = IncrementalCycle(eng, [3], speculate=True, slots=8, min_gap_ms=1.0)
     for w in range(4):
         a.assigned(w)
     for w in (2, 1, 3):
         a.reported(w, mk(w))
     assert a._timer is not None
-    b = IncrementalCycle(eng, [3], slots=8, min_gap_ms=1.0)
+    b = IncrementalCycle(eng, [3], speculate=True, slots=8, min_gap_ms=1.0)
     assert a._closed and a._timer is None
     eng.busy = False
     for w in range(3):
@@ -881,5 +883,5 @@ def test_a_dropped_open_cycle_is_abandoned_by_the_next_one(monkeypatch):
     assert eng.result == [mk(10), mk(11), mk(12)]
     with pytest.raises(AggregationError):
         a.close(b"ck", framing="template")
-    c = IncrementalCycle(eng, [3], slots=8)  # b was closed: abandoning it is a no-op
+    c = IncrementalCycle(eng, [3], speculate=True, slots=8)  # b was closed: abandoning it is a no-op
     assert eng.cycle_owner is c and b.last_close
