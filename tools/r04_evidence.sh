@@ -20,3 +20,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 200 rocprofv3 --pmc $c -d $OUT/rp/pmc_$c -o run --output-format csv -- python3 tools/prof_report_path.py run 1 40 > $OUT/rp_$c.log 2>&1 || { tail -5 $OUT/rp_$c.log; exit 1; }
 done
 echo "report-path profile ok"
+if [ "$3" = trace ]; then
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-config-lines > $OUT/bench_trace_default.json 2> $OUT/bench_trace_default.err || { tail -5 $OUT/bench_trace_default.err; exit 1; }
+  echo "default bench trace ok"
+fi
