@@ -250,6 +250,10 @@ struct pgh_ctx {
     // state_gen is unchanged -- every fold, rewind, restart, weight or checkpoint change bumps it.
     hipStream_t peek_stream = nullptr;
     hipEvent_t peek_ev = nullptr;
+    // the D2H runs in D2H_PIECE pieces, an event behind each: the peek thread copies a piece out as
+    // soon as it lands (the copy-out overlaps the rest of the D2H instead of following all of it)
+    std::vector<hipEvent_t> peek_piece_ev;
+    size_t peek_pieces = 0;    // pieces of the last peek's D2H
     float* h_peek = nullptr;   // pinned, peek_cap floats
     size_t peek_cap = 0;
     float* d_peek = nullptr;   // [pvec]: the peeked new checkpoint (swapped with d_ckpt on commit)
@@ -1483,6 +1487,7 @@ void pgh_destroy(pgh_ctx* c) {
     if (c->copy) (void)hipStreamDestroy(c->copy);
     if (c->aux) (void)hipStreamDestroy(c->aux);
     if (c->peek_ev) (void)hipEventDestroy(c->peek_ev);
+    for (auto e : c->peek_piece_ev) (void)hipEventDestroy(e);
     if (c->peek_stream) (void)hipStreamDestroy(c->peek_stream);
     delete c;
 }
@@ -2481,16 +2486,20 @@ void peek_thread_main(pgh_ctx* c) {
             pieces.swap(c->pk_pieces);
             gen = c->pk_gen;
         }
-        bool ok = hipEventSynchronize(c->peek_ev) == hipSuccess;
-        if (ok) {
-            std::vector<OutPiece> op;
-            size_t total = 0;
-            for (auto& pc : pieces) {
-                op.push_back(OutPiece{pc.first, pc.second});
-                total += pc.second;
-            }
-            scatter_out((const uint8_t*)c->h_peek, 0, total, op, *c->pool_peek);
+        // piece k of the D2H (D2H_PIECE bytes of h_peek) is copied out as soon as its event fires
+        std::vector<OutPiece> op;
+        size_t total = 0;
+        for (auto& pc : pieces) {
+            op.push_back(OutPiece{pc.first, pc.second});
+            total += pc.second;
         }
+        bool ok = true;
+        for (size_t k = 0; ok && k < c->peek_pieces && k * D2H_PIECE < total; ++k) {
+            ok = hipEventSynchronize(c->peek_piece_ev[k]) == hipSuccess;
+            const size_t off = k * D2H_PIECE, len = std::min(D2H_PIECE, total - off);
+            if (ok) scatter_out((const uint8_t*)c->h_peek + off, off, len, op, *c->pool_peek);
+        }
+        ok = ok && hipEventSynchronize(c->peek_ev) == hipSuccess;
         {
             std::lock_guard<std::mutex> lk(c->pk_mu);
             c->pk_done_gen = ok ? gen : 0;
@@ -2584,7 +2593,19 @@ int pgh_fold_peek(pgh_ctx* c, int mode) {
     RC(record_fold(c, s));  // a checkpoint upload waits for this read of d_ckpt
     CK(c, hipEventRecord(c->peek_ev, s));
     CK(c, hipStreamWaitEvent(c->peek_stream, c->peek_ev, 0));
-    CK(c, hipMemcpyAsync(c->h_peek, c->d_peek, (size_t)c->pg * 4, hipMemcpyDeviceToHost, c->peek_stream));
+    const size_t total = (size_t)c->pg * 4, np = (total + D2H_PIECE - 1) / D2H_PIECE;
+    while (c->peek_piece_ev.size() < np) {
+        hipEvent_t e = nullptr;
+        CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->peek_piece_ev.push_back(e);
+    }
+    for (size_t k = 0; k < np; ++k) {
+        const size_t off = k * D2H_PIECE, len = std::min(D2H_PIECE, total - off);
+        CK(c, hipMemcpyAsync((uint8_t*)c->h_peek + off, (const uint8_t*)c->d_peek + off, len, hipMemcpyDeviceToHost,
+                             c->peek_stream));
+        CK(c, hipEventRecord(c->peek_piece_ev[k], c->peek_stream));
+    }
+    c->peek_pieces = np;
     CK(c, hipEventRecord(c->peek_ev, c->peek_stream));
     c->peek_gen = c->state_gen;
     return PGH_OK;
@@ -2604,7 +2625,8 @@ int pgh_fold_peek_into(pgh_ctx* c, int mode, uint8_t* out, size_t n) {
     }
     RC(pgh_fold_peek(c, mode));
     if (!out || !pgh_int::peek_valid(c)) return PGH_OK;  // skipped: nothing to copy
-    if (!c->pool_peek) c->pool_peek.reset(new CopyPool(4, c->local_cpus));
+    // 8 threads: a piece's copy-out keeps pace with its PCIe D2H (4 were slower than the link)
+    if (!c->pool_peek) c->pool_peek.reset(new CopyPool(std::min(8, std::max(1, c->copy_threads)), c->local_cpus));
     if (!c->pk_thread.joinable()) c->pk_thread = std::thread(peek_thread_main, c);
     {
         std::lock_guard<std::mutex> lk(c->pk_mu);
