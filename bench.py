@@ -1306,7 +1306,7 @@ def report_close(ctx, args, eng, cycles: int = 4, assigned: int = 100):
     arms = {}
     # (arm, IncrementalCycle options): the product default first, then the alternatives
     kinds = (("default", {}), ("speculative_peek", {"speculate": True, "peek": True}),
-             ("speculative_no_peek", {"speculate": True, "peek": False}), ("certain_only", {"speculate": False}))
+             ("speculative_no_peek", {"speculate": True, "peek": False}))
     with ThreadPoolExecutor(1, thread_name_prefix="executor") as executor:
         for arrival, gap_ms in (("paced", 5.0), ("back_to_back", 0.0)):
             for kind, opts in kinds:
