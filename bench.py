@@ -1286,9 +1286,9 @@ def report_close(ctx, args, eng, cycles: int = 4, assigned: int = 100):
     ``reported`` returning to the new checkpoint bytes ready on the executor thread -- nothing
     waits between the two, nothing syncs the GPU before the clock starts.  Two arrival patterns
     (reports `paced` 5 ms apart -- a node handles each report for tens of ms anyway, its DB write
-    included, tools/node_sim.py -- and `back_to_back`) x the product default and the alternatives
-    (speculative folds with / without the peeked close, certain-only folds); the headline is the
-    product default, paced.  1 warm-up cycle each."""
+    included, tools/node_sim.py -- and `back_to_back`) x the product default (certain-only folds
+    since r04) and the opt-in alternatives (speculative folds with / without the peeked close); the
+    headline is the product default, paced.  1 warm-up cycle each."""
     from concurrent.futures import ThreadPoolExecutor
 
     import numpy as np
