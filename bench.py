@@ -325,6 +325,46 @@ def attach_config_lines(args, rec: dict):
             rec[key] = config_line(args, wl)
 
 
+def pre_world_lines(args) -> dict:
+    """The child lines of this run -- the one-process group and the config-4 / config-5 worlds over
+    the same GPUs -- run BEFORE this process, or any rank of its world, touches a GPU: a parent
+    holding a HIP context while its child runs slowed the child's config-4 step by 13 % (176 vs
+    154 ms, profiles/r04g/).  Under torch.distributed.run rank 0 runs them while the other ranks
+    wait on the launcher's store (no GPU touched); at N = 1 this process runs them first.  Ranks
+    this script spawned leave them to their parent (spawn_ranks), which never touches a GPU."""
+    out = {}
+    spawned = os.environ.get("PGH_BENCH_SPAWNED") == "1"
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if spawned or args.group or not (wants_group_line(args) or wants_config_lines(args)):
+        return out
+    rank = int(os.environ.get("RANK", "0"))
+
+    def run():
+        if wants_group_line(args):
+            out["group"] = group_line(args)
+        attach_config_lines(args, out)
+
+    if world == 1:
+        run()
+        return out
+    # torch.distributed.run: a barrier on the launcher's own store, before any process group exists
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), is_master=False,
+                          timeout=timedelta(seconds=1800))
+    key = f"pgh_bench_pre_world_{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}"
+    if rank == 0:
+        try:
+            run()
+        finally:
+            store.set(key, "done")
+    else:
+        store.wait([key])
+    return out
+
+
 def check_sampled(ctx, args, full, lo: int, hi: int, expected) -> dict:
     """``--check``: a checker leg outside the timed region (like cpu_baseline, the only other place
     this script runs the oracle).  Every rank samples global param indices of its own shard [lo, hi)
@@ -1467,6 +1507,7 @@ def main():
         # queues were requested at import); cpu_baseline children run with glibc's defaults
         PROCESS_TUNING.update(pygrid_amd.tune_process(hw_queues=False))
         PROCESS_TUNING["hw_queues"] = HW_QUEUES
+    pre = pre_world_lines(args)  # child lines first: nothing of this world holds a GPU yet
     global LIVE_TRAFFIC
     if (args.gpus == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.group and not args.dry_run
             and not args.no_live_traffic and args.workload in PMC_KERNEL and not under_profiler()):
@@ -1478,10 +1519,7 @@ def main():
                "check": args.check}
         ctx.close()
         if ctx.rank == 0:
-            if launched_elsewhere() and wants_group_line(args):
-                rec["group"] = group_line(args)
-            if ctx.world == 1 or launched_elsewhere():
-                attach_config_lines(args, rec)
+            rec.update(pre)
             print(json.dumps(rec), flush=True)
         return
     if ctx.group:
@@ -1528,10 +1566,7 @@ def main():
         ctx.barrier()  # every rank's slab is freed before the group child allocates on all GPUs
     ctx.close()
     if ctx.rank == 0:
-        if launched_elsewhere() and wants_group_line(args):
-            rec["group"] = group_line(args)  # a fresh child: this process never re-execs
-        if ctx.world == 1 or launched_elsewhere():
-            attach_config_lines(args, rec)  # fresh child worlds over the same GPUs
+        rec.update(pre)  # measured before this world touched a GPU (pre_world_lines)
         print(json.dumps(rec), flush=True)
 
 
