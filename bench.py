@@ -347,6 +347,12 @@ def pre_world_lines(args) -> dict:
     if world == 1:
         run()
         return out
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() != "true":
+        # another launcher: no store to wait on before the process group forms; rank 0 runs them
+        # first and the others wait in init_process_group (their GPUs touched: no deadlock risk)
+        if rank == 0:
+            run()
+        return out
     # torch.distributed.run: a barrier on the launcher's own store, before any process group exists
     from datetime import timedelta
 
