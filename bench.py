@@ -373,15 +373,18 @@ def pre_world_lines(args) -> dict:
 
 def check_sampled(ctx, args, full, lo: int, hi: int, expected) -> dict:
     """``--check``: a checker leg outside the timed region (like cpu_baseline, the only other place
-    this script runs the oracle).  Every rank samples global param indices of its own shard [lo, hi)
-    (both edges included) and computes the oracle's new-checkpoint values for them from its own
+    this script runs the oracle).  Every rank takes its share of a strided 4,096-param sample of
+    its own shard [lo, hi) (both edges included) and computes the oracle's values for them from its own
     inputs (``expected(idx)``); rank 0 gathers them and compares ``full`` -- the all-gathered new
     checkpoint, or the one shard at N = 1 -- at every rank's indices, bit for bit."""
     import numpy as np
 
     torch = ctx.torch
-    rng = np.random.default_rng(args.seed + 7919 * ctx.rank)
-    idx = np.unique(np.concatenate([[lo, hi - 1], rng.integers(lo, hi, 62)])).astype(np.int64)
+    # a strided sample of 4,096 params over the whole model (SURVEY 8(d): config 4's golden check),
+    # this rank's share of it, plus its shard's edges
+    k = max(1, -(-4096 // ctx.world))
+    idx = np.unique(np.concatenate([[lo, hi - 1], lo + (np.arange(k, dtype=np.int64) * (hi - lo)) // k]))
+    idx = idx[(idx >= lo) & (idx < hi)].astype(np.int64)
     want = np.ascontiguousarray(expected(idx), np.float32)
     mine = (idx.tolist(), want.view(np.uint32).tolist())
     if ctx.world > 1:
