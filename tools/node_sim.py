@@ -104,6 +104,12 @@ def run_arm(eng, cycles, gap_ms, opts, pinned, db, rng, ckpt, texts, framing="fr
     timer = Timer()
     timer.wrap(ref_fl_events.base64, "b64decode", "decode")
     timer.wrap(node, "on_report", "ingest")
+    # the close's phases on the executor thread (its own bucket): the whole _average_plan_diffs,
+    # the checkpoint save (the node's DB write), preparing the next cycle's report-time state
+    timer.wrap(node, "average_plan_diffs", "close_average_plan_diffs")
+    timer.wrap(mod.model_manager, "save", "close_save")
+    timer.wrap(node, "on_cycle_created", "close_next_cycle_prepare")
+    timer.wrap(mod.cycle_manager, "complete_cycle", "close_complete_cycle")
     finish = incremental.IncrementalCycle.finish
     engine_close = []
 
@@ -121,6 +127,7 @@ def run_arm(eng, cycles, gap_ms, opts, pinned, db, rng, ckpt, texts, framing="fr
         cfg = {"min_diffs": REPORTERS, "max_diffs": REPORTERS, "num_cycles": 0}
         proc, _, _ = host_process(mod, cfg, ckpt)
         handler, encode, decode, write, ingest, closes, engine_share = [], [], [], [], [], [], []
+        phases = []
         for cyc in range(cycles + 1):  # cycle 0 warms up
             keys = {w: assign(mod, f"w{w}", proc) for w in range(ASSIGNED)}
             reporters = [w for w in rng.permutation(ASSIGNED) if w != 0][:REPORTERS]
@@ -149,6 +156,9 @@ def run_arm(eng, cycles, gap_ms, opts, pinned, db, rng, ckpt, texts, framing="fr
                     write.append(total - enc - b.get("decode", 0.0) - b.get("ingest", 0.0))
             fut = ex.futures["complete_cycle"]
             fut.result(120)
+            if cyc:
+                phases.append(ex.pool.submit(lambda: dict(timer.bucket())).result())
+            ex.pool.submit(lambda: timer.bucket().clear()).result()
             if mod.cycle_manager.task_errors:
                 raise SystemExit(f"close failed: {mod.cycle_manager.task_errors!r}")
             t2 = time.perf_counter()
@@ -173,6 +183,7 @@ def run_arm(eng, cycles, gap_ms, opts, pinned, db, rng, ckpt, texts, framing="fr
             "close_ms": pct(closes, 50), "closes_ms": [round(c, 3) for c in closes],
             "engine_close_ms": pct([e for e in engine_share if e is not None], 50),
             "engine_closes": close_info[1:],
+            "close_phases_ms": [{k: round(v, 3) for k, v in p.items()} for p in phases],
             "node_stats": stats, "pinned_pool": pools}
 
 
