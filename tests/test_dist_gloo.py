@@ -197,3 +197,49 @@ def test_plan_ranges_partition(length, chunks, unit, tail):
     assert all(b > a and a % unit == 0 for a, b in r)
     assert all(b == a2 for (_, b), (a2, _) in zip(r, r[1:]))
     assert len(r) <= chunks + tail
+
+
+def _check_worker(rank, world, port, P, corrupt, q):
+    """bench.check_sampled at world > 1: every rank samples its shard and computes the expected
+    values from its own 'inputs'; rank 0 compares the all-gathered vector."""
+    import sys
+    import types
+
+    from conftest import ROOT
+
+    sys.path.insert(0, str(ROOT))
+    sys.argv = ["bench.py"]
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard_bounds(P, world, rank)
+        part = (torch.arange(lo, hi, dtype=torch.float32) * 0.25)
+        if corrupt and rank == world - 1 and hi > lo:
+            part[-1] = torch.nextafter(part[-1], torch.tensor(1e9))  # one ulp off at the last shard's edge
+        full = gather_flat(part, P, world, rank)
+        ctx = types.SimpleNamespace(torch=torch, world=world, rank=rank, dist=dist)
+        got = bench.check_sampled(ctx, types.SimpleNamespace(seed=5), full, lo, hi,
+                                  lambda idx: idx.astype(np.float32) * np.float32(0.25))
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_bench_check_leg_over_two_ranks(corrupt):
+    P, world = 10_001, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_check_worker, args=(r, world, port, P, corrupt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+    assert res[1] is None  # only rank 0 reports
+    r0 = res[0]
+    assert r0["ranks"] == 2 and r0["params_checked"] >= 4096
+    assert r0["bit_exact"] is (not corrupt) and r0["mismatches"] == int(corrupt)
