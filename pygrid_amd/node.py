@@ -364,7 +364,6 @@ class NodeEngine:
                 model = self.model_manager.get(fl_process_id=cycle.fl_process_id)
                 ckpt = self.model_manager.load(model_id=model.id)
             self._gate.acquire_exclusive()  # no report is between its DB write and its ingest now
-            gated = True
             try:
                 with self._lock:
                     st = self._cycles.pop(cycle.id, None)
@@ -372,14 +371,18 @@ class NodeEngine:
                         self._owner = None
                     if not isinstance(st, IncrementalCycle) and st != _DECLINED:
                         self._abandon_others()  # the close-time path re-lays the engine's slab
-                if not isinstance(st, IncrementalCycle):
-                    self._gate.release_exclusive()  # the close-time path takes it for its query
-                    gated = False
-                    if st == _DECLINED:
-                        self.stats["closes_declined"] += 1
-                        return original(cm, server_config, cycle)
-                    self.stats["closes_close_time"] += 1
-                    return close_time(cm, server_config, cycle)
+            except BaseException:
+                self._gate.release_exclusive()
+                raise
+            if not isinstance(st, IncrementalCycle):
+                self._gate.release_exclusive()  # the close-time path takes it for its own query
+                if st == _DECLINED:
+                    self.stats["closes_declined"] += 1
+                    return original(cm, server_config, cycle)
+                self.stats["closes_close_time"] += 1
+                return close_time(cm, server_config, cycle)
+            gated, fallback = True, None
+            try:
                 if ckpt is None:
                     model = self.model_manager.get(fl_process_id=cycle.fl_process_id)
                     ckpt = self.model_manager.load(model_id=model.id)
@@ -391,23 +394,22 @@ class NodeEngine:
                 new = st.finish(ckpt.value, framing=self.framing, fetch=lambda rid: by_id[rid].diff)
             except PlanNotAcceleratedError as e:  # incl. ModelNotAcceleratedError: a non-float32 diff
                 log.info("engine declined cycle %s (%s): running the reference averaging", cycle.id, e)
-                self.stats["closes_declined"] += 1
-                if gated:
-                    self._gate.release_exclusive()
-                    gated = False
-                return original(cm, server_config, cycle)
+                fallback = "original"
             except AggregationError as e:
                 log.warning("report-time close of cycle %s failed (%s): close-time path over the DB rows",
                             cycle.id, e)
-                self.aggregator._resident = None
-                self.stats["closes_close_time"] += 1
-                if gated:
-                    self._gate.release_exclusive()
-                    gated = False
-                return close_time(cm, server_config, cycle)
+                fallback = "close_time"
             finally:
                 if gated:
                     self._gate.release_exclusive()
+            # the fallbacks run outside the try: their own errors reach complete_cycle's log, once
+            if fallback == "original":
+                self.stats["closes_declined"] += 1
+                return original(cm, server_config, cycle)
+            if fallback == "close_time":
+                self.aggregator._resident = None
+                self.stats["closes_close_time"] += 1
+                return close_time(cm, server_config, cycle)
             self.stats["closes_report_time"] += 1
             self.stats["refolds"] += int(st.last_close.get("refold", False))
             self.stats["diffs_from_db"] += st.last_close.get("from_db", 0)

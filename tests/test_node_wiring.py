@@ -315,3 +315,31 @@ def test_uninstall_restores_the_node():
     n.uninstall()
     assert dict(vars(mod.CycleManager)) == before[0] and mod.run_task_once is before[1]
     assert vars(mod.model_manager) == before[2]
+
+
+def test_a_failing_close_time_fallback_runs_once():
+    """The report-time close fails (AggregationError) -> the close-time path over the DB rows; when
+    that fails too, its error reaches complete_cycle's log once -- it is not retried by the close's
+    own error handling."""
+    from pygrid_amd.exceptions import AggregationError
+    from pygrid_amd.incremental import IncrementalCycle
+
+    sc = Scenario(CFG3, True)
+    calls = []
+
+    def failing(*a, **k):
+        calls.append(1)
+        raise AggregationError("engine failure (test)")
+    sc.node.aggregator.average_plan_diffs = failing
+    orig_finish = IncrementalCycle.finish
+    IncrementalCycle.finish = lambda self, *a, **k: (_ for _ in ()).throw(AggregationError("finish failed (test)"))
+    try:
+        for w in range(3):
+            sc.assign(w)
+        for w in range(3):
+            sc.report(w)
+    finally:
+        IncrementalCycle.finish = orig_finish
+    assert len(calls) == 1
+    assert len(sc.cm.task_errors) == 1 and "engine failure" in str(sc.cm.task_errors[0])
+    sc.node.uninstall()
