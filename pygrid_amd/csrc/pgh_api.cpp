@@ -361,10 +361,6 @@ struct pgh_ctx {
     // launch costs its drain (ResNet-18 fold 7.45 ms as 4 ranges on two streams vs 6.91 ms as one,
     // r02r), about what the earlier D2H start saves in a close (report closes within noise, r02l/r02r).
     int final_split = 1;
-    // PGH_SLOT_FINAL_RANGES: the same split for the FINAL pass of a report-time close (a slot fold
-    // of the rows left at close: short, so its D2H would otherwise wait for all of it) -- on by
-    // default: 1.98 -> 1.41 ms close after a back-to-back burst at 8 ranges (profiles/r03ah/)
-    int slot_final_split = 8;
     int64_t client_base = 0;  // synthetic client k is generated as global client client_base + k
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
@@ -785,10 +781,6 @@ int join_aux(pgh_ctx* c, hipStream_t s) {
 
 // Ranges of a FINAL fold pass: 1, or final_split 4-aligned ranges of the shard.
 int final_ranges(const pgh_ctx* c) { return c->final_split > 1 && c->pg >= (1 << 20) ? c->final_split : 1; }
-int slot_final_ranges(const pgh_ctx* c) {
-    const int k = c->final_split > 1 ? c->final_split : c->slot_final_split;  // PGH_FINAL_RANGES wins
-    return k > 1 && c->pg >= (1 << 20) ? k : 1;
-}
 int64_t range_edge(const pgh_ctx* c, int k, int K) { return k >= K ? c->pg : (c->pg * k / K) & ~(int64_t)3; }
 
 // HBM -> host results move in pieces of at most D2H_PIECE, the DMA of piece i + 1 beside the host
@@ -1388,7 +1380,6 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_PINNED_GATHER")) c->pinned_gather = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_BLOCK_BYTES")) c->block_bytes = (size_t)std::max(0LL, std::atoll(e));
     if (const char* e = std::getenv("PGH_FINAL_RANGES")) c->final_split = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("PGH_SLOT_FINAL_RANGES")) c->slot_final_split = std::max(1, std::atoi(e));
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming) == hipSuccess &&
@@ -2317,13 +2308,17 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final, boo
         a.flags = (first ? pgh::FL_FIRST : 0) | (final && last ? pgh::FL_FINAL : 0);
         a.mode = mode;
         a.variant = c->variant;
-        // the FINAL pass as K param ranges, each followed by its mark (pipelined close)
-        const int K = (a.flags & pgh::FL_FINAL) ? slot_final_ranges(c) : 1;
+        // The FINAL pass of a report-time close (a short fold of the rows left) as ranges of 4 MiB of
+        // output, one after another on one stream, each followed by its mark: the D2H pieces (8 MiB)
+        // start behind the first two instead of behind the whole fold.  Ranges aligned to the pieces on
+        // one stream closed 0.1-0.15 ms sooner than 8 equal ranges alternating over two streams
+        // (profiles/r04m/: 2.04 vs 2.19 ms, close start -> new checkpoint bytes).
+        const int64_t RF = (int64_t)(D2H_PIECE / 8);
+        const int K = (a.flags & pgh::FL_FINAL) && c->pg >= (1 << 20) ? (int)((c->pg + RF - 1) / RF) : 1;
         if (a.flags & pgh::FL_FINAL) clear_final_marks(c);
-        if (K > 1) RC(fork_aux(c, s));
         for (int r = 0; r < K; ++r) {
-            const hipStream_t rs = K > 1 ? range_stream(c, s, r) : s;
-            const int64_t lo = K == 1 ? 0 : range_edge(c, r, K), hi = K == 1 ? c->pg : range_edge(c, r + 1, K);
+            const hipStream_t rs = s;
+            const int64_t lo = std::min(c->pg, RF * r), hi = K == 1 ? c->pg : std::min(c->pg, RF * (r + 1));
             pgh::FedavgArgs ar = a;
             ar.map.off = lo;
             ar.p = hi - lo;
@@ -2336,7 +2331,6 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final, boo
             RC(timed_launch(c, rs, bytes, [&] { return pgh::launch_fedavg_rows(ar, tab, rs); }));
             if (K > 1) RC(add_final_mark(c, rs, hi));
         }
-        if (K > 1) RC(join_aux(c, s));
         done += m;
     } while (done < n);
     RC(record_fold(c, s));

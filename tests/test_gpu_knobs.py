@@ -1,4 +1,4 @@
-"""GPU: every environment knob the library still reads, at a
+"""GPU: every environment knob the library still reads (environment knobs), at a
 non-default value, closes bit-exact against the oracle.  PGH_BLOCK_BYTES,
 PGH_FINAL_RANGES and PGH_PINNED_GATHER have their own tests (test_gpu_parity.py,
 test_gpu_pipelined_close.py, test_gpu_pinned_report.py).  The library reads the environment when
@@ -47,16 +47,15 @@ def test_close_time_knobs(monkeypatch, env):
             _check(CycleAggregator(eng).average_plan_diffs({}, ck_pb, d_pbs), O.fedavg_mean(ckpt, diffs))
 
 
-@pytest.mark.parametrize("ranges", ["1", "3"])
 @pytest.mark.parametrize("speculate", [False, True])
-def test_slot_final_ranges(monkeypatch, ranges, speculate):
-    """PGH_SLOT_FINAL_RANGES (default 8): the report-time close's FINAL pass as one launch, or as
-    3 ranges (not a divisor of anything here), with the D2H behind them."""
+def test_report_time_close_in_output_ranges(speculate):
+    """The report-time close's FINAL pass runs as ranges of 4 MiB of output on one stream, the D2H
+    pieces behind them (no knob since r04): a 1.1 M-param shard (two ranges, the second short)
+    closes bit-exact, with and without speculative folds."""
     from pygrid_amd import Engine
     from pygrid_amd.incremental import IncrementalCycle
 
-    monkeypatch.setenv("PGH_SLOT_FINAL_RANGES", ranges)
-    ckpt, diffs, ck_pb, d_pbs = _case(910 + int(ranges), n=6)
+    ckpt, diffs, ck_pb, d_pbs = _case(911, n=6)
     with Engine(0) as eng:
         inc = IncrementalCycle(eng, [int(np.prod(s)) for s in SHAPES], slots=8, checkpoint=ck_pb,
                                speculate=speculate, lazy=False)
