@@ -50,3 +50,25 @@ def test_installed_sql_node_with_pinned_reports_on_the_gpu(tmp_path, engine, spe
     # every report decoded into a page-locked block; every block freed once its views were gone
     assert pools == [(12, 0, 0), (2, 0, 0)], pools
     assert CFG["num_cycles"] == 3
+
+
+@pytest.mark.parametrize("speculate", [False, True], ids=["certain-only", "speculative"])
+def test_installed_sql_node_on_a_group(tmp_path, speculate):
+    """The same node on a one-process group of two children sharing GPU 0 (what a node with
+    several GPUs installs: ``install(devices=[...])``): each report's payload slices go to their
+    child, every child folds its shard, the close frames one checkpoint -- byte-identical to the
+    reference node; the page-locked blocks all come back."""
+    from pygrid_amd import Engine
+
+    with Engine(devices=[0, 0]) as grp:
+        def fresh_group():
+            grp.reset()
+            grp.ckpt_owner = None
+            return grp
+
+        eng = run_both(tmp_path, script_three_cycles, engine=fresh_group, ckpt=mnist_ckpt(), diff_fn=mnist_diff,
+                       pinned_reports=4, speculate=speculate)
+        st = eng.stats
+        assert st["closes_report_time"] == 3 and st["report_errors"] == 0, st
+    gc.collect()
+    assert [(p.hits, p.misses, p.blocks) for p in eng.pools] == [(12, 0, 0), (2, 0, 0)]
