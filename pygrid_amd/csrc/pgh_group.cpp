@@ -560,7 +560,7 @@ int pgh_group_allgather_resident(pgh_ctx* c, void** d_full_out) {
 
 }  // extern "C"
 
-// ---- the public entry points on a group context (dispatched from pgh_api.cpp) ---------------------
+// ---- the public entry points on a group context (dispatched from pgh_*.cpp) ---------------------
 
 namespace pgh_group_api {
 

@@ -1,5 +1,6 @@
-// Internal interface between the single-GPU context (pgh_api.cpp) and the multi-GPU group driver
-// (pgh_group.cpp).  Not installed; the public surface is include/pgh_api.h.
+// Internal interface between the single-GPU context (pgh_api.cpp, pgh_ingest.cpp, pgh_reduce.cpp,
+// pgh_slots.cpp) and the multi-GPU group driver (pgh_group.cpp).
+// Not installed; the public surface is include/pgh_api.h.
 //
 // A group context (pgh_create_group) is a pgh_ctx whose `grp` is set: every public entry point
 // hands it to pgh_group::* below, which drives one child pgh_ctx per GPU through the same public

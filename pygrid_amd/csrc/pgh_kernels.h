@@ -1,5 +1,6 @@
-// Internal launcher interface between the C-ABI context code (pgh_api.cpp) and the gfx950
-// kernels (pgh_kernels.hip).  Not installed; the public surface is include/pgh_api.h.
+// Internal launcher interface between the C-ABI context code (pgh_api.cpp, pgh_ingest.cpp,
+// pgh_reduce.cpp, pgh_slots.cpp) and the gfx950 kernels (pgh_kernels.hip).
+// Not installed; the public surface is include/pgh_api.h.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>

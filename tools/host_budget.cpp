@@ -4,7 +4,7 @@
 //   read     T threads sum a pageable buffer (host-DRAM read bandwidth)
 //   copy     T threads copy pageable -> pageable with non-temporal stores (DRAM read + write)
 //   stage    T threads copy pageable -> page-locked with non-temporal stores: the library's
-//            staging copy pool (pgh_api.cpp copy_stream) alone, no DMA
+//            staging copy pool (pgh_api.cpp copy_stream, CopyPool in pgh_ctx.h) alone, no DMA
 //   register hipHostRegister + hipHostUnregister of fresh pageable buffers of one diff's size
 //            (page-locking a message in place instead of copying it); register_parallel: T threads
 //   h2d      page-locked -> GPU 0 DMA (hipMemcpyAsync)
