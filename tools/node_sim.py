@@ -213,13 +213,20 @@ def main():
     arms = {}
     if "--cpu" in sys.argv:  # dev check of this tool on a GPU-less box: the tests' numpy engine
         from fake_engine import NumpyEngine
+    kinds = {"default": {}, "peek": {"speculate": True, "peek": True}, "spec": {"speculate": True, "peek": False},
+             "certain": {"speculate": False}}
+    framing = "template" if "--cpu" in sys.argv else "fresh"
     with (Engine(0) if "--cpu" not in sys.argv else _nullctx(NumpyEngine())) as eng:
+        # An untimed pass of the first arm: the process's first arm ran its report handlers at
+        # 74-81 ms p50 against 29-37 for every later arm, whatever the arm (the .encode() copy 12-14 ms
+        # instead of 2, the DB write 60 instead of 25: first-touch host memory, profiles/r04d, r04i,
+        # r04p), so each arm is measured in the same warm process.
+        pace, kind = want[0].split("_")
+        run_arm(eng, 1, gap if pace == "paced" else 0.0, kinds[kind], pinned, db, rng, ckpt, texts, framing=framing)
         for name in want:
             pace, kind = name.split("_")
-            opts = {"default": {}, "peek": {"speculate": True, "peek": True}, "spec": {"speculate": True, "peek": False},
-                    "certain": {"speculate": False}}[kind]
-            arms[name] = run_arm(eng, cycles, gap if pace == "paced" else 0.0, opts,
-                                 pinned, db, rng, ckpt, texts, framing="template" if "--cpu" in sys.argv else "fresh")
+            arms[name] = run_arm(eng, cycles, gap if pace == "paced" else 0.0, kinds[kind],
+                                 pinned, db, rng, ckpt, texts, framing=framing)
             print(f"# {name}: close {arms[name]['close_ms']} ms, handler p50 {arms[name]['report_handler_ms']['p50']} ms",
                   file=sys.stderr, flush=True)
     print(json.dumps({
@@ -228,6 +235,7 @@ def main():
                     "submit_worker_diff (SQLAlchemy LargeBinary write + commit) -> engine ingest; close by "
                     "run_task_once on an executor thread",
         "db": db, "pinned_reports": pinned, "cycles": cycles, "gap_ms": gap,
+        "warmup": f"one untimed cycle of {want[0]} first, then every arm's own untimed cycle 0",
         "close_definition": "last report handler returned -> new checkpoint committed + next cycle open "
                             "(complete_cycle on the executor thread)",
         "arms": arms}))
