@@ -27,6 +27,21 @@ def test_library_exports_every_declared_symbol():
     assert b"pgh_create_group" in (ROOT / "pygrid_amd" / "libpygrid_hip.so").read_bytes()
 
 
+def test_library_exports_no_undeclared_c_symbol():
+    """The only unmangled functions the library exports are the header's: internal helpers stay
+    internal (helpers in anonymous namespaces inside an ``extern "C"`` block used to be exported)."""
+    import shutil
+    import subprocess
+
+    if not shutil.which("nm"):
+        pytest.skip("nm not installed")
+    out = subprocess.run(["nm", "-D", "--defined-only", str(ROOT / "pygrid_amd" / "libpygrid_hip.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[2] for ln in out.splitlines() if len(ln.split()) == 3 and ln.split()[1] == "T"}
+    c_names = {s for s in exported if not s.startswith("_Z")}
+    assert c_names == set(declared_symbols()), sorted(c_names ^ set(declared_symbols()))
+
+
 def test_library_has_gfx950_code_object():
     data = (ROOT / "pygrid_amd" / "libpygrid_hip.so").read_bytes()
     assert b"amdgcn-amd-amdhsa--gfx950" in data
