@@ -50,6 +50,16 @@ def group3():
 
 
 @pytest.fixture(scope="module")
+def group8():
+    """The driver's 8-GPU node layout (eight param shards, eight children), here all on GPU 0."""
+    from pygrid_amd import Engine
+
+    eng = Engine(devices=[0] * 8)
+    yield eng
+    eng.close()
+
+
+@pytest.fixture(scope="module")
 def group1():
     from pygrid_amd import Engine
 
@@ -317,12 +327,22 @@ def test_group_random_cycles(group2, group3, seed):
     """Randomized chained cycles on 2- and 3-child groups: model sizes from 1 param (one active
     child) to off-grid shards, close-time State closes and report-time cycles alternating, every
     mode, each cycle's output feeding the next -- bit-exact against the oracle."""
+    _random_cycles(group2 if seed % 2 else group3, 7000 + seed)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_group8_random_cycles(group8, seed):
+    """The same randomized chained cycles on an eight-child group (the 8-GPU node's shard count):
+    models smaller than eight params leave children without a shard."""
+    _random_cycles(group8, 7100 + seed)
+
+
+def _random_cycles(eng, seed):
     from pygrid_amd.cycle import CycleAggregator
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast, parse_state
 
-    rng = np.random.default_rng(7000 + seed)
-    eng = group2 if seed % 2 else group3
+    rng = np.random.default_rng(seed)
     P = int(rng.choice([1, 5, 64, 65, 129, 191, 4_099, 70_001, 262_147]))
     cut = sorted(int(x) for x in rng.choice(np.arange(1, P), size=min(2, P - 1), replace=False)) if P > 2 else []
     numel = [b - a for a, b in zip([0] + cut, cut + [P])]
@@ -359,3 +379,78 @@ def test_group_random_cycles(group2, group3, seed):
         for g, w in zip(got, want):
             assert np.array_equal(bits(g), bits(w))
         ckpt = [np.asarray(g, F).reshape(-1) for g in got]
+
+
+# ---- eight children: the 8-GPU node's layout on one device -------------------------------------------
+
+def test_group8_shape_and_peer_allgather(group8):
+    assert group8.n_gpus == 8
+    rng = np.random.default_rng(350)
+    P, N = 100_003, 5
+    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
+    c = rng.standard_normal(P).astype(F)
+    group8.set_layout([P])
+    group8.reserve(N)
+    group8.ckpt_upload(c)
+    for k in range(N):
+        group8.ingest(k, d[k])
+    group8.fedavg_resident(0)
+    ptrs = group8.allgather_resident()
+    assert group8.group_backend() == 0 and len(ptrs) == 8
+    want = coracle.fedavg(0, d, c)
+    S = -(-(-(-P // 8)) // 64) * 64  # every shard padded to the same multiple of 64
+    for p in ptrs:
+        full = d2h(p, 8 * S)
+        got = np.concatenate([full[k * S:k * S + min(S, P - k * S)] for k in range(8) if k * S < P])
+        assert np.array_equal(bits(got), bits(want))
+
+
+@pytest.mark.parametrize("client_shard", [False, True])
+@pytest.mark.parametrize("N", [1, 7, 9])
+def test_group8_secagg(group8, client_shard, N):
+    """Param shards and client shards over eight children (fewer clients than children included)."""
+    P, S = 5_003, 2
+    sh = _shares(360 + N, N, S, P)
+    sh[0, 0, :5] = [2**63 - 1, -2**63, -1, 1, 0]
+    group8.set_layout([P])
+    group8.set_client_sharding(client_shard)
+    try:
+        group8.reserve(N, 1, S)
+        for k in range(N):
+            group8.ingest(k, sh[k])
+        s, dec = group8.secagg(10, 3)
+    finally:
+        group8.set_client_sharding(False)
+    ws = O.secagg_sum(sh)
+    assert np.array_equal(s, ws)
+    assert np.array_equal(bits(dec), bits(O.fix_prec_decode(ws)))
+
+
+@pytest.mark.parametrize("speculate", [False, True])
+def test_group8_report_time_cycle(group8, speculate):
+    """Report-time folds fanned out to eight children: shuffled reports, dropouts, a re-report."""
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    rng = np.random.default_rng(370)
+    shapes = [(300, 77), (77,), (5,)]
+    n = 30
+    reporters = [w for w in range(n) if w != 0 and rng.random() >= 0.2]
+    diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in reporters}
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    ck_pb = build_state_fast(ckpt)
+    inc = IncrementalCycle(group8, [int(np.prod(s)) for s in shapes], slots=12, fold_batch=3, checkpoint=ck_pb,
+                           speculate=speculate, mark_every=2, lazy=False)
+    for w in range(n):
+        inc.assigned(w)
+    order = [int(w) for w in rng.permutation(reporters)]
+    again = order[len(order) // 2]
+    for w in order:
+        inc.reported(w, build_state_fast(diffs[w]))
+        if w == order[-3]:  # a re-report with a new diff, late in the cycle
+            diffs[again] = [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes]
+            inc.reported(again, build_state_fast(diffs[again]))
+    new = inc.close(ck_pb)
+    want = O.fedavg_mean(ckpt, [diffs[w] for w in sorted(reporters)])
+    for got, w in zip(parse_state(new), want):
+        assert np.array_equal(bits(got), bits(w))
