@@ -124,6 +124,7 @@ void free_slab(pgh_ctx* c) {
     c->h_peek = nullptr; c->peek_cap = 0; c->peek_gen = 0;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
+    if (c->dec) (void)hipStreamSynchronize(c->dec);  // a varint decode writes slab rows
     for (auto& fe : c->fold_evs) (void)hipEventSynchronize(fe.second);  // folds on caller streams
     (void)hipFree(c->d_slab); c->d_slab = nullptr; c->slab_bytes = 0;
     (void)hipFree(c->d_ckpt); c->d_ckpt = nullptr;
@@ -482,10 +483,11 @@ int state_shard_spans(pgh_ctx* c, const uint8_t* pb, size_t n, std::vector<std::
     return PGH_OK;
 }
 
-// Stream `s` waits for every ingest copy / synthetic fill issued so far.
+// Stream `s` waits for every ingest copy / synthetic fill / varint decode issued so far.
 int order_after_ingest(pgh_ctx* c, hipStream_t s) {
     CK(c, hipEventRecord(c->copy_done, c->copy));
     CK(c, hipStreamWaitEvent(s, c->copy_done, 0));
+    if (c->dec_last) CK(c, hipStreamWaitEvent(s, c->dec_last, 0));
     return PGH_OK;
 }
 
@@ -1071,7 +1073,14 @@ void pgh_destroy(pgh_ctx* c) {
     (void)hipFree(c->d_rec);
     for (double* p : c->rec_old) (void)hipFree(p);
     (void)hipFree(c->d_vbytes);
-    (void)hipFree(c->d_vtab);
+    if (c->dec) (void)hipStreamSynchronize(c->dec);
+    for (auto& b : c->vbuf) {
+        (void)hipFree(b.bytes);
+        (void)hipFree(b.tab);
+        if (b.done) (void)hipEventDestroy(b.done);
+    }
+    if (c->dec_in) (void)hipEventDestroy(c->dec_in);
+    if (c->dec) (void)hipStreamDestroy(c->dec);
     if (c->h_vtab) (void)hipHostFree(c->h_vtab);
     if (c->vtab_ev) (void)hipEventDestroy(c->vtab_ev);
     (void)hipFree(c->d_gtab);
@@ -1256,6 +1265,7 @@ int pgh_sync(pgh_ctx* c) {
     if (!c) return PGH_E_ARG;
     DeviceGuard g(c->device);
     CK(c, hipStreamSynchronize(c->copy));
+    if (c->dec) CK(c, hipStreamSynchronize(c->dec));
     CK(c, hipStreamSynchronize(c->stream));
     return PGH_OK;
 }

@@ -263,13 +263,29 @@ struct pgh_ctx {
     std::unique_ptr<CopyPool> pool_copy;
 
     // secagg shares as State bytes: varint payloads in HBM + their chunk table (k_varint_decode)
+    // Each decode runs on its own stream (dec) behind its message's DMAs, so the copy stream's next
+    // DMA does not queue behind it; the HBM bytes and chunk table alternate between two buffers (the
+    // DMA of one message beside the decode of the one before).
+    struct VarintBuf {
+        uint8_t* bytes = nullptr;
+        size_t cap = 0;
+        pgh::VChunk* tab = nullptr;
+        size_t tab_cap = 0;
+        hipEvent_t done = nullptr;  // the last decode that read this buffer
+        bool used = false;
+    };
+    VarintBuf vbuf[2];
+    int vbuf_next = 0;
+    hipStream_t dec = nullptr;
+    hipEvent_t dec_in = nullptr;     // copy stream -> dec: a message's bytes and table have landed
+    hipEvent_t dec_last = nullptr;   // the last decode issued: folds wait for it (order_after_ingest)
+    pgh::VChunk* h_vtab = nullptr;   // pinned host image of a chunk table
+    size_t vtab_cap = 0;
+    hipEvent_t vtab_ev = nullptr;    // the last table upload (h_vtab reusable after it)
+    bool vtab_used = false;
+    // page-locked fp32 State messages (below) stage through this buffer
     uint8_t* d_vbytes = nullptr;
     size_t vbytes_cap = 0;
-    pgh::VChunk* d_vtab = nullptr;
-    pgh::VChunk* h_vtab = nullptr;  // pinned
-    size_t vtab_cap = 0;
-    hipEvent_t vtab_ev = nullptr;
-    bool vtab_used = false;
     // page-locked fp32 State messages (pgh_ingest_state): DMA'd whole into d_vbytes, gathered into the
     // slab row by k_gather_f32 with this chunk table (PGH_PINNED_GATHER=0: one DMA per payload piece)
     pgh::GChunk* d_gtab = nullptr;

@@ -172,8 +172,8 @@ int grow_device(pgh_ctx* c, void** p, size_t* cap, size_t need, const char* what
 }
 
 // Stage one party message: chunk bytes -> pinned ring (copied and counted by the pool threads)
-// -> its region of the HBM byte buffer, on the copy stream.  Nothing is decoded yet.
-int stage_share_msg(pgh_ctx* c, ShareMsg& m) {
+// -> its region of the HBM byte buffer `dev`, on the copy stream.  Nothing is decoded yet.
+int stage_share_msg(pgh_ctx* c, ShareMsg& m, uint8_t* dev) {
     const double t0 = now_ms();
     const size_t nk = m.chunks.size();
     size_t k = 0;
@@ -193,7 +193,7 @@ int stage_share_msg(pgh_ctx* c, ShareMsg& m) {
             uint8_t* dst = pin + ((size_t)m.chunks[q].off - s0);
             m.st[q] = pgh_state::varint_copy_stats(dst, m.src[q], (size_t)m.chunks[q].n);
         });
-        CK(c, hipMemcpyAsync(c->d_vbytes + s0, pin, fill, hipMemcpyHostToDevice, c->copy));
+        CK(c, hipMemcpyAsync(dev + s0, pin, fill, hipMemcpyHostToDevice, c->copy));
         CK(c, hipEventRecord(c->pin_ev[ps], c->copy));
         c->pin_used[ps] = true;
         k = k1;
@@ -258,9 +258,27 @@ int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>
     return PGH_OK;
 }
 
-// Every party validated: one chunk table for all of them, then one decode per party into its
-// slab row (the shard's range), on the copy stream.
-int decode_share_msgs(pgh_ctx* c, std::vector<ShareMsg>& msgs, int slot) {
+// A varint buffer holding `bytes` of messages and a table of `tab_bytes` (grown when short, after
+// the decode that last read it).  The dec stream and its events are made on the first use.
+int prepare_vbuf(pgh_ctx* c, pgh_ctx::VarintBuf& b, size_t bytes, size_t tab_bytes) {
+    if (!c->dec) {
+        CK(c, hipStreamCreateWithFlags(&c->dec, hipStreamNonBlocking));
+        CK(c, hipEventCreateWithFlags(&c->dec_in, hipEventDisableTiming));
+        for (auto& x : c->vbuf) CK(c, hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
+    }
+    if ((bytes > b.cap || tab_bytes > b.tab_cap) && b.used) CK(c, hipEventSynchronize(b.done));
+    RC(grow_device(c, (void**)&b.bytes, &b.cap, bytes, "share payload buffer"));
+    void* t = b.tab;
+    RC(grow_device(c, &t, &b.tab_cap, tab_bytes, "varint chunk table"));
+    b.tab = (pgh::VChunk*)t;
+    // the copy stream's DMAs into this buffer wait for the decode that last read it (two messages ago)
+    if (b.used) CK(c, hipStreamWaitEvent(c->copy, b.done, 0));
+    return PGH_OK;
+}
+
+// Every party validated: one chunk table for all of them (uploaded behind the payload DMAs), then
+// one decode per party into its slab row (the shard's range), on the dec stream.
+int decode_share_msgs(pgh_ctx* c, std::vector<ShareMsg>& msgs, int slot, pgh_ctx::VarintBuf& b) {
     size_t nk = 0;
     for (auto& m : msgs) nk += m.chunks.size();
     if (nk == 0) return PGH_OK;  // every tensor empty
@@ -270,16 +288,13 @@ int decode_share_msgs(pgh_ctx* c, std::vector<ShareMsg>& msgs, int slot) {
     if (tb > c->vtab_cap) {
         if (c->h_vtab) (void)hipHostFree(c->h_vtab);
         c->h_vtab = nullptr;
-        size_t cap = 0;
-        void* d = c->d_vtab;
-        RC(grow_device(c, &d, &cap, tb, "varint chunk table"));
-        c->d_vtab = (pgh::VChunk*)d;
-        if (hipHostMalloc((void**)&c->h_vtab, cap, hipHostMallocDefault) != hipSuccess) {
+        c->vtab_cap = 0;
+        if (hipHostMalloc((void**)&c->h_vtab, b.tab_cap, hipHostMallocDefault) != hipSuccess) {
             (void)hipGetLastError();
-            c->vtab_cap = 0;
-            return fail(c, PGH_E_OOM, "pinned chunk table of %zu bytes failed", cap);
+            c->h_vtab = nullptr;
+            return fail(c, PGH_E_OOM, "pinned chunk table of %zu bytes failed", b.tab_cap);
         }
-        c->vtab_cap = cap;
+        c->vtab_cap = b.tab_cap;
         c->vtab_used = false;
     }
     size_t at = 0;
@@ -287,18 +302,22 @@ int decode_share_msgs(pgh_ctx* c, std::vector<ShareMsg>& msgs, int slot) {
         std::memcpy(c->h_vtab + at, m.chunks.data(), m.chunks.size() * sizeof(pgh::VChunk));
         at += m.chunks.size();
     }
-    CK(c, hipMemcpyAsync(c->d_vtab, c->h_vtab, tb, hipMemcpyHostToDevice, c->copy));
+    CK(c, hipMemcpyAsync(b.tab, c->h_vtab, tb, hipMemcpyHostToDevice, c->copy));
     CK(c, hipEventRecord(c->vtab_ev, c->copy));
     c->vtab_used = true;
+    CK(c, hipEventRecord(c->dec_in, c->copy));
+    CK(c, hipStreamWaitEvent(c->dec, c->dec_in, 0));
     at = 0;
     for (size_t s = 0; s < msgs.size(); ++s) {
         const int n = (int)msgs[s].chunks.size();
-        const hipError_t e = pgh::launch_varint_decode(c->d_vbytes, c->d_vtab + at, n,
-                                                       (int64_t*)slot_row(c, slot, (int)s), slab_map(c), c->lo, c->hi,
-                                                       c->copy);
+        const hipError_t e = pgh::launch_varint_decode(b.bytes, b.tab + at, n, (int64_t*)slot_row(c, slot, (int)s),
+                                                       slab_map(c), c->lo, c->hi, c->dec);
         if (e != hipSuccess) return fail(c, PGH_E_HIP, "varint decode launch failed: %s", hipGetErrorString(e));
         at += (size_t)n;
     }
+    CK(c, hipEventRecord(b.done, c->dec));
+    b.used = true;
+    c->dec_last = b.done;
     return PGH_OK;
 }
 }  // namespace
@@ -319,13 +338,17 @@ int pgh_ingest_state_shares(pgh_ctx* c, int client, int n_parties, const uint8_t
         RC(plan_share_msg(c, pbs[s], ns[s], client, s, total, &msgs[(size_t)s]));
         total += msgs[(size_t)s].bytes;
     }
+    size_t nk = 0;
+    for (auto& m : msgs) nk += m.chunks.size();
     DeviceGuard g(c->device);
     int slot = 0;
     RC(claim_slot(c, client, &slot));
-    RC(grow_device(c, (void**)&c->d_vbytes, &c->vbytes_cap, total + 16, "share payload buffer"));
-    for (auto& m : msgs) RC(stage_share_msg(c, m));
+    pgh_ctx::VarintBuf& b = c->vbuf[c->vbuf_next];
+    c->vbuf_next ^= 1;
+    RC(prepare_vbuf(c, b, total + 16, std::max<size_t>(nk, 1) * sizeof(pgh::VChunk)));
+    for (auto& m : msgs) RC(stage_share_msg(c, m, b.bytes));
     for (int s = 0; s < n_parties; ++s) RC(check_share_msg(c, &msgs[(size_t)s], client, s));
-    RC(decode_share_msgs(c, msgs, slot));
+    RC(decode_share_msgs(c, msgs, slot, b));
     return mark_ingested(c, client, slot);
 }
 
