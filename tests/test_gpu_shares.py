@@ -227,3 +227,37 @@ def test_share_state_random_value_mixes(engine, seed):
     want = O.secagg_sum(sh)
     assert np.array_equal(s, want)
     assert np.array_equal(d.view(np.uint32), O.fix_prec_decode(want).view(np.uint32))
+
+
+def test_share_state_decode_buffers_alternate_and_grow(engine):
+    """The varint decodes run on their own stream with two alternating HBM byte buffers: messages of
+    growing and shrinking wire size (1-byte to 10-byte varints, so each buffer grows while the other
+    one's decode may be in flight), a client re-ingested right after its first decode, and a STREAM
+    ring of two slots folded one client at a time (slots overwritten behind their folds) -- the sums
+    bit-exact against the oracle."""
+    rng = np.random.default_rng(15)
+    numel = [90_001, 13]
+    P, S, N = sum(numel), 2, 10
+    sh = np.empty((N, S, P), np.int64)
+    for c in range(N):  # alternate short and long varints, the long ones getting longer
+        sh[c] = rng.integers(0, 128, (S, P)) if c % 2 == 0 else -rng.integers(1, 2**(20 + 4 * c), (S, P), dtype=np.int64)
+    msgs = [[build_state_i64_fast(split(sh[c, s], numel)) for s in range(S)] for c in range(N)]
+    engine.set_layout(numel)
+    engine.reserve(N, 1, S)
+    for c in range(N):
+        engine.ingest_state_shares(c, msgs[c])
+        if c == 3:  # overwrite client 1 (small messages) and client 3 (long ones) at once
+            sh[1] = rng.integers(I64_MIN, I64_MAX, (S, P), dtype=np.int64, endpoint=True)
+            engine.ingest_state_shares(1, [build_state_i64_fast(split(sh[1, s], numel)) for s in range(S)])
+            engine.ingest_state_shares(3, msgs[3])
+    s, d = engine.secagg(10, 3)
+    want = O.secagg_sum(sh)
+    assert np.array_equal(s, want)
+    assert np.array_equal(d.view(np.uint32), O.fix_prec_decode(want).view(np.uint32))
+    msgs[1] = [build_state_i64_fast(split(sh[1, s], numel)) for s in range(S)]
+    engine.reserve(2, 1, S)
+    engine.stream_begin(16, 1)  # PGH_STREAM_SECAGG, a fold per client through a ring of two slots
+    for c in range(N):
+        engine.ingest_state_shares(c, msgs[c])
+    s2, _ = engine.stream_finish_secagg(10, 3)
+    assert np.array_equal(s2, want)
