@@ -18,6 +18,15 @@ def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
+def wait_for_peek(eng, timeout_s=5.0):
+    import time
+
+    deadline = time.monotonic() + timeout_s
+    while not eng.peek_valid():
+        assert time.monotonic() < deadline, "no valid peek within 5 s of the last report (retry lost)"
+        time.sleep(0.002)
+
+
 def _want(mode, ckpt, rows, weights=None):
     if mode == 0:
         return O.fedavg_mean(ckpt, rows)
@@ -50,6 +59,10 @@ def test_committed_peek_is_bit_exact_and_chains(devices, mode):
                 inc.assigned(w)
             for w in rng.permutation(reporters):
                 inc.reported(int(w), build_state_fast(diffs[int(w)]))
+            # the last report's peek is skipped when the previous one's copy is still running (reports
+            # back to back); the settle timer takes it once the reports pause -- the regime the
+            # committed peek is for
+            wait_for_peek(eng)
             new = inc.close(ck)
             assert inc.last_close["peeked"], inc.last_close
             want = _want(mode, want, [diffs[w] for w in reporters], [weights[w] for w in reporters])
@@ -120,6 +133,7 @@ def test_abandoned_cycle_peek_copy_finishes_before_the_next_peek():
                 del inc  # dropped with its peek copy in flight
                 gc.collect()
                 continue
+            wait_for_peek(eng)
             new = inc.close(ck)
             assert inc.last_close["peeked"], inc.last_close
             want = O.fedavg_mean(ckpt, [diffs[w] for w in range(4)])
