@@ -9,7 +9,7 @@ import gc
 import numpy as np
 import pytest
 
-from test_node_sql import CFG, SqlScenario, run_both, script_three_cycles
+from test_node_sql import CFG, SqlScenario, random_script, run_both, script_three_cycles
 
 pytestmark = pytest.mark.gpu
 F = np.float32
@@ -72,3 +72,20 @@ def test_installed_sql_node_on_a_group(tmp_path, speculate):
         assert st["closes_report_time"] == 3 and st["report_errors"] == 0, st
     gc.collect()
     assert [(p.hits, p.misses, p.blocks) for p in eng.pools] == [(12, 0, 0), (2, 0, 0)]
+
+
+@pytest.mark.parametrize("speculate", [False, True], ids=["certain-only", "speculative"])
+def test_randomised_scripts_on_the_gpu_sql_node(tmp_path, engine, speculate):
+    """tests/test_node_sql.py's random scripts on the GPU engine with page-locked report blocks and
+    the close on an executor thread: byte-identical checkpoints and DB diffs."""
+    def fresh_engine():
+        engine.reset()
+        engine.ckpt_owner = None
+        return engine
+
+    for trial in range(4):
+        script, slots = random_script(600 + trial, f"g{trial}")
+        eng = run_both(tmp_path / f"t{trial}", script, engine=fresh_engine, ckpt=mnist_ckpt(), diff_fn=mnist_diff,
+                       threaded=True, pinned_reports=4, speculate=speculate, slots=slots)
+        st = eng.stats
+        assert st["closes_report_time"] == 3 and st["report_errors"] == 0, (trial, st)

@@ -277,41 +277,44 @@ def test_install_into_node_by_package_name(tmp_path, monkeypatch):
             del sys.modules[m]
 
 
+def random_script(seed: int, prefix: str):
+    """Three cycles (CFG: max_diffs 4) of a fresh set of 5-8 workers each, reports in random order with
+    re-reports, a fifth report arriving after the close (late), and restarts of the node process."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(5, 9))
+    ops = []
+    for cyc in range(3):
+        ws = [f"{prefix}c{cyc}w{i}" for i in range(n)]
+        ops.append(("assign", ws))
+        for w in list(rng.permutation(ws))[:5]:
+            ops.append(("report", w, 0))
+            if rng.random() < 0.25:
+                ops.append(("report", w, 1))
+            if rng.random() < 0.1:
+                ops.append(("restart",))
+
+    def script(sc):
+        for op in ops:
+            if op[0] == "assign":
+                sc.assign(*op[1])
+            elif op[0] == "report":
+                sc.report(op[1], version=op[2])
+            else:
+                sc.restart()
+    return script, int(rng.integers(2, 7))
+
+
 @pytest.mark.parametrize("speculate", [False, True], ids=["certain-only", "speculative"])
 @pytest.mark.parametrize("threaded", [False, True], ids=["sync", "executor"])
 def test_randomised_scripts_on_the_sql_node(tmp_path, threaded, speculate):
-    """Random scripts through the reference's storage and handler: per cycle a fresh set of workers
-    assigned, reports in random order (re-reports, one late report after the close, restarts of the
-    node process mid-cycle), random slot budgets -- installed and shipped nodes save identical
-    checkpoints and hold identical diff blobs."""
-    import numpy as np
-
+    """Random scripts (``random_script``) through the reference's storage and handler, random slot
+    budgets: installed and shipped nodes save identical checkpoints and hold identical diff blobs."""
     totals = collections.Counter()
     for trial in range(8):
-        rng = np.random.default_rng(500 + trial)
-        n = int(rng.integers(5, 9))
-        ops = []
-        for cyc in range(3):  # CFG: max_diffs 4, three cycles
-            ws = [f"t{trial}c{cyc}w{i}" for i in range(n)]
-            ops.append(("assign", ws))
-            for w in list(rng.permutation(ws))[:5]:  # the 5th report comes after the close: late
-                ops.append(("report", w, 0))
-                if rng.random() < 0.25:
-                    ops.append(("report", w, 1))
-                if rng.random() < 0.1:
-                    ops.append(("restart",))
-
-        def script(sc):
-            for op in ops:
-                if op[0] == "assign":
-                    sc.assign(*op[1])
-                elif op[0] == "report":
-                    sc.report(op[1], version=op[2])
-                else:
-                    sc.restart()
-
-        eng = run_both(tmp_path / f"t{trial}", script, threaded=threaded, speculate=speculate,
-                       slots=int(rng.integers(2, 7)))
+        script, slots = random_script(500 + trial, f"t{trial}")
+        eng = run_both(tmp_path / f"t{trial}", script, threaded=threaded, speculate=speculate, slots=slots)
         totals.update(eng.stats)
     assert totals["report_errors"] == 0, totals
     assert totals["closes_report_time"] == 24 and totals["diffs_from_db"] >= 1, totals  # restarts read the DB
