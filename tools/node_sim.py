@@ -28,6 +28,7 @@ and the next cycle open (the executor's ``complete_cycle``), with the engine's s
 import base64
 import functools
 import json
+import os
 import sys
 import threading
 import time
@@ -94,6 +95,11 @@ class Timer:
 
 
 def run_arm(eng, cycles, gap_ms, opts, pinned, db, rng, ckpt, texts, framing="fresh"):
+    if db != "sqlite://":  # a file: a fresh one per arm (each arm hosts its own FL process)
+        path = db[len("sqlite:///"):]
+        for suffix in ("", "-journal", "-wal", "-shm"):
+            if os.path.exists(path + suffix):
+                os.remove(path + suffix)
     mod, store = make_sql_node(db)
     ex = Executor()
     mod.run_task_once = ex.run_task_once
