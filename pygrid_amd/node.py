@@ -512,6 +512,15 @@ _MISSING = _Missing()
 
 
 def _as_checkpoint(cp, model_id, value) -> Checkpoint:
+    state = getattr(cp, "_sa_instance_state", None)
+    if state is not None and state.key is not None and state.session is not None and "number" not in cp.__dict__:
+        # A ModelCheckPoint the save's commit expired (expire_on_commit): reading any attribute would
+        # reload the whole row, its 47 MB blob included -- 55-60 ms per close for a value we hold.
+        # Read the small columns alone; the id is the identity key (no query).
+        cls = type(cp)
+        ident = state.key[1][0]
+        number, alias, mid = state.session.query(cls.number, cls.alias, cls.model_id).filter(cls.id == ident).one()
+        return Checkpoint(id=ident, model_id=mid, number=number, alias=alias, value=value)
     return Checkpoint(id=getattr(cp, "id", 0), model_id=getattr(cp, "model_id", model_id),
                       number=getattr(cp, "number", 0), alias=getattr(cp, "alias", "latest"), value=value)
 

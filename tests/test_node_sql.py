@@ -318,3 +318,35 @@ def test_randomised_scripts_on_the_sql_node(tmp_path, threaded, speculate):
         totals.update(eng.stats)
     assert totals["report_errors"] == 0, totals
     assert totals["closes_report_time"] == 24 and totals["diffs_from_db"] >= 1, totals  # restarts read the DB
+
+
+def test_installed_close_reads_no_checkpoint_blob(tmp_path):
+    """After the first cycle, no close of the installed node SELECTs a checkpoint's ``value``: the
+    input checkpoint is resident (HBM + the write-through cache), and caching the saved one reads
+    its small columns only -- touching the ``ModelCheckPoint`` the save's commit expired would
+    reload its 47 MB blob (55-60 ms per close at ResNet-18 size)."""
+    from sqlalchemy import event
+
+    sc = SqlScenario(tmp_path / "node.db", True)
+    try:
+        blob_selects = []
+
+        def seen(conn, cursor, statement, params, context, executemany):
+            s = statement.lower()
+            if s.lstrip().startswith("select") and "model_centric_model_checkpoint.value" in s:
+                blob_selects.append(statement)
+        sc.assign("w1", "w2", "w3", "w4")
+        for w in ("w2", "w1", "w4", "w3"):
+            sc.report(w)  # first close: the checkpoint is read from the DB once
+        event.listen(sc.store.engine, "before_cursor_execute", seen)
+        for cyc in (1, 2):
+            sc.assign("w1", "w2", "w3", "w4")
+            for w in ("w3", "w1", "w2", "w4"):
+                sc.report(w, version=cyc)
+        assert sc.stats["closes_report_time"] == 3, sc.stats
+        assert not blob_selects, blob_selects
+        cached = sc.node.store.lookup(model_id=sc.proc.id if hasattr(sc.proc, "id") else 1, alias="latest")
+        rows = sc.checkpoints()
+        assert cached is not None and (cached.number, cached.alias, cached.value) == rows[-1]
+    finally:
+        sc.finish()
