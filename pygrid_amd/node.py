@@ -147,6 +147,9 @@ class NodeEngine:
         self.trigger = CycleCloseTrigger(lambda fn, *a: fn(*a), executor=executor) if close_trigger == "replay" \
             else None
         self._cycles: Dict[object, object] = {}  # cycle id -> IncrementalCycle | _DECLINED | _ELSEWHERE
+        # (worker id, request key) -> (WorkerCycle id, cycle id) of the rows assigned through this
+        # process: a report finds its row without a DB query (rows assigned before a restart: queried)
+        self._assigned: Dict[tuple, tuple] = {}
         self._owner = None  # the cycle id whose IncrementalCycle holds the engine
         self._lock = threading.RLock()  # the maps above; held only briefly
         self._gate = _Gate()  # reports (shared) vs a close's snapshot of the rows (exclusive)
@@ -174,7 +177,7 @@ class NodeEngine:
 
         def assign(cm, worker, cycle, hash_key):
             wc = orig["assign"](cm, worker, cycle, hash_key)
-            node.on_assign(cm, cycle, wc)
+            node.on_assign(cm, cycle, wc, key=(getattr(worker, "id", None), hash_key))
             return wc
 
         def submit_worker_diff(cm, worker_id, request_key, diff):
@@ -331,22 +334,29 @@ class NodeEngine:
         imported into ``cycle_manager.py:18``)."""
         return self.mod.complete_cycle
 
-    def on_assign(self, cm, cycle, wc):
+    def on_assign(self, cm, cycle, wc, key=None):
         st = self._cycle_state(cm, cycle)
         if isinstance(st, IncrementalCycle):
             st.assigned(wc.id, key=wc.id)
+            if key is not None and key[0] is not None:
+                with self._lock:
+                    self._assigned[key] = (wc.id, cycle.id)
 
     def on_report(self, cm, worker_id, request_key, diff):
         """After the reference's DB write.  Never raises: the response stays the reference's, and a
         diff the engine could not take is read from the DB at close."""
         try:
-            wc = _first_row(cm, worker_id=worker_id, request_key=request_key)
-            st = self._cycles.get(wc.cycle_id)
+            hit = self._assigned.get((worker_id, request_key))
+            if hit is None:
+                wc = _first_row(cm, worker_id=worker_id, request_key=request_key)
+                hit = (wc.id, wc.cycle_id)
+            row_id, cycle_id = hit
+            st = self._cycles.get(cycle_id)
             if st is None and self.report_time:
-                cycle = cm._cycles.first(id=wc.cycle_id)
+                cycle = cm._cycles.first(id=cycle_id)
                 st = self._cycle_state(cm, cycle) if cycle is not None else None
             if isinstance(st, IncrementalCycle):
-                st.reported(wc.id, diff)
+                st.reported(row_id, diff)
         except (PyGridError, StateParseError) as e:
             self.stats["report_errors"] += 1
             log.warning("report of worker %s kept for the close-time read (%s)", worker_id, e)
@@ -367,6 +377,7 @@ class NodeEngine:
             try:
                 with self._lock:
                     st = self._cycles.pop(cycle.id, None)
+                    self._assigned = {k: v for k, v in self._assigned.items() if v[1] != cycle.id}
                     if self._owner == cycle.id:
                         self._owner = None
                     if not isinstance(st, IncrementalCycle) and st != _DECLINED:

@@ -350,3 +350,18 @@ def test_installed_close_reads_no_checkpoint_blob(tmp_path):
         assert cached is not None and (cached.number, cached.alias, cached.value) == rows[-1]
     finally:
         sc.finish()
+
+
+def test_reports_find_their_rows_without_a_query(tmp_path, monkeypatch):
+    """A report of a row assigned through the installed node finds its WorkerCycle id and cycle from
+    the assignment (no query after the handler's DB write); rows assigned before a restart are
+    looked up in the DB -- the checkpoints stay the reference's."""
+    calls = []
+    real = pnode._first_row
+    monkeypatch.setattr(pnode, "_first_row", lambda *a, **k: calls.append(k) or real(*a, **k))
+    eng = run_both(tmp_path, script_three_cycles)
+    # script_three_cycles: cycle 1's late report (its cycle closed: the rows are forgotten) and the
+    # two reports of cycle 3 that follow the restart
+    assert [(c["worker_id"], c["request_key"]) for c in calls] == [("w3", "key-w3-1"), ("w3", "key-w3-3"),
+                                                                  ("w4", "key-w4-3")], calls
+    assert eng.stats["closes_report_time"] == 3
