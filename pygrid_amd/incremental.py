@@ -186,13 +186,25 @@ class IncrementalCycle:
             engine.ckpt_owner = self
             self._ckpt = checkpoint
         # the new checkpoint's bytes, framed and faulted in while the cycle is open (the close then
-        # copies into resident pages: with speculative folds there is little fold left to hide that)
+        # copies into resident pages: with speculative folds there is little fold left to hide that).
+        # Certain-only: on a thread of its own, so the 47 MB frame and its page faults (3-5 ms) stay
+        # off the previous close, which creates this cycle (a close that comes first frames its own
+        # bytes).  With the peek, at once: every peek from the first report on copies into it.
         self._prepared = None
         if checkpoint is not None and hasattr(engine, "ckpt_patch_into"):
-            try:
-                self._prepared = (checkpoint, state_codec.prepared_fresh_frame(checkpoint))
-            except StateParseError:
-                self._prepared = None
+            if self._peek:
+                self._prepare(checkpoint)
+            else:
+                threading.Thread(target=self._prepare, args=(checkpoint,), name="pgh-prepare", daemon=True).start()
+
+    def _prepare(self, checkpoint: bytes):
+        try:
+            frame = state_codec.prepared_fresh_frame(checkpoint)
+        except StateParseError:
+            return
+        with self._lock:
+            if not self._closed:
+                self._prepared = (checkpoint, frame)
 
     # ---- assignment (cycle_manager.assign, fl_controller.py:131-132) ---------------------------
     def assigned(self, worker, key=None):
