@@ -187,24 +187,24 @@ class IncrementalCycle:
             self._ckpt = checkpoint
         # the new checkpoint's bytes, framed and faulted in while the cycle is open (the close then
         # copies into resident pages: with speculative folds there is little fold left to hide that).
-        # Certain-only: on a thread of its own, so the 47 MB frame and its page faults (3-5 ms) stay
-        # off the previous close, which creates this cycle (a close that comes first frames its own
-        # bytes).  With the peek, at once: every peek from the first report on copies into it.
+        # The frame is allocated here; certain-only, its page faults (3-5 ms for 47 MB) run on a thread
+        # of its own, off the previous close, which creates this cycle (``finish`` joins it).  With
+        # the peek, at once: every peek from the first report on copies into it.
         self._prepared = None
+        self._prep_thread: Optional[threading.Thread] = None
         if checkpoint is not None and hasattr(engine, "ckpt_patch_into"):
-            if self._peek:
-                self._prepare(checkpoint)
-            else:
-                threading.Thread(target=self._prepare, args=(checkpoint,), name="pgh-prepare", daemon=True).start()
-
-    def _prepare(self, checkpoint: bytes):
-        try:
-            frame = state_codec.prepared_fresh_frame(checkpoint)
-        except StateParseError:
-            return
-        with self._lock:
-            if not self._closed:
+            try:
+                frame = state_codec.fresh_frame_bytes(checkpoint)  # allocated and framed here, on this thread
+            except StateParseError:
+                frame = None
+            if frame is not None:
                 self._prepared = (checkpoint, frame)
+                if self._peek:
+                    state_codec.prefault(frame)
+                else:
+                    self._prep_thread = threading.Thread(target=state_codec.prefault, args=(frame,),
+                                                         name="pgh-prefault", daemon=True)
+                    self._prep_thread.start()
 
     # ---- assignment (cycle_manager.assign, fl_controller.py:131-132) ---------------------------
     def assigned(self, worker, key=None):
@@ -601,6 +601,9 @@ class IncrementalCycle:
                 log.info("re-folding the cycle in the DB's order: %s", refold)
                 self.engine.fold_restart()
                 self._weights = []
+            if self._prep_thread is not None:  # a few ms of work at most, and less than doing it here
+                self._prep_thread.join()
+                self._prep_thread = None
             prep = self._prepared[1] if self._prepared and self._prepared[0] is checkpoint else None
             self._prepared = None
             # nothing left to fold and the last peek still matches: its result IS the new checkpoint

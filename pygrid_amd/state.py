@@ -113,14 +113,20 @@ def fresh_frame_bytes(template: bytes, ids=None):
     return out, ptr
 
 
+def prefault(frame):
+    """Fault in the pages of a ``fresh_frame_bytes`` result (``pgh_host_prefault``)."""
+    out, ptr = frame
+    if ptr:
+        _lib.load().pgh_host_prefault(C.c_void_p(ptr), len(out))
+
+
 def prepared_fresh_frame(template: bytes, ids=None):
     """``fresh_frame_bytes`` with the payload pages already faulted in (``pgh_host_prefault``): made
     while a cycle is still open, so the close copies the new checkpoint into resident pages instead
     of faulting ~11 K of them in while the D2H waits."""
-    out, ptr = fresh_frame_bytes(template, ids)
-    if ptr:
-        _lib.load().pgh_host_prefault(C.c_void_p(ptr), len(out))
-    return out, ptr
+    frame = fresh_frame_bytes(template, ids)
+    prefault(frame)
+    return frame
 
 
 def fresh_checkpoint(engine, template: bytes, ids=None, prepared=None) -> bytes:
