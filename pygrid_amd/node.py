@@ -263,7 +263,7 @@ class NodeEngine:
         return self._orig_run(name, func, *args)
 
     # ---- report-time state -------------------------------------------------------------------
-    def _cycle_state(self, cm, cycle, create: bool = True):
+    def _cycle_state(self, cm, cycle, create: bool = True, fresh: bool = False):
         """The cycle's IncrementalCycle (made on first use, from its DB rows after a restart), or a
         marker saying why there is none.  None (nothing recorded, retried on the next call) while
         another thread's close holds the engine: a handler does not wait for it."""
@@ -284,7 +284,7 @@ class NodeEngine:
                     self._cycles[cycle.id] = _ELSEWHERE  # the engine serves another open cycle
                     return _ELSEWHERE
                 try:
-                    inc = self._new_cycle(cm, cycle)
+                    inc = self._new_cycle(cm, cycle, fresh)
                 except PlanNotAcceleratedError as e:
                     log.info("cycle %s: %s -- the node averages it", cycle.id, e)
                     self._cycles[cycle.id] = _DECLINED
@@ -295,7 +295,7 @@ class NodeEngine:
         finally:
             self._engine_lock.release()
 
-    def _new_cycle(self, cm, cycle) -> IncrementalCycle:
+    def _new_cycle(self, cm, cycle, fresh: bool = False) -> IncrementalCycle:
         server_config, _ = self.process_manager.get_configs(id=cycle.fl_process_id)
         avg_plan, plan_key = hosted_plan(server_config, cycle, self.process_manager, self.plan_manager,
                                          self.aggregator.mean_plans)
@@ -314,8 +314,9 @@ class NodeEngine:
         inc = IncrementalCycle(self.engine, numel, mode=mode, slots=self.slots, fold_batch=self.fold_batch,
                                checkpoint=ckpt, speculate=self.speculate,
                                **({} if self.peek is None else {"peek": self.peek}))
-        for row in _rows(cm, cycle_id=cycle.id):  # after a restart: the rows assigned before it
-            inc.assigned(row.id, key=row.id)
+        if not fresh:  # after a restart: the rows assigned before it (a cycle just created has none)
+            for row in _rows(cm, cycle_id=cycle.id):
+                inc.assigned(row.id, key=row.id)
         return inc
 
     def on_cycle_created(self, cm, cycle):
@@ -323,7 +324,7 @@ class NodeEngine:
             self.trigger.schedule_deadline(cycle.id, getattr(cycle, "end", None),
                                            args=(self._task_fn(), cm, cycle.id))
         try:
-            self._cycle_state(cm, cycle)
+            self._cycle_state(cm, cycle, fresh=True)
         except Exception as e:  # noqa: BLE001 -- preparing early is an optimisation only
             log.warning("cycle %s: report-time state not prepared (%s); close-time path", cycle.id, e)
             with self._lock:
