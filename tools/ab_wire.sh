@@ -2,6 +2,8 @@
 # A/B of the shares-from-the-wire close (bench.py --workload resnet18-secagg-state): the library in
 # tools/_variantA (a snapshot of the tree before a change) against the tree, interleaved on one lease.
 #   bash tools/ab_wire.sh <tag> [rounds]
+# Snapshot A first (mtimes kept, so the copy is not rebuilt):
+#   mkdir -p tools/_variantA && cp -rp bench.py pygrid_amd oracle include tools/_variantA/
 set -o pipefail
 OUT=gpurun_out/${1:-ab_wire}
 mkdir -p $OUT
