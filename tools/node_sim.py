@@ -18,6 +18,7 @@ routes.py:314; ``max_diffs`` = 80), shuffled arrival.  Arms: reports ``paced`` `
 close (``peek``) / without (``spec``) / certain-only folds (``certain``).
 
     python tools/node_sim.py [cycles] [--gap-ms=5] [--no-pinned] [--db=PATH] [--arms=paced_spec,...] [--cpu]
+                             [--devices=0,0]   (a one-process group, as install(devices=[...]))
 
 Prints one JSON line: per arm the report handler latency (p50 / p99 / max) and its phases (the
 handler's base64 decode including ``.encode()``, the DB write + commit, the engine's ingest), and
@@ -222,7 +223,8 @@ def main():
     kinds = {"default": {}, "peek": {"speculate": True, "peek": True}, "spec": {"speculate": True, "peek": False},
              "certain": {"speculate": False}}
     framing = "template" if "--cpu" in sys.argv else "fresh"
-    with (Engine(0) if "--cpu" not in sys.argv else _nullctx(NumpyEngine())) as eng:
+    devices = [int(d) for d in opt["devices"].split(",")] if "devices" in opt else None
+    with (_nullctx(NumpyEngine()) if "--cpu" in sys.argv else Engine(devices=devices) if devices else Engine(0)) as eng:
         # An untimed pass of the first arm: the process's first arm ran its report handlers at
         # 74-81 ms p50 against 29-37 for every later arm, whatever the arm (the .encode() copy 12-14 ms
         # instead of 2, the DB write 60 instead of 25: first-touch host memory, profiles/r04d, r04i,
@@ -240,7 +242,7 @@ def main():
                     "shuffled order; JSON base64 text -> restated fl_events.report (.encode() + b64decode) -> "
                     "submit_worker_diff (SQLAlchemy LargeBinary write + commit) -> engine ingest; close by "
                     "run_task_once on an executor thread",
-        "db": db, "pinned_reports": pinned, "cycles": cycles, "gap_ms": gap,
+        "db": db, "pinned_reports": pinned, "cycles": cycles, "gap_ms": gap, "devices": devices,
         "warmup": f"one untimed cycle of {want[0]} first, then every arm's own untimed cycle 0",
         "close_definition": "last report handler returned -> new checkpoint committed + next cycle open "
                             "(complete_cycle on the executor thread)",
