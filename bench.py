@@ -115,10 +115,14 @@ def parse():
                          "comes later than its last report; 0: at once)")
     ap.add_argument("--sync-before-close", action="store_true",
                     help="resnet18-report: wait for the GPU before the close and time that wait apart")
+    ap.add_argument("--speculate", action="store_true",
+                    help="resnet18-report: the opt-in speculative folds (and peeked close) instead of the "
+                         "certain-only default")
     ap.add_argument("--eager-speculate", action="store_true",
-                    help="resnet18-report: speculative folds at every report even while the GPU is busy")
+                    help="resnet18-report with --speculate: speculative folds at every report even while the "
+                         "GPU is busy")
     ap.add_argument("--no-speculate", action="store_true",
-                    help="resnet18-report: fold only certain positions early (no speculative folds / rewinds)")
+                    help="resnet18-report: certain-only folds (the default since round 4; kept for old scripts)")
     ap.add_argument("--no-group-line", action="store_true",
                     help="N > 1 per-rank runs: skip the one-process group over the same GPUs measured after the "
                          "ranks exit (the JSON line's `group` record)")
@@ -1210,11 +1214,13 @@ def run_resnet18_report(ctx, args, eng, N):
     reporters = [w for w in range(N) if w != 0 and rng.random() >= 0.2]
     arrival = [int(w) for w in rng.permutation(reporters)]
     slots, batch = args.ring or N, 8
-    closes, early, at_close, rewinds, pending = [], [], [], [], []
+    closes, early, at_close, rewinds, pending, spec = [], [], [], [], [], []
 
     def cycle():
         inc = IncrementalCycle(eng, numel, slots=slots, fold_batch=batch, checkpoint=ck_pb,
-                               speculate=False if args.no_speculate else None, lazy=not args.eager_speculate)
+                               speculate=bool(args.speculate and not args.no_speculate),
+                               lazy=not args.eager_speculate)
+        spec.append(inc.speculate)
         for w in range(N):
             inc.assigned(w)
         for w in arrival:
@@ -1258,7 +1264,7 @@ def run_resnet18_report(ctx, args, eng, N):
              "close_ms_after_last_report_all": [round(c, 3) for c in closes],
              "folded_before_close": int(np.median(early)) if early else 0,
              "rows_folded_at_close": int(np.median(at_close)) if at_close else 0,
-             "speculative_folds": not args.no_speculate,
+             "speculative_folds": bool(spec and spec[-1]),
              "report_gap_ms": args.report_gap_ms,
              "close_gap_ms": args.close_gap_ms,
              "pending_gpu_ms_at_close": [round(x, 3) for x in pending] if pending else None,

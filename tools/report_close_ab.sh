@@ -29,14 +29,16 @@ tests)
       tests/test_gpu_pinned_report.py tests/test_gpu_speculative_close.py -x -q --timeout 300 --timeout-method thread > "$out/pytest_new.log" 2>&1
   rc=$?; tail -3 "$out/pytest_new.log"; exit $rc ;;
 bench)
-  for arm in "spec:" "eager:--eager-speculate" "nospec:--no-speculate" "spec5:--report-gap-ms 5" "nospec5:--no-speculate --report-gap-ms 5" \
-      "spec_end20:--close-gap-ms 20" "nospec_end20:--no-speculate --close-gap-ms 20"; do
+  # speculative folds are opt-in since round 4 (--speculate); certain-only is the default
+  for arm in "spec:--speculate" "eager:--speculate --eager-speculate" "nospec:" "spec5:--speculate --report-gap-ms 5" \
+      "nospec5:--report-gap-ms 5" "spec_end20:--speculate --close-gap-ms 20" "nospec_end20:--close-gap-ms 20"; do
     name=${arm%%:*}; flags=${arm#*:}
     timeout -k 10 200 python -u bench.py --workload resnet18-report --steps "$steps" --warmup 2 --no-cpu-baseline \
         --sync-before-close $flags > "$out/report_$name.json" 2> "$out/report_$name.err" || exit 1
     python -c "import json; d=json.loads(open('$out/report_$name.json').read().splitlines()[-1]); print('$name', d['close_ms_after_last_report'], d['close_ms_after_last_report_all'], d['pending_gpu_ms_at_close'], d.get('rewinds_per_cycle'), d['value'])"
   done ;;
 node)
+  # round 3's node_sim flags; since round 4 tools/node_sim.py takes --arms=paced_default,... instead
   for arm in "spec0:--close-gap-ms=0" "nospec0:--no-speculate --close-gap-ms=0" "spec50:" "nospec50:--no-speculate"; do
     name=${arm%%:*}; flags=${arm#*:}
     timeout -k 10 300 python -u tools/node_sim.py 8 $flags > "$out/node_$name.json" 2> "$out/node_$name.err" || { tail -5 "$out/node_$name.err"; exit 1; }
