@@ -80,10 +80,13 @@ def main():
     for e in summary.values():
         e["kernels_sha256"] = sha
     (dst / "pmc_summary.json").write_text(json.dumps(summary, indent=1) + "\n")
-    traffic = {w: {str(e["variant"]): {kk: e[kk] for kk in ("hbm_bytes_per_launch", "alg_bytes_per_launch", "ratio",
-                                                           "kernel", "layout", "source", "kernels_sha256")}}
-               for w, e in summary.items()}
-    (ROOT / "profiles" / "pmc_traffic.json").write_text(json.dumps(traffic, indent=1) + "\n")
+    path = ROOT / "profiles" / "pmc_traffic.json"
+    traffic = json.loads(path.read_text()) if path.exists() else {}  # other tools' rows (report-path/*) stay
+    traffic.update({w: {str(e["variant"]): {kk: e[kk] for kk in ("hbm_bytes_per_launch", "alg_bytes_per_launch",
+                                                                "ratio", "kernel", "layout", "source",
+                                                                "kernels_sha256")}}
+                    for w, e in summary.items()})
+    path.write_text(json.dumps(traffic, indent=1) + "\n")
     for w, e in summary.items():
         print(w, e["variant"], f"ratio {e['ratio']:.6f}")
 
