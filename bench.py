@@ -30,6 +30,13 @@ Other BASELINE configs (--workload), each printed as its own JSON line of the sa
   resnet18-report        the same cycle with report-time aggregation: each
                          State diff is folded into HBM as it is reported, the checkpoint uploaded
                          at cycle start; reports the cycle close latency after the last report
+
+The default run (resnet18-fedavg) also carries configs 1, 3, 4 and 5 as sub-lines (`config1` ...
+`config5`), each a fresh child run with a bit-exact check, and -- at N > 1 -- the one-process group
+over the same GPUs (`group`).  The whole run keeps to one deadline (--budget-s, under the driver's
+600 s): every child gets at most what is left after the headline's reserve, a child that runs out
+leaves {"error": "timeout after ... s", "stage": ...} in its slot, and the headline line is printed
+whatever happens (a watchdog prints it with an error when the headline itself cannot finish).
 """
 from __future__ import annotations
 
@@ -37,6 +44,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -115,14 +123,6 @@ def parse():
                          "comes later than its last report; 0: at once)")
     ap.add_argument("--sync-before-close", action="store_true",
                     help="resnet18-report: wait for the GPU before the close and time that wait apart")
-    ap.add_argument("--speculate", action="store_true",
-                    help="resnet18-report: the opt-in speculative folds (and peeked close) instead of the "
-                         "certain-only default")
-    ap.add_argument("--eager-speculate", action="store_true",
-                    help="resnet18-report with --speculate: speculative folds at every report even while the "
-                         "GPU is busy")
-    ap.add_argument("--no-speculate", action="store_true",
-                    help="resnet18-report: certain-only folds (the default since round 4; kept for old scripts)")
     ap.add_argument("--no-group-line", action="store_true",
                     help="N > 1 per-rank runs: skip the one-process group over the same GPUs measured after the "
                          "ranks exit (the JSON line's `group` record)")
@@ -135,9 +135,143 @@ def parse():
                          "the oracle computes them from that rank's inputs, rank 0 compares the all-gathered "
                          "new checkpoint bit for bit (a checker leg outside the timed region)")
     ap.add_argument("--no-config-lines", action="store_true",
-                    help="default workload: skip the config-4 / config-5 lines (c4-stream, c5-ingest --check over "
-                         "the same --gpus, each in a fresh child world) attached under `config4` / `config5`")
+                    help="default workload: skip the config lines (mnist-state --check on one GPU; resnet18-secagg, "
+                         "c4-stream, c5-ingest --check over the same --gpus; each in a fresh child run) attached "
+                         "under `config1` / `config3` / `config4` / `config5`")
+    ap.add_argument("--budget-s", type=float, default=None,
+                    help=f"deadline of the whole run, seconds (default: PGH_BENCH_BUDGET_S or {DEFAULT_BUDGET_S:.0f}, "
+                         "under the driver's 600 s).  Every child line gets min(its own limit, what is left minus "
+                         "--headline-reserve-s); the headline line is printed whatever happens")
+    ap.add_argument("--headline-reserve-s", type=float, default=None,
+                    help="seconds of the budget kept for the headline world (default 150 at N = 1: its "
+                         "end-to-end and report-time closes and cpu_baseline; 120 at N > 1)")
     return ap.parse_args()
+
+
+# ---- the run's deadline ------------------------------------------------------
+# One absolute deadline (wall clock) for this process and everything it starts: child runs get a
+# deadline of their own (PGH_BENCH_DEADLINE, inside their `timeout` limit), ranks spawned here share
+# this one.  Stage durations go on the line under `budget`.
+DEFAULT_BUDGET_S = 540.0
+MIN_CHILD_S = 20.0        # a child that would get less is not started (its slot says why)
+WATCHDOG_MARGIN_S = 10.0  # the watchdog prints the headline line this long before the deadline
+RUN = {"t0": time.time(), "deadline": None, "budget_s": None, "stage": "start", "stages": {}, "printed": False}
+_EMIT = threading.Lock()
+
+
+def set_deadline(args):
+    budget = args.budget_s if args.budget_s is not None else float(os.environ.get("PGH_BENCH_BUDGET_S",
+                                                                                  DEFAULT_BUDGET_S))
+    deadline = RUN["t0"] + budget
+    inherited = os.environ.get("PGH_BENCH_DEADLINE")
+    if inherited:  # a child run (its parent's limit) or a spawned rank (its parent's deadline)
+        deadline = min(deadline, float(inherited))
+    RUN["deadline"], RUN["budget_s"] = deadline, round(deadline - RUN["t0"], 1)
+    os.environ["PGH_BENCH_DEADLINE"] = repr(deadline)
+
+
+def remaining() -> float:
+    return float("inf") if RUN["deadline"] is None else RUN["deadline"] - time.time()
+
+
+def headline_reserve(args) -> float:
+    if args.headline_reserve_s is not None:
+        return float(args.headline_reserve_s)
+    return 150.0 if args.gpus == 1 else 120.0
+
+
+def stub_sleep(stage: str):
+    """Test hook (tests/test_bench_launch.py): PGH_BENCH_STUB="config4=1000,group=0" replaces the
+    named child runs by a stand-in that sleeps that long and prints a dry-run line."""
+    for item in os.environ.get("PGH_BENCH_STUB", "").split(","):
+        name, _, secs = item.partition("=")
+        if name.strip() == stage:
+            return float(secs or 0)
+    return None
+
+
+def run_child(args, stage: str, cmd, want_s: float, reserve=None, kill="TERM", **kw):
+    """Run one child line under ``timeout -k 10 <limit>`` with limit = min(want_s, what is left of
+    the run's budget minus ``reserve`` (default: the headline's)).  Returns (CompletedProcess or
+    None, error dict or None): a child given less than MIN_CHILD_S is not started, one that hits
+    its limit is reported as a timeout; either way the caller puts the error in the child's slot
+    and the run goes on."""
+    import subprocess
+
+    keep = reserve if reserve is not None else headline_reserve(args)
+    limit = int(min(want_s, remaining() - keep))
+    if limit < MIN_CHILD_S:
+        RUN["stages"][stage] = "skipped"
+        return None, {"error": f"skipped: {max(remaining(), 0):.0f} s of the run's {RUN['budget_s']} s budget left, "
+                               f"{keep:.0f} s kept for the headline", "stage": stage}
+    secs = stub_sleep(stage)
+    if secs is not None:
+        cmd = [sys.executable, "-c", "import json, sys, time; time.sleep(float(sys.argv[1])); "
+               "print(json.dumps({'dry_run': True, 'stub': sys.argv[2]}))", str(secs), stage]
+    env = kw.pop("env", None) or child_env()
+    env["PGH_BENCH_DEADLINE"] = repr(time.time() + limit - 5)  # the child's own watchdog fires first
+    print(f"bench.py: {stage}: {limit} s limit ({remaining():.0f} s of the budget left)", file=sys.stderr, flush=True)
+    RUN["stage"] = stage
+    t = time.time()
+    try:
+        r = subprocess.run(["timeout", "-s", kill, "-k", "10", str(limit)] + list(cmd), cwd=str(ROOT), env=env,
+                           text=True, **kw)
+    except OSError as e:
+        return None, {"error": f"{stage} child did not start: {e}", "stage": stage}
+    finally:
+        RUN["stages"][stage] = round(time.time() - t, 1)
+    if r.returncode in (124, 137) and time.time() - t >= limit - 1:
+        return r, {"error": f"timeout after {limit} s", "stage": stage, "command": " ".join(map(str, cmd[1:]))}
+    return r, None
+
+
+def json_lines(text) -> list:
+    return [ln for ln in (text or "").splitlines() if ln.startswith("{")]
+
+
+def headline_error_line(args, why: str, n_gpus=None) -> dict:
+    """The headline line when the headline could not finish: the contract's keys, value null."""
+    return {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": n_gpus or args.gpus, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32" if args.workload != "resnet18-secagg" else "int64",
+            "data": DATA_DEVICE, "config": {"workload": args.workload}, "roofline": None, "cpu_baseline": None,
+            "error": why, "stage": RUN["stage"]}
+
+
+def emit(rec: dict) -> bool:
+    """Print THE result line (once per process: the watchdog and the normal path race for it)."""
+    with _EMIT:
+        if RUN["printed"]:
+            return False
+        RUN["printed"] = True
+        rec["budget"] = {"budget_s": RUN["budget_s"], "elapsed_s": round(time.time() - RUN["t0"], 1),
+                         "stages_s": dict(RUN["stages"])}
+        print(json.dumps(rec), flush=True)
+        return True
+
+
+def start_watchdog(args, pre: dict):
+    """Print the headline line anyway shortly before the deadline (rank 0; the other ranks just
+    exit a little later), then end the process: a hung collective or a slow stage costs the
+    headline's value, never the whole line."""
+    if RUN["deadline"] is None:
+        return
+    rank = int(os.environ.get("RANK", "0"))
+    margin = WATCHDOG_MARGIN_S if rank == 0 else WATCHDOG_MARGIN_S / 2
+
+    def fire():
+        while remaining() > margin:
+            time.sleep(min(remaining() - margin, 2.0))
+        why = f"stage '{RUN['stage']}' did not finish within the run's {RUN['budget_s']} s budget"
+        done = RUN["printed"]  # the result is out: only the teardown is late
+        if rank == 0 and not done:
+            rec = headline_error_line(args, why)
+            rec.update(pre)
+            emit(rec)
+        print(f"bench.py: {why}; exiting", file=sys.stderr, flush=True)
+        os._exit(0 if done else 3)
+
+    threading.Thread(target=fire, name="pgh-bench-deadline", daemon=True).start()
 
 
 def usable_cores() -> tuple:
@@ -165,20 +299,23 @@ def usable_cores() -> tuple:
 
 
 def spawn_ranks(args) -> int:
-    """``--gpus N`` (N > 1) started without a launcher: start N rank processes of this script with
-    the environment torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE,
-    MASTER_ADDR=127.0.0.1, a free MASTER_PORT) and return the worst exit status.  The parent imports
-    neither torch nor the engine, so it never touches a GPU; if one rank fails the others are
-    stopped (their own PIDs) instead of waiting in a collective forever.  Rank 0's result line is
-    held here; after every rank has exited, the one-process group over the same GPUs runs in a
-    fresh child (``group_line``) and its summary goes onto that line under ``group``."""
+    """``--gpus N`` (N > 1) started without a launcher: run the child lines first (this parent
+    imports neither torch nor the engine, so it never touches a GPU), then start N rank processes
+    of this script with the environment torch.distributed.run would give them (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT) and the run's deadline, and return the
+    worst exit status.  If one rank fails the others are stopped (their own PIDs) instead of
+    waiting in a collective forever, and at the deadline every rank is.  Rank 0's result line
+    (or, failing that, an error line) gets the child lines and is printed here."""
     import socket
     import subprocess
 
+    pre = pre_world_lines(args)
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     procs = []
+    RUN["stage"] = "headline"
+    t = time.time()
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
@@ -187,6 +324,9 @@ def spawn_ranks(args) -> int:
                                       stdout=subprocess.PIPE if r == 0 else None, text=True))
     rc = 0
     live = list(procs)
+    out = []
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()  # rank 0's pipe is drained as it writes
     while live:
         for p in list(live):
             r = p.poll()
@@ -197,22 +337,28 @@ def spawn_ranks(args) -> int:
                 rc = rc or r
                 for q in live:
                     q.terminate()
+        if live and remaining() < 0:  # the ranks' own watchdogs should have ended them by now
+            rc = rc or 124
+            for q in live:
+                q.kill()
         time.sleep(0.05)
     for p in procs:
         p.wait()
-    out = procs[0].stdout.read() if procs[0].stdout else ""
-    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
-    for ln in out.splitlines():
+    reader.join(10)
+    RUN["stages"]["headline"] = round(time.time() - t, 1)
+    text = out[0] if out else ""
+    for ln in text.splitlines():
         if not ln.startswith("{"):
             print(ln, flush=True)
-    if rc != 0 or not lines:
-        return rc or 1
-    rec = json.loads(lines[-1])
-    if wants_group_line(args):
-        rec["group"] = group_line(args)
-    attach_config_lines(args, rec)
-    print(json.dumps(rec), flush=True)
-    return 0
+    lines = json_lines(text)
+    if lines:
+        rec = json.loads(lines[-1])
+        rec.pop("budget", None)
+    else:
+        rec = headline_error_line(args, f"the {args.gpus} ranks exited {rc} without a result line")
+    rec.update(pre)
+    emit(rec)
+    return rc or (1 if rec.get("error") else 0)
 
 
 GROUP_WORKLOADS = {"resnet18-fedavg", "resnet18-iterative", "resnet18-weighted", "resnet18-secagg", "secagg-clients"}
@@ -235,10 +381,10 @@ def wants_group_line(args) -> bool:
 
 def group_line(args, limit_s: int = 300) -> dict:
     """The path the node deploys at N > 1 (its single process drives every GPU through one library
-    context, ``pgh_create_group``), measured on the same GPUs right after
-    the per-rank world has exited: ``bench.py --group --gpus N`` in a FRESH child (no process that
-    touched a GPU re-execs), summarised for the per-rank line.  ``rccl`` says whether the group's
-    exchange ran over RCCL (distinct devices) or peer copies."""
+    context, ``pgh_create_group``), measured on the same GPUs before the
+    per-rank world forms: ``bench.py --group --gpus N`` in a FRESH child (no process that touched a
+    GPU re-execs), summarised for the per-rank line.  ``rccl`` says whether the group's exchange ran
+    over RCCL (distinct devices) or peer copies."""
     import subprocess
 
     cmd = [sys.executable, str(Path(__file__).resolve()), "--group", "--gpus", str(args.gpus), "--workload",
@@ -250,21 +396,19 @@ def group_line(args, limit_s: int = 300) -> dict:
         cmd += ["--clients", str(args.clients)]
     if args.params:
         cmd += ["--params", str(args.params)]
-    env = child_env()
-    print(f"bench.py: one-process group over {args.gpus} GPUs in a fresh child ({limit_s} s limit)", file=sys.stderr,
-          flush=True)
-    try:  # stderr passes through: the child's progress stays visible
-        r = subprocess.run(["timeout", "-k", "10", str(limit_s)] + cmd, cwd=str(ROOT), env=env,
-                           stdout=subprocess.PIPE, text=True)
-    except OSError as e:
-        return {"error": f"group child did not start: {e}"}
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    # stderr passes through: the child's progress stays visible
+    r, err = run_child(args, "group", cmd, limit_s, stdout=subprocess.PIPE)
+    if err:
+        return err
+    lines = json_lines(r.stdout)
     if r.returncode != 0 or not lines:
-        return {"error": f"group child exited {r.returncode} (limit {limit_s} s; its stderr is above)",
+        return {"error": f"group child exited {r.returncode} (its stderr is above)", "stage": "group",
                 "command": " ".join(cmd[1:])}
     g = json.loads(lines[-1])
     if g.get("dry_run"):
         return g
+    if g.get("error"):
+        return {"error": g["error"], "stage": "group", "command": " ".join(cmd[1:])}
     cfg = g.get("config", {})
     out = {"value": g.get("value"), "unit": g.get("unit"), "n_gpus": g.get("n_gpus"),
            "ms_per_step": g.get("ms_per_step"), "kernel_ms": g.get("kernel_ms"),
@@ -278,65 +422,91 @@ def group_line(args, limit_s: int = 300) -> dict:
     return out
 
 
-CONFIG_LINES = {"config4": "c4-stream", "config5": "c5-ingest"}
+# key: (workload, GPUs (None: this run's --gpus), steps cap, with its cpu_baseline).  In run order:
+# the cheap config-1 close first, then the configs only a multi-GPU run exercises in their stated
+# form (4, 5), then config 3 (187.7 GB resident per GPU).
+CONFIG_LINES = {"config1": ("mnist-state", 1, None, True), "config4": ("c4-stream", None, 5, False),
+                "config5": ("c5-ingest", None, 5, False), "config3": ("resnet18-secagg", None, 10, True)}
+FOLD_BYTES_NOTE = {
+    "c5-ingest": "fold batch 2: each fold launch also reads and writes the running state (4 B + 4 B per param "
+                 "per 2 clients), so the fold kernel moves 2x its diff bytes; fold_frac counts those bytes, "
+                 "e2e_frac only the diff bytes (the step is PCIe-bound)",
+    "c4-stream": "value and e2e_frac include the on-device generation of every chunk (4 B written per param per "
+                 "client, alternating with the fold); fold_frac is the fold kernel alone",
+    "resnet18-secagg": "fold_frac: 8*S*N*P + 12*P bytes (shares in; int64 sum and float32 decode out) over the "
+                       "k_secagg launch time; e2e_frac: the share bytes 8*S*N*P over the whole step",
+    "mnist-state": "latency line (bytes in -> bytes out, 3 clients): cycle_close_ms is the figure; fold_frac is "
+                   "the 0.3M-param fold kernel alone",
+}
 
 
 def wants_config_lines(args) -> bool:
-    return args.workload == "resnet18-fedavg" and not args.group and not args.no_config_lines
+    return args.workload == "resnet18-fedavg" and not args.group and not args.no_config_lines and not under_profiler()
 
 
-def config_line(args, workload: str, limit_s: int = 420) -> dict:
-    """BASELINE configs 4 and 5 over the same --gpus as this run, each a fresh child world
-    (``bench.py --gpus N --workload <w> --check``: it forms its own N ranks; no process that touched a
-    GPU re-execs), summarised for this line: what ran (ranks, backend), its throughput and the
-    sampled bit-exact check of the sharded result after the all-gather."""
+def config_line(args, key: str, limit_s: int = 420) -> dict:
+    """One BASELINE config as a fresh child run (``bench.py --gpus N --workload <w> --check``: it
+    forms its own N ranks; no process that touched a GPU re-execs), summarised for this line: what
+    ran (ranks, backend), its value with ``e2e_frac`` = value / (GPUs x HBM peak), the dominant
+    kernel's own roofline fraction ``fold_frac`` (the two differ: FOLD_BYTES_NOTE says how), the
+    bit-exact check and, where the config has one, its cpu_baseline."""
     import subprocess
 
-    cmd = [sys.executable, str(Path(__file__).resolve()), "--gpus", str(args.gpus), "--workload", workload,
-           "--steps", str(min(args.steps, 5)), "--warmup", "1", "--seed", str(args.seed), "--no-cpu-baseline",
-           "--no-live-traffic", "--no-group-line", "--no-config-lines", "--check"]
+    workload, gpus, steps_cap, cpu = CONFIG_LINES[key]
+    gpus = gpus or args.gpus
+    steps = min(args.steps, steps_cap) if steps_cap else args.steps
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--gpus", str(gpus), "--workload", workload,
+           "--steps", str(steps), "--warmup", str(1 if steps_cap else args.warmup), "--seed", str(args.seed),
+           "--no-live-traffic", "--no-group-line", "--no-config-lines", "--check",
+           "--cpu-seconds", str(args.cpu_seconds)]
+    if not cpu or args.no_cpu_baseline:
+        cmd.append("--no-cpu-baseline")
     if args.dry_run:
         cmd.append("--dry-run")
-    env = child_env()
-    print(f"bench.py: {workload} over {args.gpus} GPU(s) in a fresh child world ({limit_s} s limit)", file=sys.stderr,
-          flush=True)
-    try:
-        r = subprocess.run(["timeout", "-k", "10", str(limit_s)] + cmd, cwd=str(ROOT), env=env,
-                           stdout=subprocess.PIPE, text=True)
-    except OSError as e:
-        return {"error": f"{workload} child did not start: {e}"}
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    r, err = run_child(args, key, cmd, limit_s, stdout=subprocess.PIPE)
+    if err:
+        return err
+    lines = json_lines(r.stdout)
     if r.returncode != 0 or not lines:
-        return {"error": f"{workload} child exited {r.returncode} (limit {limit_s} s; its stderr is above)",
+        return {"error": f"{workload} child exited {r.returncode} (its stderr is above)", "stage": key,
                 "command": " ".join(cmd[1:])}
     g = json.loads(lines[-1])
     if g.get("dry_run"):
         return g
-    keep = ("value", "unit", "n_gpus", "steps", "ms_per_step", "pct_hbm_peak_per_gpu", "dist_backend", "rccl_ranks",
-            "check", "fold_kernel_client_diff_GBps_aggregated", "fold_kernel_client_diff_GBps_per_gpu",
-            "ingest_GBps_per_gpu", "bound_by")
+    if g.get("error"):
+        return {"error": g["error"], "stage": key, "command": " ".join(cmd[1:])}
+    keep = ("value", "unit", "n_gpus", "steps", "ms_per_step", "kernel_ms", "cycle_close_ms", "dtype",
+            "pct_hbm_peak_per_gpu", "dist_backend", "rccl_ranks", "check", "fold_kernel_client_diff_GBps_aggregated",
+            "fold_kernel_client_diff_GBps_per_gpu", "ingest_GBps_per_gpu", "bound_by", "cpu_baseline")
     out = {k: g[k] for k in keep if k in g}
-    out["workload"] = (g.get("config") or {}).get("workload")
-    out["parallelism"] = (g.get("config") or {}).get("parallelism")
-    out["frac"] = (g.get("roofline") or {}).get("frac")
+    cfg, roof = g.get("config") or {}, g.get("roofline") or {}
+    out["workload"] = cfg.get("workload")
+    out["parallelism"] = cfg.get("parallelism")
+    if g.get("value") is not None:
+        out["e2e_frac"] = round(g["value"] / (g.get("n_gpus") or gpus) / HBM_PEAK_GBS, 4)
+    out["fold_frac"] = roof.get("frac")
+    out["fold_kernel"] = {k: roof.get(k) for k in ("kernel", "kernel_ms_avg", "alg_bytes_per_launch", "achieved",
+                                                   "launches")}
+    out["fold_bytes_note"] = FOLD_BYTES_NOTE.get(workload)
     out["command"] = " ".join(cmd[1:])
     return out
 
 
 def attach_config_lines(args, rec: dict):
     if wants_config_lines(args):
-        for key, wl in CONFIG_LINES.items():
-            rec[key] = config_line(args, wl)
+        for key in CONFIG_LINES:
+            rec[key] = config_line(args, key)
 
 
-def pre_world_lines(args) -> dict:
-    """The child lines of this run -- the one-process group and the config-4 / config-5 worlds over
-    the same GPUs -- run BEFORE this process, or any rank of its world, touches a GPU: a parent
-    holding a HIP context while its child runs slowed the child's config-4 step by 13 % (176 vs
-    154 ms, profiles/r04g/).  Under torch.distributed.run rank 0 runs them while the other ranks
-    wait on the launcher's store (no GPU touched); at N = 1 this process runs them first.  Ranks
-    this script spawned leave them to their parent (spawn_ranks), which never touches a GPU."""
-    out = {}
+def pre_world_lines(args, out=None) -> dict:
+    """The child lines of this run -- configs 1, 3, 4, 5 and the one-process group over the same
+    GPUs -- run BEFORE this process, or any rank of its world, touches a GPU: a parent holding a
+    HIP context while its child runs slowed the child's config-4 step by 13 % (176 vs 154 ms,
+    profiles/r04g/).  Under torch.distributed.run rank 0 runs them while the other ranks wait on
+    the launcher's store (no GPU touched; the wait ends by the run's deadline); at N = 1, and in
+    the parent that spawns ranks itself, this process runs them first.  Each is limited by the
+    run's budget (run_child).  Fills and returns ``out``."""
+    out = {} if out is None else out
     spawned = os.environ.get("PGH_BENCH_SPAWNED") == "1"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if spawned or args.group or not (wants_group_line(args) or wants_config_lines(args)):
@@ -344,9 +514,9 @@ def pre_world_lines(args) -> dict:
     rank = int(os.environ.get("RANK", "0"))
 
     def run():
+        attach_config_lines(args, out)
         if wants_group_line(args):
             out["group"] = group_line(args)
-        attach_config_lines(args, out)
 
     if world == 1:
         run()
@@ -362,8 +532,10 @@ def pre_world_lines(args) -> dict:
 
     import torch.distributed as dist
 
+    # the other ranks wait no longer than the run's deadline (their watchdog ends them after it)
+    wait_s = max(30.0, remaining())
     store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), is_master=False,
-                          timeout=timedelta(seconds=1800))
+                          timeout=timedelta(seconds=wait_s))
     key = f"pgh_bench_pre_world_{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}"
     if rank == 0:
         try:
@@ -371,11 +543,14 @@ def pre_world_lines(args) -> dict:
         finally:
             store.set(key, "done")
     else:
-        store.wait([key])
+        try:
+            store.wait([key], timedelta(seconds=wait_s))
+        except Exception as e:  # noqa: BLE001 -- go on: rank 0's watchdog still prints the line
+            print(f"bench.py: rank {rank}: no word from rank 0's child lines ({e})", file=sys.stderr, flush=True)
     return out
 
 
-def check_sampled(ctx, args, full, lo: int, hi: int, expected) -> dict:
+def check_sampled(ctx, args, full, lo: int, hi: int, expected, against: str = None) -> dict:
     """``--check``: a checker leg outside the timed region (like cpu_baseline, the only other place
     this script runs the oracle).  Every rank takes its share of a strided 4,096-param sample of
     its own shard [lo, hi) (both edges included) and computes the oracle's values for them from its own
@@ -403,8 +578,51 @@ def check_sampled(ctx, args, full, lo: int, hi: int, expected) -> dict:
     have = full[torch.from_numpy(all_idx).to(full.device)].float().cpu().numpy().view(np.uint32)
     bad = int((have != all_want).sum())
     return {"bit_exact": bad == 0, "mismatches": bad, "params_checked": int(all_idx.size), "ranks": ctx.world,
-            "against": "oracle (coracle.fedavg over the sampled params of every client, from each rank's own inputs)",
+            "against": against or "oracle (coracle.fedavg over the sampled params of every client, from each rank's "
+                                  "own inputs)",
             "after": "all-gather of the sharded new checkpoint" if ctx.world > 1 else "one GPU (no exchange)"}
+
+
+def check_resident(ctx, args, full, mode, dtype, N, S, lo, hi, local_sums=None) -> dict:
+    """``--check`` of the resident configs 2 and 3 (a checker leg outside the timed region): the
+    oracle regenerates every client's diff (or S shares) at a strided 4,096-param sample on the CPU
+    (oracle.synth_diff / synth_shares: the restatement of the on-device generator) and computes
+    the expected values with the C oracle (coracle.fedavg / coracle.secagg); rank 0 compares the
+    new checkpoint (config 3: the decoded sum) after the all-gather bit for bit, and every rank
+    compares its own int64 Z_2^64 sums."""
+    import numpy as np
+
+    from oracle import coracle
+    from oracle import oracle as O
+
+    torch = ctx.torch
+    if dtype == 0:
+        w = np.array([(c % 7 + 1) * 0.5 for c in range(N)], np.float32) if mode == 2 else None
+
+        def expected(idx):
+            u = idx.astype(np.uint64)
+            return coracle.fedavg(mode, np.stack([O.synth_diff(args.seed, c, u) for c in range(N)]),
+                                  O.synth_ckpt(args.seed, u), w)
+        return check_sampled(ctx, args, full, lo, hi, expected,
+                             against=f"oracle (coracle.fedavg mode {mode} over the sampled params of all {N} clients, "
+                                     "regenerated on the CPU)")
+    bad_sums = [0]
+
+    def expected_dec(idx):
+        u = idx.astype(np.uint64)
+        want_s, want_d = coracle.secagg(np.stack([O.synth_shares(args.seed, c, S, u) for c in range(N)]), idx.size)
+        got = local_sums[torch.from_numpy(idx - lo).to(local_sums.device)].cpu().numpy()
+        bad_sums[0] = int((got != want_s).sum())
+        return want_d
+    rec = check_sampled(ctx, args, full, lo, hi, expected_dec,
+                        against=f"oracle (coracle.secagg over the sampled params of all {N} clients x {S} parties, "
+                                "regenerated on the CPU): decoded float32 after the all-gather and every rank's "
+                                "int64 sums")
+    bad = int(ctx.sum_over_ranks(float(bad_sums[0])))
+    if rec is not None:
+        rec["sum_mismatches"] = bad
+        rec["bit_exact"] = bool(rec["bit_exact"] and bad == 0)
+    return rec
 
 
 def cpu_baseline(kind: str, P: int, seed: int, budget_s: float, n: int = 32, all_cores: int = 0):
@@ -512,9 +730,13 @@ def in_reference_allocator(fn: str, kwargs: dict, blobs=None):
                 "for k, v in spec['files'].items():\n"
                 "    kw[k] = [Path(p).read_bytes() for p in v] if isinstance(v, list) else Path(v).read_bytes()\n"
                 "print(json.dumps(getattr(bench, spec['fn'])(**kw)))")
-        r = subprocess.run([sys.executable, "-c", code], cwd=str(ROOT), capture_output=True, text=True,
+        # part of the headline: it may use the budget up to the watchdog's margin
+        r, err = run_child(None, "cpu_baseline", [sys.executable, "-c", code], 600,
+                           reserve=WATCHDOG_MARGIN_S + 5, capture_output=True,
                            input=json.dumps({"fn": fn, "kwargs": kwargs, "files": files}),
-                           env=dict(os.environ, PGH_MALLOC_TUNE="0"), timeout=600)
+                           env=dict(os.environ, PGH_MALLOC_TUNE="0"))
+        if err:
+            raise RuntimeError(f"CPU baseline child: {err['error']}")
         if r.returncode != 0:
             raise RuntimeError(f"CPU baseline child failed: {r.stderr.strip().splitlines()[-1:]}")
         out = json.loads(r.stdout.strip().splitlines()[-1])
@@ -638,17 +860,20 @@ def measure_live_traffic(args, timeout_s=(240, 120)):
 
     tmp = Path(tempfile.mkdtemp(prefix="pgh_pmc_"))
     child = [sys.executable, str(ROOT / "bench.py"), "--workload", args.workload, "--steps", "2", "--warmup", "1",
-             "--no-cpu-baseline", "--no-e2e", "--no-live-traffic", "--seed", str(args.seed)]
+             "--no-cpu-baseline", "--no-e2e", "--no-live-traffic", "--no-config-lines", "--seed", str(args.seed)]
     if args.variant is not None:
         child += ["--variant", str(args.variant)]
     got, alg = {}, None
     try:
         # the first pass may pay a fresh box's first `import torch` (1-2 minutes): a longer limit
         for counter, limit in zip(("FETCH_SIZE", "WRITE_SIZE"), timeout_s):
-            print(f"bench.py: live PMC pass {counter} (rocprofv3 --pmc, {limit} s limit)", file=sys.stderr, flush=True)
-            r = subprocess.run(["timeout", "-s", "KILL", str(limit), prof, "--pmc", counter, "-d",
-                                str(tmp / counter), "-o", "run", "--output-format", "csv", "--"] + child,
-                               cwd=str(ROOT), capture_output=True, text=True)
+            r, err = run_child(args, f"pmc_{counter}", [prof, "--pmc", counter, "-d", str(tmp / counter), "-o", "run",
+                                                        "--output-format", "csv", "--"] + child,
+                               limit, kill="KILL", capture_output=True, env=dict(os.environ))
+            if err:
+                print(f"bench.py: live PMC pass {counter}: {err['error']}; quoting the committed traffic",
+                      file=sys.stderr)
+                return None
             if r.returncode != 0:
                 print(f"bench.py: live PMC pass {counter} failed (rc {r.returncode}); quoting the committed "
                       f"traffic", file=sys.stderr)
@@ -849,6 +1074,10 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
         diff_bytes, dt, kernel = 8 * parties * N * pg, "int64", "k_secagg"
     torch.cuda.synchronize()
     el, st = timed(ctx, step, args.steps, args.warmup, eng)
+    checked = None
+    if args.check:
+        full = og.assemble() if ctx.world > 1 else (out if dtype == 0 else d_out)
+        checked = check_resident(ctx, args, full, mode, dtype, N, parties, lo, hi, s_out if dtype == 1 else None)
     value = diff_bytes * ctx.world * args.steps / el / 1e9
     cfg = {"workload": f"{args.workload}: P_shard={pg} params/GPU x {N} clients"
                        + (f" x {parties} parties int64" if dtype == 1 else " fp32") + ", resident in HBM",
@@ -857,7 +1086,8 @@ def run_resident(ctx, args, eng, mode, dtype, N, parties, pg, P, lo, hi):
                f" + {ctx.coll} all-gather ({args.gather_chunks} ranges, last halved {args.gather_tail}x, overlapped with the fold)" if ctx.world > 1 else ""),
            "kernel_variant": eng.effective_variant(mode if dtype == 0 else 16)}
     rec = record(ctx, args, args.workload, value, el, dt, cfg,
-                 roofline_of(st, args.workload, cfg["kernel_variant"], kernel))
+                 roofline_of(st, args.workload, cfg["kernel_variant"], kernel),
+                 {"check": checked} if args.check else None)
     kind = "secagg" if dtype == 1 else {0: "mean", 1: "iterative", 2: "weighted"}[mode]
     return attach_cpu_baseline(ctx, args, rec, kind, pg)
 
@@ -1042,9 +1272,25 @@ def run_mnist_state(ctx, args, eng):
     from pygrid_amd.state_schema import build_state_fast
     from pygrid_amd.workloads import MNIST_SHAPES
 
-    rng = np.random.default_rng(args.seed)
-    ck = [rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in MNIST_SHAPES]
-    ds = [[rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2) for s in MNIST_SHAPES] for _ in range(3)]
+    golden = None
+    if args.check:
+        # checker leg: the golden fixture's inputs (tests/golden/mnist_synth.json: the oracle's
+        # counter-based generator, seed 1234), so the new checkpoint can be held against its SHA-256
+        import hashlib
+
+        from oracle.gen_golden import mnist_inputs, split
+
+        golden = json.loads((ROOT / "tests" / "golden" / "mnist_synth.json").read_text())
+        flat_d, flat_c = mnist_inputs(golden["seed"], golden["n_clients"])
+        sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
+        if sha(flat_d) != golden["sha256_diffs"] or sha(flat_c) != golden["sha256_ckpt"]:
+            raise SystemExit("bench.py mnist-state --check: the regenerated inputs are not the golden fixture's")
+        ck = split(flat_c, MNIST_SHAPES)
+        ds = [split(d, MNIST_SHAPES) for d in flat_d]
+    else:
+        rng = np.random.default_rng(args.seed)
+        ck = [rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in MNIST_SHAPES]
+        ds = [[rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2) for s in MNIST_SHAPES] for _ in range(3)]
     ck_pb = build_state_fast(ck)
     d_pb = [build_state_fast(d) for d in ds]
     # config 1 hosts a non-iterative plan: the operator's opt-in lets the engine run it as MEAN
@@ -1075,13 +1321,26 @@ def run_mnist_state(ctx, args, eng):
                        "plan's bytes), State bytes -> checkpoint bytes (scan + H2D + fused mean/apply + D2H + "
                        "fresh framing)", "clients": 3, "params_per_gpu": P,
            "params_total": P, "parallelism": "single GPU", "kernel_variant": eng.effective_variant()}
+    extra = {"new_checkpoint_bytes": len(new), "first_close_ms_with_plan_probe": round(first_ms, 3),
+             "note": "latency-bound: host protobuf scan, 3 H2D copies and a 0.3M-param kernel"}
+    if golden is not None:
+        from pygrid_amd.state_schema import parse_state
+
+        flat = np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in parse_state(new)])
+        got = hashlib.sha256(flat.tobytes()).hexdigest()
+        extra["check"] = {"bit_exact": got == golden["sha256_mean"], "sha256_new_checkpoint_params": got,
+                          "params_checked": int(flat.size),
+                          "against": "tests/golden/mnist_synth.json sha256_mean (the oracle's mean of the golden "
+                                     "inputs, pinned by the reference's avg_plan KAT; DESIGN.md section 4)"}
     rec = record(ctx, args, "mnist-state", value, el, "f32", cfg,
-                 roofline_of(st, "mnist-state", eng.effective_variant(), "k_fedavg"),
-                 {"new_checkpoint_bytes": len(new), "first_close_ms_with_plan_probe": round(first_ms, 3),
-                  "note": "latency-bound: host protobuf scan, 3 H2D copies and a 0.3M-param kernel"}, step_is="close")
+                 roofline_of(st, "mnist-state", eng.effective_variant(), "k_fedavg"), extra, step_is="close")
     if not args.no_cpu_baseline:
-        rec["cpu_baseline"] = in_reference_allocator("cpu_baseline_state", {"P": P, "n_target": 3, "budget_s": 4.0},
-                                                     {"ck_pb": ck_pb, "d_pbs": list(d_pb)})
+        try:
+            rec["cpu_baseline"] = in_reference_allocator("cpu_baseline_state",
+                                                         {"P": P, "n_target": 3, "budget_s": 4.0},
+                                                         {"ck_pb": ck_pb, "d_pbs": list(d_pb)})
+        except Exception as e:  # noqa: BLE001
+            rec["cpu_baseline"] = {"error": str(e)}
     return rec
 
 
@@ -1214,13 +1473,10 @@ def run_resnet18_report(ctx, args, eng, N):
     reporters = [w for w in range(N) if w != 0 and rng.random() >= 0.2]
     arrival = [int(w) for w in rng.permutation(reporters)]
     slots, batch = args.ring or N, 8
-    closes, early, at_close, rewinds, pending, spec = [], [], [], [], [], []
+    closes, early, at_close, pending = [], [], [], []
 
     def cycle():
-        inc = IncrementalCycle(eng, numel, slots=slots, fold_batch=batch, checkpoint=ck_pb,
-                               speculate=bool(args.speculate and not args.no_speculate),
-                               lazy=not args.eager_speculate)
-        spec.append(inc.speculate)
+        inc = IncrementalCycle(eng, numel, slots=slots, fold_batch=batch, checkpoint=ck_pb)
         for w in range(N):
             inc.assigned(w)
         for w in arrival:
@@ -1238,12 +1494,11 @@ def run_resnet18_report(ctx, args, eng, N):
         new = inc.close(ck_pb)
         closes.append((time.perf_counter() - t0) * 1e3)
         at_close.append(inc.last_close["n"] - inc.last_close["early"])
-        rewinds.append(inc.rewinds)
         return new
 
     for _ in range(args.warmup):
         cycle()
-    for x in (closes, early, at_close, rewinds, pending):
+    for x in (closes, early, at_close, pending):
         x.clear()
     eng.reset_stats()
     t0 = time.perf_counter()
@@ -1264,11 +1519,9 @@ def run_resnet18_report(ctx, args, eng, N):
              "close_ms_after_last_report_all": [round(c, 3) for c in closes],
              "folded_before_close": int(np.median(early)) if early else 0,
              "rows_folded_at_close": int(np.median(at_close)) if at_close else 0,
-             "speculative_folds": bool(spec and spec[-1]),
              "report_gap_ms": args.report_gap_ms,
              "close_gap_ms": args.close_gap_ms,
              "pending_gpu_ms_at_close": [round(x, 3) for x in pending] if pending else None,
-             "rewinds_per_cycle": float(np.median(rewinds)) if rewinds else 0,
              "h2d_GBps": round(st["h2d_bytes_total"] / (st["h2d_ms_total"] / 1e3) / 1e9, 2) if st["h2d_ms_total"] else None,
              "new_checkpoint_bytes": len(new),
              "note": "PCIe-inclusive whole cycle (reports + close); compare close_ms_after_last_report with "
@@ -1339,11 +1592,9 @@ def report_close(ctx, args, eng, cycles: int = 4, assigned: int = 100):
     ResNet-18 workers, ~20 % never report (worker 0 among them, routes.py:314), the rest in shuffled
     order, each State diff to HBM (and folded) when reported.  Timed: from the last report's
     ``reported`` returning to the new checkpoint bytes ready on the executor thread -- nothing
-    waits between the two, nothing syncs the GPU before the clock starts.  Two arrival patterns
-    (reports `paced` 5 ms apart -- a node handles each report for tens of ms anyway, its DB write
-    included, tools/node_sim.py -- and `back_to_back`) x the product default (certain-only folds
-    since r04) and the opt-in alternatives (speculative folds with / without the peeked close); the
-    headline is the product default, paced.  1 warm-up cycle each."""
+    waits between the two, nothing syncs the GPU before the clock starts.  Two arrival patterns:
+    reports `paced` 5 ms apart (a node handles each report for tens of ms anyway, its DB write
+    included, tools/node_sim.py; the headline) and `back_to_back`.  1 warm-up cycle each."""
     from concurrent.futures import ThreadPoolExecutor
 
     import numpy as np
@@ -1359,15 +1610,12 @@ def report_close(ctx, args, eng, cycles: int = 4, assigned: int = 100):
                                   for s in RESNET18_SHAPES]) for _ in range(4)]
     reporters = [w for w in range(assigned) if w != 0 and rng.random() >= 0.2]
     arms = {}
-    # (arm, IncrementalCycle options): the product default first, then the alternatives
-    kinds = (("default", {}), ("speculative_peek", {"speculate": True, "peek": True}),
-             ("speculative_no_peek", {"speculate": True, "peek": False}))
     with ThreadPoolExecutor(1, thread_name_prefix="executor") as executor:
         for arrival, gap_ms in (("paced", 5.0), ("back_to_back", 0.0)):
-            for kind, opts in kinds:
+            for kind in ("default",):
                 closes, left = [], []
                 for cyc in range(cycles + 1):
-                    inc = IncrementalCycle(eng, numel, slots=assigned, checkpoint=ck_pb, **opts)
+                    inc = IncrementalCycle(eng, numel, slots=assigned, checkpoint=ck_pb)
                     for w in range(assigned):
                         inc.assigned(w)
                     for i, w in enumerate(rng.permutation(reporters)):
@@ -1379,13 +1627,12 @@ def report_close(ctx, args, eng, cycles: int = 4, assigned: int = 100):
                     if cyc:
                         closes.append((time.perf_counter() - t0) * 1e3)
                         left.append(inc.last_close["n"] - inc.last_close["early"])
-                if kind == "default":
-                    default = {"speculate": inc.speculate, "peek": inc.peek_enabled}
                 arms[f"{arrival}_{kind}"] = {"close_ms": round(float(np.median(closes)), 3),
                                             "closes_ms": [round(c, 3) for c in closes],
                                             "rows_left_to_fold_at_close": int(np.median(left))}
     head = arms["paced_default"]
-    return {"close_ms_after_last_report": head["close_ms"], "arms": arms, "default": default,
+    return {"close_ms_after_last_report": head["close_ms"], "arms": arms,
+            "folds": "certain-only (the speculative folds of ABI 6-7 were retired in r05)",
             "assigned": assigned, "reporters": len(reporters), "gpus": ctx.n_gpus,
             "definition": "the reference's trigger: the last report's handler returns, the close runs at once on "
                           "an executor thread (run_task_once, cycle_manager.py:176-178); timed from that return "
@@ -1505,16 +1752,37 @@ def main_group(ctx, args):
     else:
         rec = run_group_resident(ctx, args, eng, mode, dtype, N, parties, Pg)
         if args.workload == "resnet18-fedavg" and not args.no_e2e:
-            rec["cycle_close_e2e"] = e2e_close(ctx, args, eng, N)
-            rec["cycle_close_report_time"] = report_close(ctx, args, eng)
-    print(json.dumps(rec), flush=True)
+            RUN["stage"] = "cycle_close_e2e"
+            rec["cycle_close_e2e"] = e2e_close(ctx, args, eng, N) if time_for("cycle_close_e2e", 40) \
+                else skipped("cycle_close_e2e")
+            RUN["stage"] = "cycle_close_report_time"
+            rec["cycle_close_report_time"] = report_close(ctx, args, eng) \
+                if time_for("cycle_close_report_time", 45) else skipped("cycle_close_report_time")
+    emit(rec)
+    RUN["stage"] = "teardown"
     eng.close()
+
+
+def time_for(stage: str, need_s: float) -> bool:
+    """Whether an optional part of the headline (need_s: its usual duration) still fits before the
+    watchdog; if not it is skipped and the line says so."""
+    if remaining() - WATCHDOG_MARGIN_S >= need_s:
+        return True
+    RUN["stages"][stage] = "skipped"
+    return False
+
+
+def skipped(stage: str) -> dict:
+    return {"skipped": f"{max(remaining(), 0):.0f} s of the run's {RUN['budget_s']} s budget left", "stage": stage}
 
 
 def main():
     args = parse()
+    set_deadline(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.group:
         sys.exit(spawn_ranks(args))  # no launcher: form the N-rank world here (no GPU touched yet)
+    pre = {}
+    start_watchdog(args, pre)
     if not args.no_tune:
         import pygrid_amd
 
@@ -1522,11 +1790,15 @@ def main():
         # queues were requested at import); cpu_baseline children run with glibc's defaults
         PROCESS_TUNING.update(pygrid_amd.tune_process(hw_queues=False))
         PROCESS_TUNING["hw_queues"] = HW_QUEUES
-    pre = pre_world_lines(args)  # child lines first: nothing of this world holds a GPU yet
+    pre_world_lines(args, pre)  # child lines first: nothing of this world holds a GPU yet
     global LIVE_TRAFFIC
     if (args.gpus == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.group and not args.dry_run
             and not args.no_live_traffic and args.workload in PMC_KERNEL and not under_profiler()):
         LIVE_TRAFFIC = measure_live_traffic(args)  # child processes; this one has not touched the GPU yet
+    RUN["stage"] = "headline"
+    t_head = time.time()
+    if stub_sleep("headline"):  # test hook: a headline that cannot finish in time
+        time.sleep(stub_sleep("headline"))
     ctx = Ctx(args)
     if args.dry_run:
         rec = {"dry_run": True, "n_gpus": ctx.n_gpus, "backend": ctx.backend, "group": ctx.group,
@@ -1535,7 +1807,7 @@ def main():
         ctx.close()
         if ctx.rank == 0:
             rec.update(pre)
-            print(json.dumps(rec), flush=True)
+            emit(rec)
         return
     if ctx.group:
         main_group(ctx, args)
@@ -1571,24 +1843,24 @@ def main():
         rec = run_resident(ctx, args, eng, mode, dtype, N, parties, hi - lo, P, lo, hi)
         if args.workload == "resnet18-fedavg" and ctx.world == 1 and not args.no_e2e:
             # the bytes -> bytes close of the same config (BASELINE.md cycle close), beside the kernel line
-            rec["cycle_close_e2e"] = e2e_close(ctx, args, eng, N)
-            rec["cycle_close_report_time"] = report_close(ctx, args, eng)
+            RUN["stage"] = "cycle_close_e2e"
+            rec["cycle_close_e2e"] = e2e_close(ctx, args, eng, N) if time_for("cycle_close_e2e", 40) \
+                else skipped("cycle_close_e2e")
+            RUN["stage"] = "cycle_close_report_time"
+            rec["cycle_close_report_time"] = report_close(ctx, args, eng) \
+                if time_for("cycle_close_report_time", 45) else skipped("cycle_close_report_time")
+    RUN["stage"] = "teardown"
     eng.close()
     del eng
     if ctx.world > 1:
         ctx.torch.cuda.synchronize()
         ctx.torch.cuda.empty_cache()
-        ctx.barrier()  # every rank's slab is freed before the group child allocates on all GPUs
+        ctx.barrier()
     ctx.close()
+    RUN["stages"]["headline"] = round(time.time() - t_head, 1)
     if ctx.rank == 0:
         rec.update(pre)  # measured before this world touched a GPU (pre_world_lines)
-        print(json.dumps(rec), flush=True)
-
-
-def launched_elsewhere() -> bool:
-    """True under torch.distributed.run (the driver's N > 1 launch): rank 0 runs the group line
-    itself.  Ranks this script spawned leave it to their parent (spawn_ranks)."""
-    return int(os.environ.get("WORLD_SIZE", "1")) > 1 and os.environ.get("PGH_BENCH_SPAWNED") != "1"
+        emit(rec)
 
 
 if __name__ == "__main__":

@@ -33,10 +33,11 @@ def _has(rec: dict, sub: dict):
 
 
 def _config_lines(rec: dict, n: int):
-    """Configs 4 and 5 ran as their own N-rank worlds: the ranks, the
-    collective backend and the --check request are on the line."""
-    for key, wl in (("config4", "c4-stream"), ("config5", "c5-ingest")):
-        _has(rec[key], {"dry_run": True, "n_gpus": n, "workload": wl, "dist_backend": "gloo" if n > 1 else None,
+    """Configs 3, 4 and 5 ran as their own N-rank worlds, config 1
+    on one GPU: the ranks, the collective backend and the --check request are on the line."""
+    for key, wl, g in (("config1", "mnist-state", 1), ("config3", "resnet18-secagg", n), ("config4", "c4-stream", n),
+                       ("config5", "c5-ingest", n)):
+        _has(rec[key], {"dry_run": True, "n_gpus": g, "workload": wl, "dist_backend": "gloo" if g > 1 else None,
                         "rccl_ranks": 0, "check": True, "group": False})
 
 
@@ -170,3 +171,53 @@ def test_check_leg_compares_bit_for_bit(monkeypatch):
         return v
     bad = bench.check_sampled(ctx, args, full, 0, 1000, off_by_one_ulp)
     assert not bad["bit_exact"] and bad["mismatches"] == 1
+
+
+def test_headline_printed_inside_the_budget_when_a_child_overruns():
+    """VERDICT r4 next #1, at the driver's N = 8 geometry (torch.distributed.run, 8 ranks, gloo):
+    a config child that sleeps past its limit is killed at it and its slot holds the timeout, the
+    children after it are skipped for lack of budget, and rank 0 still prints the headline line
+    inside --budget-s."""
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PGH_BENCH_STUB"] = "config1=0,config4=1000,config5=0,config3=0,group=0"
+    budget = 75
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", "29531", str(ROOT / "bench.py"),
+                        "--gpus", "8", "--dry-run", "--budget-s", str(budget), "--headline-reserve-s", "35"],
+                       cwd=str(ROOT), env=env, capture_output=True, text=True, timeout=240)
+    wall = time.time() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 8 and rec["dist_backend"] == "gloo"
+    assert rec["config1"] == {"dry_run": True, "stub": "config1"}
+    assert rec["config4"]["error"].startswith("timeout after") and rec["config4"]["stage"] == "config4"
+    for key in ("config5", "config3", "group"):
+        assert rec[key]["error"].startswith("skipped") and rec[key]["stage"] == key, rec[key]
+    assert rec["budget"]["budget_s"] <= budget and rec["budget"]["stages_s"]["config4"] >= 20
+    assert wall < budget + 15, wall  # + the launcher's own start and teardown
+
+
+def test_watchdog_prints_the_headline_line_when_the_headline_cannot_finish():
+    import time
+
+    t0 = time.time()
+    r = _run(["--dry-run", "--no-config-lines", "--budget-s", "25"], {"PGH_BENCH_STUB": "headline=300"}, timeout=120)
+    assert time.time() - t0 < 40
+    assert r.returncode == 3
+    rec = _json_line(r.stdout)
+    assert rec["value"] is None and rec["metric"].startswith("client-diff GB/s") and rec["stage"] == "headline"
+    assert "did not finish within" in rec["error"]
+
+
+def test_spawned_ranks_line_survives_a_hung_headline():
+    """Without a launcher: the parent (no GPU) runs the child lines, spawns the ranks, and prints
+    rank 0's watchdog line with the child lines merged in."""
+    r = _run(["--gpus", "2", "--dry-run", "--budget-s", "50", "--headline-reserve-s", "25"],
+             {"PGH_BENCH_STUB": "config1=0,config4=0,config5=0,config3=0,group=0,headline=300"}, timeout=150)
+    assert r.returncode != 0
+    rec = _json_line(r.stdout)
+    assert rec["value"] is None and "did not finish within" in rec["error"]
+    assert rec["config4"] == {"dry_run": True, "stub": "config4"}
