@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PGH_ABI_VERSION 7
+#define PGH_ABI_VERSION 8
 
 typedef struct pgh_ctx pgh_ctx;
 
@@ -213,46 +213,6 @@ int pgh_fold_slots_finish_resident(pgh_ctx* ctx, int mode, const int32_t* slots,
  * assumed, or a folded worker re-reported (submit_worker_diff overwrites its diff, :162-174):
  * the caller then re-folds every diff in the query's order, bit-identical to the reference. */
 int pgh_fold_slots_restart(pgh_ctx* ctx);
-/* Speculative report-time folds (ABI 6).  The close-time order is only certain up to the first
- * assigned worker that has not reported; pgh_fold_slots_keep folds slots beyond that point into the
- * running state WITHOUT freeing them (their diffs stay in HBM), and pgh_fold_mark saves the running
- * state under `mark` (>= 0; replaces an older state of that id), so that when an earlier worker
- * reports after all -- or re-reports -- pgh_fold_rewind restores the state saved before its
- * position and the folds continue from there, bit-identical to folding in the final order.  The
- * close then folds only the diffs after the last rewind point (pgh_fold_slots_finish_resident).
- * Neither saving nor rewinding copies: a mark keeps the fold-state buffer as it stands (the next
- * fold writes a spare one) and the fold after a rewind reads its state from the mark's buffer.
- * Each mark holds P_shard floats of HBM until pgh_fold_unmark, pgh_reset or pgh_reserve; the
- * weights of PGH_WEIGHTED_MEAN (fold order) are the caller's to set again after a rewind. */
-int pgh_fold_slots_keep(pgh_ctx* ctx, int mode, const int32_t* slots, int n);
-int pgh_fold_mark(pgh_ctx* ctx, int mark);
-int pgh_fold_rewind(pgh_ctx* ctx, int mark);
-int pgh_fold_unmark(pgh_ctx* ctx, int mark);
-/* *busy = 1 while the last slot fold issued is still running (a caller may then leave further
- * speculative folds for later instead of queueing re-folds behind it), else 0.  Never blocks. */
-int pgh_fold_busy(pgh_ctx* ctx, int* busy);
-/* Speculative close (ABI 6).  pgh_fold_peek runs the FINAL pass of the fold state as it stands --
- * ckpt - avg over the clients folded so far, into a buffer of its own -- and copies the result to a
- * pinned host buffer behind it (its own stream: beside the ingest DMAs), without ending the cycle;
- * while the previous peek's copy is still running it does nothing (there is no valid peek then).
- * pgh_peek_patch_state(out) then, if NOTHING changed since (no fold, rewind, restart, weights or
- * checkpoint change), writes this context's payload slices of the framed State message `out`
- * (pgh_state_fresh's framing) from that copy and makes the peeked result the resident checkpoint --
- * exactly as pgh_fold_slots_finish_resident(no slots) + pgh_ckpt_patch_state(out, out) would -- and
- * sets *ok = 1; otherwise *ok = 0 and nothing changes.  A group commits all of its GPUs or none. */
-int pgh_fold_peek(pgh_ctx* ctx, int mode);
-/* pgh_fold_peek, and then a host thread of the context copies the peek's payload slices into the
- * framed message `out` (pgh_state_fresh's framing) as soon as the D2H lands, while the cycle is
- * still open: a pgh_peek_patch_state(out) that commits this peek then only swaps buffers.  `out`
- * must stay valid, and unread by the caller, until the next pgh_fold_peek_into with another output,
- * pgh_peek_patch_state, pgh_ckpt_patch_state, pgh_reset or pgh_destroy returns (each waits for the
- * copy). */
-int pgh_fold_peek_into(pgh_ctx* ctx, int mode, uint8_t* out, size_t n);
-int pgh_peek_patch_state(pgh_ctx* ctx, uint8_t* out, size_t n, int* ok);
-/* ABI 7: *valid = 1 when a peek of the fold state as it stands now exists (the last pgh_fold_peek
- * took one and nothing changed since; a group: every GPU's), else 0 -- e.g. the peek was skipped
- * because the previous one's copy was still running.  Never blocks. */
-int pgh_peek_valid(pgh_ctx* ctx, int* valid);
 
 /* Z_2^64 share sum over all clients x parties, then decode float32(sum) / base**prec.
  * sum_out (int64) and dec_out (float32) are host arrays of P_shard; either may be NULL. */

@@ -106,15 +106,6 @@ SIGNATURES = {
     "pgh_fold_slots": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
     "pgh_fold_slots_finish_resident": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
     "pgh_fold_slots_restart": (_i, [_vp]),
-    "pgh_fold_slots_keep": (_i, [_vp, _i, C.POINTER(C.c_int32), _i]),
-    "pgh_fold_mark": (_i, [_vp, _i]),
-    "pgh_fold_rewind": (_i, [_vp, _i]),
-    "pgh_fold_unmark": (_i, [_vp, _i]),
-    "pgh_fold_busy": (_i, [_vp, C.POINTER(C.c_int)]),
-    "pgh_fold_peek": (_i, [_vp, _i]),
-    "pgh_fold_peek_into": (_i, [_vp, _i, _vp, _sz]),
-    "pgh_peek_patch_state": (_i, [_vp, _vp, _sz, C.POINTER(C.c_int)]),
-    "pgh_peek_valid": (_i, [_vp, C.POINTER(C.c_int)]),
     "pgh_ckpt_download": (_i, [_vp, _vp]),
     "pgh_ckpt_patch_state": (_i, [_vp, C.c_char_p, _sz, _vp]),
     "pgh_secagg": (_i, [_vp, _i, _i, _vp, _vp]),
@@ -146,7 +137,7 @@ SIGNATURES = {
     "pgh_b64_decode_clean": (_i, [_vp, _sz, _vp, _sz, C.POINTER(_sz), _i]),
 }
 
-ABI_VERSION = 7  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
+ABI_VERSION = 8  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
 _LIB = None
 
 

@@ -117,11 +117,6 @@ double now_ms() {
 }
 
 void free_slab(pgh_ctx* c) {
-    peek_job_wait(c);  // the peek thread reads h_peek
-    if (c->peek_stream) (void)hipStreamSynchronize(c->peek_stream);  // a peek's D2H reads d_peek
-    (void)hipFree(c->d_peek); c->d_peek = nullptr;
-    if (c->h_peek) (void)hipHostFree(c->h_peek);
-    c->h_peek = nullptr; c->peek_cap = 0; c->peek_gen = 0;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     if (c->dec) (void)hipStreamSynchronize(c->dec);  // a varint decode writes slab rows
@@ -129,15 +124,10 @@ void free_slab(pgh_ctx* c) {
     (void)hipFree(c->d_slab); c->d_slab = nullptr; c->slab_bytes = 0;
     (void)hipFree(c->d_ckpt); c->d_ckpt = nullptr;
     (void)hipFree(c->d_out); c->d_out = nullptr;
-    c->ckpt_valid = false; ++c->state_gen;
+    c->ckpt_valid = false;
     for (auto& m : c->final_marks) c->rmark_pool.push_back(m.ev);
     c->final_marks.clear();
     (void)hipFree(c->d_acc); c->d_acc = nullptr;
-    for (auto& m : c->fold_marks) (void)hipFree(m.second.buf);
-    c->fold_marks.clear();
-    for (float* b : c->acc_spare) (void)hipFree(b);
-    c->acc_spare.clear();
-    c->acc_src = nullptr;
     (void)hipFree(c->d_uacc); c->d_uacc = nullptr;
     (void)hipFree(c->d_sum); c->d_sum = nullptr;
     (void)hipFree(c->d_dec); c->d_dec = nullptr;
@@ -580,16 +570,6 @@ void clear_marks(pgh_ctx* c) {
     c->marks.clear();
 }
 
-// Forget every saved slot-fold state (and a pending rewind: the caller discards the fold state too).
-// Their buffers become spares; anything still reading them is ordered on c->stream before the next
-// writer (a slot fold on the same stream).
-void drop_fold_marks(pgh_ctx* c) {
-    for (auto& m : c->fold_marks)
-        if (m.second.buf) c->acc_spare.push_back(m.second.buf);
-    c->fold_marks.clear();
-    c->acc_src = nullptr;
-}
-
 // STREAM: the slots of clients up to `last_client` held clients up to last_client - R before;
 // the copy stream waits for the fold that consumed those.
 int order_stream_overwrite(pgh_ctx* c, int64_t last_client) {
@@ -734,7 +714,6 @@ int fold_run(pgh_ctx* c, int kind, int64_t c0, int64_t n, bool final, const Fina
         done += seg;
     } while (done < n);
     RC(record_fold(c, s));
-    ++c->state_gen;
     return record_slab_fold(c, s);
 }
 
@@ -1065,7 +1044,6 @@ void pgh_destroy(pgh_ctx* c) {
     if (c->grp) { pgh_group_api::destroy(c); return; }
     DeviceGuard g(c->device);
     free_slab(c);
-    peek_thread_stop(c);
     for (auto& t : c->pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto e : c->pool) (void)hipEventDestroy(e);
     clear_marks(c);
@@ -1098,9 +1076,6 @@ void pgh_destroy(pgh_ctx* c) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
     if (c->aux) (void)hipStreamDestroy(c->aux);
-    if (c->peek_ev) (void)hipEventDestroy(c->peek_ev);
-    for (auto e : c->peek_piece_ev) (void)hipEventDestroy(e);
-    if (c->peek_stream) (void)hipStreamDestroy(c->peek_stream);
     delete c;
 }
 
@@ -1192,10 +1167,7 @@ int pgh_reset(pgh_ctx* c) {
     for (auto& fe : c->fold_evs) c->fold_ev_pool.push_back(fe.second);
     c->fold_evs.clear();
     clear_marks(c);
-    drop_fold_marks(c);
     release_slot_fold_events(c);  // c->stream is idle (synchronised above)
-    peek_job_wait(c);             // the caller may drop the output a peek is copying into after this
-    ++c->state_gen;
     std::fill(c->slot_client.begin(), c->slot_client.end(), -1);
     c->weights.clear();
     c->weights_on_device = false;
@@ -1275,52 +1247,6 @@ int pgh_sync(pgh_ctx* c) {
 // ---- internals for the multi-GPU group driver (pgh_internal.h) ------------------------------------
 
 namespace pgh_int {
-bool peek_valid(const pgh_ctx* c) { return c->peek_gen != 0 && c->peek_gen == c->state_gen; }
-
-void peek_wait(pgh_ctx* c) { peek_job_wait(c); }
-
-int peek_commit(pgh_ctx* c, const uint8_t* out_frame, size_t n, uint8_t* out) {
-    std::vector<std::pair<size_t, size_t>> spans;
-    RC(state_shard_spans(c, out_frame, n, &spans, "peeked checkpoint frame"));
-    DeviceGuard g(c->device);
-    peek_job_wait(c);
-    bool copied;
-    {
-        std::lock_guard<std::mutex> lk(c->pk_mu);
-        copied = c->pk_done_gen == c->peek_gen && c->pk_done_out == out;
-    }
-    clear_final_marks(c);  // they describe the fold that wrote the old checkpoint buffer
-    if (copied) {  // the peek thread already put this peek's payloads into `out`
-        std::swap(c->d_ckpt, c->d_peek);
-        c->acc_src = nullptr;
-        c->folded = 0;
-        c->st.n_folded = 0;
-        c->slot_mode = -1;
-        c->peek_gen = 0;
-        ++c->state_gen;
-        return PGH_OK;
-    }
-    CK(c, hipEventSynchronize(c->peek_ev));
-    std::vector<OutPiece> pieces;
-    size_t total = 0;
-    for (auto& sp : spans) {
-        pieces.push_back(OutPiece{out + sp.first, sp.second});
-        total += sp.second;
-    }
-    if (total != (size_t)c->pg * 4) return fail(c, PGH_E_ARG, "frame holds %zu payload bytes of this shard, %lld expected",
-                                                 total, (long long)c->pg * 4);
-    scatter_out((const uint8_t*)c->h_peek, 0, total, pieces, *c->pool_copy);
-    std::swap(c->d_ckpt, c->d_peek);  // the peeked result IS the new checkpoint, as after a FINAL fold
-    c->acc_src = nullptr;
-    c->folded = 0;
-    c->st.n_folded = 0;
-    c->slot_mode = -1;
-    c->peek_gen = 0;
-    ++c->state_gen;
-    return PGH_OK;
-}
-
-
 int usable_cpus() {
     static const int n = [] {
         int cpus = 0;
@@ -1390,7 +1316,6 @@ void* vec(pgh_ctx* c, int which) {
     }
 }
 int patch_payloads(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out) {
-    peek_job_wait(c);  // a peek's payload copy may still be writing the same output
     RC(check_dtype(c, PGH_F32));
     if (!tmpl || !out) return fail(c, PGH_E_ARG, "tmpl / out is NULL");
     RC(check_ckpt(c, "pgh_ckpt_patch_state"));

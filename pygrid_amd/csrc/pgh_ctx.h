@@ -6,7 +6,7 @@
 //                   observability, the shared helpers below, the group driver's internals
 //   pgh_ingest.cpp  host bytes -> HBM slab rows (raw, State messages, int64 shares, synthetic)
 //   pgh_reduce.cpp  RESIDENT and STREAM folds, the resident checkpoint, secagg
-//   pgh_slots.cpp   report-time slot folds, saved fold states, the speculative close (peek)
+//   pgh_slots.cpp   report-time slot folds (the certain prefix of the close-time order)
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -177,32 +177,6 @@ struct pgh_ctx {
     hipEvent_t xsync = nullptr;    // caller-stream <-> context-stream ordering
     hipStream_t aux = nullptr;     // second reduction stream: alternate ranges of a split FINAL pass
     hipEvent_t aux_ev = nullptr;
-    // Speculative close (pgh_fold_peek): the FINAL pass of the fold state as it stands, written to
-    // d_out and copied to the pinned h_peek on peek_stream (D2H beside the ingest H2D), valid while
-    // state_gen is unchanged -- every fold, rewind, restart, weight or checkpoint change bumps it.
-    hipStream_t peek_stream = nullptr;
-    hipEvent_t peek_ev = nullptr;
-    // the D2H runs in D2H_PIECE pieces, an event behind each: the peek thread copies a piece out as
-    // soon as it lands (the copy-out overlaps the rest of the D2H instead of following all of it)
-    std::vector<hipEvent_t> peek_piece_ev;
-    size_t peek_pieces = 0;    // pieces of the last peek's D2H
-    float* h_peek = nullptr;   // pinned, peek_cap floats
-    size_t peek_cap = 0;
-    float* d_peek = nullptr;   // [pvec]: the peeked new checkpoint (swapped with d_ckpt on commit)
-    // pgh_fold_peek_into: a host thread waits for the peek's D2H and copies its payload slices into
-    // the caller's framed output while the cycle is still open (the close then only commits)
-    std::thread pk_thread;
-    std::mutex pk_mu;
-    std::condition_variable pk_cv;
-    bool pk_stop = false, pk_busy = false;
-    uint64_t pk_gen = 0;       // peek the posted job copies
-    uint64_t pk_done_gen = 0;  // peek whose payloads are in pk_done_out
-    uint8_t* pk_out = nullptr;
-    const uint8_t* pk_done_out = nullptr;
-    std::vector<std::pair<uint8_t*, size_t>> pk_pieces;
-    std::unique_ptr<CopyPool> pool_peek;
-    uint64_t state_gen = 1;
-    uint64_t peek_gen = 0;  // state_gen the peek was taken at (0: none)
     // The last fold issued on each stream (folds may run on several caller streams at once, e.g.
     // the param ranges of the multi-GPU overlap): the copy stream waits on all before it
     // overwrites slots, and then forgets them (later copies are ordered after those waits).
@@ -312,14 +286,6 @@ struct pgh_ctx {
     int64_t client_base = 0;  // synthetic client k is generated as global client client_base + k
 
     std::vector<int64_t> slot_client;  // client held by each slot and not yet folded, or -1
-    // Saved slot-fold states (pgh_fold_mark / pgh_fold_rewind: speculative report-time folds).  A mark
-    // takes over the d_acc buffer it names (d_acc moves on to a spare one), so neither saving nor
-    // rewinding copies: after a rewind the next slot fold reads its running state from the mark's
-    // buffer (acc_src) and writes d_acc.
-    struct SavedFold { float* buf; int64_t folded; int mode; };
-    std::map<int, SavedFold> fold_marks;
-    std::vector<float*> acc_spare;     // [pvec] fold-state buffers not in use
-    const float* acc_src = nullptr;    // set by a rewind: the running state lives here, not in d_acc
     std::vector<float> weights;
     bool weights_on_device = false;
 
@@ -456,7 +422,6 @@ int order_slot_overwrite(pgh_ctx* c, int slot);
 int order_before_overwrite(pgh_ctx* c);
 int record_fold(pgh_ctx* c, hipStream_t s);
 void clear_marks(pgh_ctx* c);
-void drop_fold_marks(pgh_ctx* c);
 int order_stream_overwrite(pgh_ctx* c, int64_t last_client);
 int record_mark(pgh_ctx* c, hipStream_t s, int64_t upto);
 int join_in(pgh_ctx* c, hipStream_t cs);
@@ -494,9 +459,5 @@ int maybe_fold(pgh_ctx* c, bool force);
 int claim_slot(pgh_ctx* c, int64_t client, int* slot_out);
 int mark_ingested(pgh_ctx* c, int64_t client, int slot);
 int resident_count(pgh_ctx* c, int64_t* n_out);
-
-// ---- the speculative close's copy-out thread (pgh_slots.cpp) --------------------------------------
-void peek_job_wait(pgh_ctx* c);
-void peek_thread_stop(pgh_ctx* c);
 
 }  // namespace pgh_detail

@@ -803,68 +803,6 @@ int fold_restart(pgh_ctx* c) {
     return fan(c, [](int, pgh_ctx* k) -> int { return pgh_fold_slots_restart(k); });
 }
 
-int fold_slots_keep(pgh_ctx* c, int mode, const int32_t* slots, int n) {
-    RC(need_slab(c));
-    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_slots_keep(k, mode, slots, n); });
-}
-
-int fold_mark(pgh_ctx* c, int mark) {
-    RC(need_slab(c));
-    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_mark(k, mark); });
-}
-
-int fold_rewind(pgh_ctx* c, int mark) {
-    RC(need_slab(c));
-    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_rewind(k, mark); });
-}
-
-int fold_busy(pgh_ctx* c, int* busy) {
-    RC(need_slab(c));
-    std::vector<int> b((size_t)G(c)->kids.size(), 0);
-    RC(fan(c, [&](int i, pgh_ctx* k) -> int { return pgh_fold_busy(k, &b[(size_t)i]); }));
-    *busy = 0;
-    for (int x : b) *busy |= x;
-    return PGH_OK;
-}
-
-int fold_peek(pgh_ctx* c, int mode) {
-    RC(need_slab(c));
-    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_peek(k, mode); });
-}
-
-int fold_peek_into(pgh_ctx* c, int mode, uint8_t* out, size_t n) {
-    RC(need_slab(c));
-    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_peek_into(k, mode, out, n); });
-}
-
-int peek_valid(pgh_ctx* c, int* valid) {
-    RC(need_slab(c));
-    if (!valid) return fail(c, PGH_E_ARG, "valid is NULL");
-    *valid = 1;
-    for (pgh_ctx* k : G(c)->kids) *valid &= pgh_int::peek_valid(k) ? 1 : 0;
-    return PGH_OK;
-}
-
-// All children's peeks must still hold, or none is committed (the group's checkpoint stays whole).
-int peek_patch_state(pgh_ctx* c, uint8_t* out, size_t n, int* ok) {
-    RC(need_slab(c));
-    if (!ok || !out) return fail(c, PGH_E_ARG, "out / ok is NULL");
-    *ok = 0;
-    for (pgh_ctx* k : G(c)->kids)
-        if (!pgh_int::peek_valid(k)) {
-            for (pgh_ctx* w : G(c)->kids) pgh_int::peek_wait(w);  // the caller may reuse `out` now
-            return PGH_OK;
-        }
-    RC(fan(c, [&](int, pgh_ctx* k) -> int { return pgh_int::peek_commit(k, out, n, out); }));
-    *ok = 1;
-    return PGH_OK;
-}
-
-int fold_unmark(pgh_ctx* c, int mark) {
-    RC(need_slab(c));
-    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_fold_unmark(k, mark); });
-}
-
 int secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out) {
     pgh_group* g = G(c);
     RC(need_slab(c));

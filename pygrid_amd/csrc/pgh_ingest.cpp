@@ -430,7 +430,7 @@ int pgh_synth_ckpt_device(pgh_ctx* c, uint64_t seed, float* d_ckpt, void* stream
         return PGH_OK;
     }
     if (!c->d_ckpt) return fail(c, PGH_E_STATE, "pgh_reserve has not been called");
-    c->ckpt_valid = false; ++c->state_gen;  // the resident checkpoint is used as scratch here
+    c->ckpt_valid = false;  // the resident checkpoint is used as scratch here
     clear_final_marks(c);
     hipError_t e = pgh::launch_synth_f32(c->d_ckpt, pgh::single_block(c->pvec), c->pvec, 1, c->pg, seed,
                                          pgh::STREAM_CKPT, 0, c->lo, pgh::CKPT_SCALE, s);
@@ -451,7 +451,7 @@ int pgh_set_weights(pgh_ctx* c, const float* w, int n) {
     }
     c->weights.assign(w, w + n);
     c->weights_on_device = false;
-    ++c->state_gen;
+   
     return PGH_OK;
 }
 

@@ -42,12 +42,6 @@ int usable_cpus();
 // Write only this shard's slice of every payload of `tmpl` into `out` (from the resident checkpoint);
 // the caller writes the framing.  Pre-faults the shard's own part of `out` while the first DMA flies.
 int patch_payloads(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out);
-// Speculative close: a peek (pgh_fold_peek) still matches the fold state; commit it -- this shard's
-// payload slices of the framed message `out` from the peek, the peeked result becomes the checkpoint.
-bool peek_valid(const pgh_ctx* c);
-// Wait until the context's peek thread has finished copying into a caller's output.
-void peek_wait(pgh_ctx* c);
-int peek_commit(pgh_ctx* c, const uint8_t* out_frame, size_t n, uint8_t* out);
 }  // namespace pgh_int
 
 // Group driver entry points (pgh_group.cpp), one per public call that a group context accepts.
@@ -72,15 +66,6 @@ int ckpt_download(pgh_ctx* c, float* out);
 int ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out);
 int fold_slots(pgh_ctx* c, int mode, const int32_t* slots, int n, bool finish);
 int fold_restart(pgh_ctx* c);
-int fold_slots_keep(pgh_ctx* c, int mode, const int32_t* slots, int n);
-int fold_mark(pgh_ctx* c, int mark);
-int fold_rewind(pgh_ctx* c, int mark);
-int fold_unmark(pgh_ctx* c, int mark);
-int fold_busy(pgh_ctx* c, int* busy);
-int fold_peek(pgh_ctx* c, int mode);
-int fold_peek_into(pgh_ctx* c, int mode, uint8_t* out, size_t n);
-int peek_patch_state(pgh_ctx* c, uint8_t* out, size_t n, int* ok);
-int peek_valid(pgh_ctx* c, int* valid);
 int secagg(pgh_ctx* c, int base, int prec, int64_t* sum_out, float* dec_out);
 int stream_begin(pgh_ctx* c, int kind, int fold_batch);
 int stream_flush(pgh_ctx* c);

@@ -55,10 +55,10 @@ int pgh_fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out) {
     const double t0 = now_ms();
     const size_t bytes = sizeof(float) * (size_t)c->pg;
     RC(order_before_overwrite(c));
-    c->ckpt_valid = false; ++c->state_gen;
+    c->ckpt_valid = false;
     clear_final_marks(c);
     RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
-    c->ckpt_valid = true; ++c->state_gen;
+    c->ckpt_valid = true;
     RC(pgh_fedavg_device(c, mode, c->d_ckpt, c->d_out, c->stream));
     if (is_pinned(out)) {
         CK(c, hipMemcpyAsync(out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
@@ -83,10 +83,10 @@ int pgh_ckpt_upload(pgh_ctx* c, const float* ckpt, size_t nbytes) {
     DeviceGuard g(c->device);
     RC(order_before_overwrite(c));
     const uint8_t* src = (const uint8_t*)ckpt + (nbytes == whole ? 4 * (size_t)c->lo : 0);
-    c->ckpt_valid = false; ++c->state_gen;
+    c->ckpt_valid = false;
     clear_final_marks(c);
     RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), src, shard, is_pinned(ckpt)));
-    c->ckpt_valid = true; ++c->state_gen;
+    c->ckpt_valid = true;
     return PGH_OK;
 }
 
@@ -100,10 +100,10 @@ int pgh_ckpt_upload_state(pgh_ctx* c, const uint8_t* pb, size_t n) {
     for (auto& sp : spans) pieces.push_back(Piece{pb + sp.first, sp.second});
     DeviceGuard g(c->device);
     RC(order_before_overwrite(c));
-    c->ckpt_valid = false; ++c->state_gen;
+    c->ckpt_valid = false;
     clear_final_marks(c);
     RC(stage_pieces_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), pieces));
-    c->ckpt_valid = true; ++c->state_gen;
+    c->ckpt_valid = true;
     return PGH_OK;
 }
 
@@ -165,7 +165,6 @@ int pgh_ckpt_patch_state(pgh_ctx* c, const uint8_t* tmpl, size_t n, uint8_t* out
     std::vector<std::pair<size_t, size_t>> spans;
     RC(state_shard_spans(c, tmpl, n, &spans, "checkpoint template"));
     DeviceGuard g(c->device);
-    peek_job_wait(c);  // a peek's payload copy may still be writing the same output
     std::vector<CopyPool::Seg> gaps;
     bool ordered = true;
     if (out != tmpl) {  // template bytes outside this shard's payload slices (framing, other shards)
@@ -331,10 +330,10 @@ int pgh_stream_finish(pgh_ctx* c, const float* ckpt, float* out) {
     // d_ckpt, so fold_run's order_after_ingest orders the final fold after it (a pageable
     // pgh_ckpt_upload's last ring DMA can no longer land after this copy)
     RC(order_before_overwrite(c));
-    c->ckpt_valid = false; ++c->state_gen;
+    c->ckpt_valid = false;
     clear_final_marks(c);
     RC(stage_h2d(c, vec_dest(c->d_ckpt, c->pvec, 4), (const uint8_t*)ckpt, bytes, is_pinned(ckpt)));
-    c->ckpt_valid = true; ++c->state_gen;
+    c->ckpt_valid = true;
     RC(pgh_stream_finish_device(c, c->d_ckpt, c->d_out, c->stream));
     CK(c, hipMemcpyAsync(out, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
     CK(c, hipStreamSynchronize(c->stream));

@@ -312,55 +312,6 @@ class Engine:
         keep their diffs, weights must be set again."""
         self._check(self._lib.pgh_fold_slots_restart(self._h), "fold_slots_restart")
 
-    def fold_slots_keep(self, mode: int, slots: Sequence[int]):
-        """Fold ``slots`` into the running state and KEEP their diffs (a later rewind may fold them
-        again: speculative folds past a worker that has not reported yet)."""
-        a = np.ascontiguousarray(slots, dtype=np.int32)
-        self._check(self._lib.pgh_fold_slots_keep(self._h, int(mode), a.ctypes.data_as(C.POINTER(C.c_int32)),
-                                                  a.size), "fold_slots_keep")
-
-    def fold_mark(self, mark: int):
-        """Save the running fold state under ``mark`` (no copy; P_shard floats of HBM until unmarked)."""
-        self._check(self._lib.pgh_fold_mark(self._h, int(mark)), "fold_mark")
-
-    def fold_rewind(self, mark: int):
-        """Restore the fold state saved under ``mark`` (weights must be set again)."""
-        self._check(self._lib.pgh_fold_rewind(self._h, int(mark)), "fold_rewind")
-
-    def fold_unmark(self, mark: int):
-        self._check(self._lib.pgh_fold_unmark(self._h, int(mark)), "fold_unmark")
-
-    def fold_peek(self, mode: int, into=None):
-        """The FINAL pass of the fold state as it stands, copied to the host behind it (async).
-        ``into``: (bytes, address) of a framed output (``state.prepared_fresh_frame``): a library
-        thread also copies the payloads into it while the cycle is still open; the engine keeps
-        the bytes alive until the next peek."""
-        if into is None:
-            self._check(self._lib.pgh_fold_peek(self._h, int(mode)), "fold_peek")
-            return
-        buf, ptr = into
-        self._check(self._lib.pgh_fold_peek_into(self._h, int(mode), C.c_void_p(ptr), len(buf)), "fold_peek_into")
-        self._peek_keep = buf
-
-    def peek_patch_into(self, ptr: int, n: int) -> bool:
-        """If nothing changed since the last fold_peek: write the peeked payloads into the framed
-        message at ``ptr`` (n bytes), make the peeked result the resident checkpoint, return True."""
-        ok = C.c_int(0)
-        self._check(self._lib.pgh_peek_patch_state(self._h, C.c_void_p(ptr), n, C.byref(ok)), "peek_patch_state")
-        return bool(ok.value)
-
-    def peek_valid(self) -> bool:
-        """A peek of the fold state as it stands now exists (the last fold_peek was not skipped)."""
-        v = C.c_int(0)
-        self._check(self._lib.pgh_peek_valid(self._h, C.byref(v)), "peek_valid")
-        return bool(v.value)
-
-    def fold_busy(self) -> bool:
-        """The last slot fold issued is still running (non-blocking)."""
-        b = C.c_int(0)
-        self._check(self._lib.pgh_fold_busy(self._h, C.byref(b)), "fold_busy")
-        return bool(b.value)
-
     def ckpt_download(self) -> np.ndarray:
         out = np.empty(self.p_shard, dtype=np.float32)
         self._check(self._lib.pgh_ckpt_download(self._h, _ptr(out)), "ckpt_download")

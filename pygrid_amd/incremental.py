@@ -15,36 +15,26 @@ diff lives from WHEN it is folded:
   order);
 * the fold follows the assignment order (``assigned(w, key)``, ``key`` = the WorkerCycle row id),
   reporters only, through the slots where the diffs landed (the kernel reads them through a row
-  table).  A position is CERTAIN once every worker assigned before it has reported.  Certain-only
-  folds (default): the certain prefix is folded ``fold_batch`` at a time and freed
-  (``pgh_fold_slots``).  Speculative folds (opt-in, ``speculate=True``: under the reference's
-  trigger, a close right after the last report, they measured slower, profiles/r04b): every
-  reported diff is folded at once (``pgh_fold_slots_keep``: its slot is kept)
-  and the fold state is saved every ``mark_every`` rows and at the certain point
-  (``pgh_fold_mark``); when an earlier worker reports after all, or a kept one re-reports, the fold
-  goes back to the last saved state before its position (``pgh_fold_rewind``) and continues; slots
-  before the last saved state at the certain point are freed.  While the GPU is still busy with the
-  previous fold (``pgh_fold_busy``), or reports arrive less than ``min_gap_ms`` apart, a report is
-  folded with a later one -- or by a timer once no report has come for ``settle_ms``;
+  table).  A position is CERTAIN once every worker assigned before it has reported; the certain
+  prefix is folded ``fold_batch`` at a time and its slots freed (``pgh_fold_slots``).  Nothing is
+  folded past the first worker that has not reported: a diff folded there could land at the wrong
+  position, and undoing that costs more than it saves (the speculative folds and peeked close of
+  ABI 6-7, retired in r05: under the reference's trigger they closed slower, 2.59-2.85 vs 2.21 ms,
+  BENCH_r04 ``cycle_close_report_time.arms``);
 * ``close(checkpoint, order=..., fetch=...)`` takes the AUTHORITATIVE order -- the keys of the
-  completed-WorkerCycle query, as the node's DB returns them -- keeps the early fold up to the last
-  saved state inside its common prefix with that order, and folds the rest of the order from HBM
-  (slots), the host (parked diffs) or the DB (``fetch(w)``: diffs this process never saw, e.g.
-  reported before a restart).  When even that is impossible (the order differs inside the freed
-  prefix, a freed worker re-reported, an assignment arrived behind it) the fold restarts
-  (``pgh_fold_slots_restart``) and re-folds the whole order, the folded diffs fetched from the DB:
-  bit-identical to the reference in every case, early folding is only ever a speedup;
-* speculative close (with speculative folds, ``peek=True``): whenever every reporter is folded, the close's FINAL pass,
-  its D2H and the copy of the payloads into the cycle's prepared output bytes run ahead
-  (``pgh_fold_peek_into``); a close whose order and fold state match that peek only commits it
-  (``pgh_peek_patch_state``), any other close folds and copies as usual.
+  completed-WorkerCycle query, as the node's DB returns them -- keeps the early fold when it is a
+  prefix of that order, and folds the rest of the order from HBM (slots), the host (parked diffs)
+  or the DB (``fetch(w)``: diffs this process never saw, e.g. reported before a restart).  When
+  that is impossible (the order differs inside the folded prefix, a folded worker re-reported, an
+  assignment arrived behind it) the fold restarts (``pgh_fold_slots_restart``) and re-folds the
+  whole order, the folded diffs fetched from the DB: bit-identical to the reference in every case,
+  early folding is only ever a speedup.
 
 Report semantics (``cycle_manager.py:162-174``, ``fl_events.py:257-263``):
 
 * **re-report** before the worker's diff was folded: the new diff replaces the old one (same slot,
-  or the parked copy); after it was folded: the fold goes back to before it if its slot is still
-  kept, else the early fold is stale and ``close`` re-folds from the DB (the reference averages the
-  LATEST diff at the worker's original row position);
+  or the parked copy); after it was folded: the early fold is stale and ``close`` re-folds from the
+  DB (the reference averages the LATEST diff at the worker's original row position);
 * **late report** (after ``close``): accepted and ignored -- the reference stores it and its
   ``complete_cycle`` returns early for a completed cycle (``:186-188``);
 * **a report from a worker this object was not told about** (assigned before a restart):
@@ -55,10 +45,9 @@ Report semantics (``cycle_manager.py:162-174``, ``fl_events.py:257-263``):
   reference's close does (its ``unserialize_model_params`` raises).
 
 Thread safety: the node calls ``reported`` from request handlers and ``close`` from its executor
-thread (``tasks/cycle.py``), and the deferred fold runs on a timer thread, so every method holds
-the cycle's lock (the engine context itself is single-owner) -- except that once ``seal`` (the
-first half of ``close``) has run, ``reported`` / ``assigned`` return without taking it: a handler
-never waits for the close's fold.  A well-formed diff holding non-float32 tensors is accepted (the reference would
+thread (``tasks/cycle.py``), so every method holds the cycle's lock (the engine context itself is
+single-owner) -- except that once ``seal`` (the first half of ``close``) has run, ``reported`` /
+``assigned`` return without taking it: a handler never waits for the close's fold.  A well-formed diff holding non-float32 tensors is accepted (the reference would
 average it with torch's type promotion): the cycle is then declined as a whole -- later reports
 are only recorded, and ``close`` raises ``ModelNotAcceleratedError`` so the node averages the cycle
 with its own code, from its DB.
@@ -72,7 +61,6 @@ import bisect
 import itertools
 import logging
 import threading
-import time
 from typing import Callable, Dict, Hashable, List, Optional, Sequence
 
 from . import state as state_codec
@@ -81,9 +69,6 @@ from .exceptions import AggregationError, ModelNotAcceleratedError, StateParseEr
 
 DEFAULT_HBM_BUDGET = 64 << 30  # bytes of diffs kept in HBM per cycle when `slots` is not given
 MAX_DEFAULT_SLOTS = 4096
-DEFAULT_SPECULATION_BUDGET = 16 << 30  # bytes of HBM for saved fold states (speculative folds)
-MAX_MARKS = 256
-DEFER_LIMIT = 200  # timer re-arms after a report (settle_ms each) before the close is left to fold
 
 log = logging.getLogger(__name__)
 
@@ -95,9 +80,7 @@ def default_slots(P: int, budget: int = DEFAULT_HBM_BUDGET) -> int:
 class IncrementalCycle:
     def __init__(self, engine: Engine, numel, mode: int = MEAN, slots: Optional[int] = None, fold_batch: int = 8,
                  weights_by_worker: Optional[Dict[object, float]] = None, checkpoint: Optional[bytes] = None,
-                 early_fold: bool = True, speculate: Optional[bool] = None,
-                 speculation_budget: int = DEFAULT_SPECULATION_BUDGET, mark_every: int = 8, lazy: bool = True,
-                 min_gap_ms: float = 2.0, peek: bool = True, settle_ms: float = 5.0):
+                 early_fold: bool = True):
         self.engine = engine
         self.mode = mode
         self._numel = tuple(int(n) for n in numel)
@@ -107,31 +90,6 @@ class IncrementalCycle:
             raise AggregationError("report-time aggregation needs at least 2 HBM slots")
         self.fold_batch = max(1, int(fold_batch))
         self.early_fold = bool(early_fold)
-        # saved fold states the speculation may hold in HBM (each P floats); < 2 turns it off
-        self.max_marks = int(min(MAX_MARKS, speculation_budget // max(4 * P, 1)))
-        can = all(hasattr(engine, f) for f in ("fold_slots_keep", "fold_mark", "fold_rewind", "fold_unmark"))
-        # opt-in (r04): under the reference's trigger -- the close right after the last report -- a
-        # certain-only close was faster (profiles/r04b: 2.09 vs 3.7-4.0 ms with the peek, 2.5 without)
-        self.speculate = bool(can and self.max_marks >= 2 and speculate)
-        self.mark_every = max(1, int(mark_every))
-        # speculative folds wait while the GPU is still busy with the previous one (reports arriving
-        # back to back would otherwise queue re-folds that the next report discards)
-        self._lazy = bool(lazy) and hasattr(engine, "fold_busy")
-        self.min_gap_s = max(0.0, float(min_gap_ms)) / 1e3
-        # the timer that folds what lazy skips left waits this long after a report (a close that
-        # follows the last report at once should find the cycle lock free, not a fold in progress)
-        self.settle_s = max(self.min_gap_s, float(settle_ms) / 1e3, 1e-3)
-        # speculative close: the FINAL pass of the fold state peeked ahead (pgh_fold_peek) whenever
-        # every reporter is folded; a close that finds nothing changed commits it
-        self._peek = self.speculate and bool(peek) and hasattr(engine, "fold_peek")
-        self._peeked = None  # (fold length, rewinds) of the last peek
-        self._last_report = None
-        self._hurried = False  # the last report came less than min_gap after the one before
-        self._timer: Optional[threading.Timer] = None  # folds what a lazy skip left once reports pause
-        self._defer_left = 0
-        if speculate and not self.speculate:
-            raise AggregationError("speculative folds need an engine with fold marks and HBM for >= 2 of them "
-                                   f"({self.max_marks} fit in the budget)")
         self._seq = itertools.count()
         self._order: List[object] = []      # assigned workers, sorted by assignment key
         self._keys: List[tuple] = []        # their keys (sorted, parallel to _order)
@@ -144,21 +102,17 @@ class IncrementalCycle:
         self._free: List[int] = list(range(self.slots - 1, -1, -1))
         self._folded: List[object] = []     # in the running fold state, in fold order
         self._folded_set = set()
-        self._base = 0                      # _folded[:_base]: certain, slots freed, never re-folded
-        self._marks: List[tuple] = []       # (fold length, mark id), increasing; the base's first
-        self._mark_ids = itertools.count()
         self._stale: Optional[str] = None   # why the early fold no longer matches the reports
         self._weights_by_worker = weights_by_worker
         self._weights: List[float] = []     # fold order
         self.folded_early = 0
-        self.rewinds = 0
         self.last_close: dict = {}
         self._lock = threading.Lock()
         self._closed = False
         self._close_order: Optional[List] = None  # set by seal(), taken by finish()
         self._declined: Optional[str] = None  # why the engine cannot average this cycle
         # one open cycle per engine: a previous one left open (dropped without close) is abandoned
-        # here, so that its deferred-fold timer cannot touch this cycle's slots
+        # here, so that nothing of it touches this cycle's slots
         prev = getattr(engine, "cycle_owner", None)
         if prev is not None and prev is not self:
             prev.abandon()
@@ -186,10 +140,9 @@ class IncrementalCycle:
             engine.ckpt_owner = self
             self._ckpt = checkpoint
         # the new checkpoint's bytes, framed and faulted in while the cycle is open (the close then
-        # copies into resident pages: with speculative folds there is little fold left to hide that).
-        # The frame is allocated here; certain-only, its page faults (3-5 ms for 47 MB) run on a thread
-        # of its own, off the previous close, which creates this cycle (``finish`` joins it).  With
-        # the peek, at once: every peek from the first report on copies into it.
+        # copies into resident pages).  The frame is allocated here; its page faults (3-5 ms for
+        # 47 MB) run on a thread of its own, off the previous close, which creates this cycle
+        # (``finish`` joins it).
         self._prepared = None
         self._prep_thread: Optional[threading.Thread] = None
         if checkpoint is not None and hasattr(engine, "ckpt_patch_into"):
@@ -199,12 +152,9 @@ class IncrementalCycle:
                 frame = None
             if frame is not None:
                 self._prepared = (checkpoint, frame)
-                if self._peek:
-                    state_codec.prefault(frame)
-                else:
-                    self._prep_thread = threading.Thread(target=state_codec.prefault, args=(frame,),
-                                                         name="pgh-prefault", daemon=True)
-                    self._prep_thread.start()
+                self._prep_thread = threading.Thread(target=state_codec.prefault, args=(frame,),
+                                                     name="pgh-prefault", daemon=True)
+                self._prep_thread.start()
 
     # ---- assignment (cycle_manager.assign, fl_controller.py:131-132) ---------------------------
     def assigned(self, worker, key=None):
@@ -217,8 +167,8 @@ class IncrementalCycle:
                 return
             k = (0, key) if key is not None else (1, next(self._seq))
             i = bisect.bisect_right(self._keys, k)
-            if self._base and i <= bisect.bisect_left(self._keys, self._key_of[self._folded[self._base - 1]]):
-                # behind the freed fold prefix: never folded early; if it reports, close's order
+            if self._folded and i <= bisect.bisect_left(self._keys, self._key_of[self._folded[-1]]):
+                # behind the folded prefix: never folded early; if it reports, close's order
                 # check sees the early prefix is not the DB's prefix and re-folds
                 self._behind.add(worker)
             self._key_of[worker] = k
@@ -244,17 +194,11 @@ class IncrementalCycle:
             if self._weights_by_worker is not None and worker not in self._weights_by_worker:
                 # refused to its sender now, not when a later report folds it
                 raise AggregationError(f"worker {worker!r} reported but has no aggregation weight")
-            now = time.monotonic()
-            self._hurried = self._last_report is not None and now - self._last_report < self.min_gap_s
-            self._last_report = now
-            self._defer_left = DEFER_LIMIT
             if worker in self._folded_set:
-                # its earlier diff is in the fold state: go back to before it (its slot is still
-                # held), or -- when it was folded for good -- the close re-folds from the DB
-                if not self._rewind(self._folded.index(worker)):
-                    self._stale = f"worker {worker!r} re-reported after its diff was folded"
-                    self._reported.add(worker)
-                    return
+                # its earlier diff is in the fold state for good: the close re-folds from the DB
+                self._stale = f"worker {worker!r} re-reported after its diff was folded"
+                self._reported.add(worker)
+                return
             try:
                 self._take(worker, diff)
             except StateParseError:
@@ -336,29 +280,20 @@ class IncrementalCycle:
         return plan, len(plan) if certain is None else certain
 
     def _sync(self):
-        """Bring the fold state up to date with the reports: go back to before the first position
-        that changed, then fold what follows -- every reported diff in HBM when speculating (folded
-        and kept, a mark after each fold), else only the certain ones, ``fold_batch`` at a time
-        (folded and freed).  Slots of certain positions before a mark are freed."""
+        """Fold the certain reporters not folded yet, ``fold_batch`` at a time (folded and freed);
+        parked diffs move into slots as they free up."""
         if self._stale or self._declined or self._closed or not self.early_fold:
             return
         plan, certain = self._plan()
-        target = plan if self.speculate else plan[:certain]
-        common = _common_prefix(self._folded, target)
-        if common < len(self._folded) and not self._rewind(common):
-            return  # the early fold is not the plan's prefix any more: the close re-folds
-        if self.speculate and self._lazy and not self._parked and (self._hurried or self.engine.fold_busy()):
-            # reports arriving faster than a re-fold takes, or the GPU still folding: fold this
-            # report with a later one instead of queueing re-folds the next report throws away;
-            # if none comes within min_gap, a timer folds it (before the close, when that is later)
-            self._defer()
-            return
+        target = plan[:certain]
+        if _common_prefix(self._folded, target) < len(self._folded):
+            return  # the folded prefix is not the plan's prefix any more: the close re-folds
         run: List = []
         for w in target[len(self._folded):]:
             if w not in self._slot_of:
                 if w not in self._parked:
                     break
-                if not self._free and run and not self.speculate:
+                if not self._free and run:
                     self._fold_run(run)  # frees their slots for the parked diff
                     run = []
                 if not (len(self._free) > 1 or self._free and self._is_front(w)):
@@ -371,147 +306,21 @@ class IncrementalCycle:
                     break
                 del self._parked[w]
             run.append(w)
-        if run and (self.speculate or len(run) >= self.fold_batch):
-            self._fold_run(run, certain)
-        if self.speculate:
-            self._advance_base(certain)
-            if self._peek and self._prepared is not None and self._folded and self._folded == plan \
-                    and self._peeked != (len(self._folded), self.rewinds):
-                # every reporter so far is folded: take the close's FINAL pass now, in the background
-                try:
-                    self.engine.fold_peek(self.mode, into=self._prepared[1] if self._prepared[1][1] else None)
-                except AggregationError as e:  # e.g. no HBM for the peek buffer: close the usual way
-                    log.warning("speculative close disabled for this cycle: %s", e)
-                    self._peek = False
-                    return
-                if not hasattr(self.engine, "peek_valid") or self.engine.peek_valid():
-                    self._peeked = (len(self._folded), self.rewinds)
-                else:  # skipped (the previous peek's copy still running): try again once reports pause
-                    self._defer()
+        if len(run) >= self.fold_batch:
+            self._fold_run(run)
 
-    def _defer(self):
-        if self._timer is None and self._defer_left > 0:
-            self._defer_left -= 1
-            self._timer = threading.Timer(self.settle_s, self._deferred)
-            self._timer.daemon = True
-            self._timer.start()
-
-    def _deferred(self):
-        """Timer thread: the reports paused (no new one within min_gap) -- fold what the lazy skips
-        left, as a report arriving then would have; while the GPU is still folding, wait again."""
-        with self._lock:
-            self._timer = None
-            if self._closed or self._stale or self._declined:
-                return
-            if self._last_report is not None and time.monotonic() - self._last_report < self.settle_s:
-                self._defer()  # still arriving
-                return
-            self._hurried = False
-            try:
-                self._sync()
-            except Exception as e:  # noqa: BLE001 -- nobody to raise to: the close re-folds from the DB
-                log.warning("deferred fold failed (%s): the close re-folds this cycle", e)
-                self._stale = f"deferred fold failed: {e}"
-
-    def _cancel_timer(self):
-        if self._timer is not None:
-            self._timer.cancel()
-            self._timer = None
-
-    def _fold_run(self, ws: Sequence, certain: int = 0):
+    def _fold_run(self, ws: Sequence):
         slots = [self._slot_of[w] for w in ws]
         if self.mode == WEIGHTED_MEAN and self._weights_by_worker is not None:
             self._weights.extend(float(self._weights_by_worker[w]) for w in ws)
             self.engine.set_weights(self._weights)
-        if self.speculate:
-            # a saved state at least every `mark_every` rows (a later rewind goes back no further
-            # than that before the position that changed) and one exactly at the certain point,
-            # so that the certain diffs' slots are freed at once
-            n0 = len(self._folded)
-            cuts = sorted({*range(self.mark_every, len(ws), self.mark_every), len(ws)} |
-                          ({certain - n0} if 0 < certain - n0 < len(ws) else set()))
-            i = 0
-            for j in cuts:
-                self.engine.fold_slots_keep(self.mode, slots[i:j])
-                self._folded.extend(ws[i:j])
-                self._folded_set.update(ws[i:j])
-                self._mark()
-                self._advance_base(certain)
-                i = j
-            self.folded_early = len(self._folded)
-            return
-        else:
-            self.engine.fold_slots(self.mode, slots)
-            for w in ws:
-                del self._slot_of[w]
-            self._free.extend(reversed(slots))
+        self.engine.fold_slots(self.mode, slots)
+        for w in ws:
+            del self._slot_of[w]
+        self._free.extend(reversed(slots))
         self._folded.extend(ws)
         self._folded_set.update(ws)
         self.folded_early = len(self._folded)
-        self._base = len(self._folded)
-
-    def _mark(self):
-        n = len(self._folded)
-        if len(self._marks) >= self.max_marks:
-            # first drop the mark whose neighbours are closest (the base's stays), so that at most
-            # max_marks states are ever held
-            at = [m[0] for m in self._marks] + [n]
-            i = min(range(1, len(self._marks)), key=lambda j: at[j + 1] - at[j - 1])
-            self.engine.fold_unmark(self._marks.pop(i)[1])
-        mid = next(self._mark_ids)
-        try:
-            self.engine.fold_mark(mid)
-        except AggregationError as e:  # no HBM for another saved state: keep fewer from now on
-            log.warning("fold state not saved at %d (%s); speculation keeps %d saved states", n, e, len(self._marks))
-            self.max_marks = max(2, len(self._marks))
-            return
-        self._marks.append((n, mid))
-
-    def _advance_base(self, certain: int):
-        """Positions before ``certain`` never change again: free their slots up to the last mark
-        there, which becomes the base (the earliest point a rewind may go back to)."""
-        cert = min(certain, len(self._folded))
-        at = [i for i, (n, _) in enumerate(self._marks) if n <= cert]
-        if not at or self._marks[at[-1]][0] <= self._base:
-            return
-        i = at[-1]
-        new_base = self._marks[i][0]
-        for w in self._folded[self._base:new_base]:
-            slot = self._slot_of.pop(w, None)
-            if slot is not None:
-                self._free.append(slot)
-        for _, mid in self._marks[:i]:
-            self.engine.fold_unmark(mid)
-        del self._marks[:i]
-        self._base = new_base
-
-    def _rewind(self, n: int) -> bool:
-        """Go back to a fold state of at most ``n`` folded diffs (the latest saved one); False when
-        that would need diffs whose slots were freed."""
-        if n >= len(self._folded):
-            return True
-        if n < self._base:
-            return False
-        keep = [m for m in self._marks if m[0] <= n]
-        to = keep[-1][0] if keep else 0
-        if keep:
-            self.engine.fold_rewind(keep[-1][1])
-        else:  # before the first mark: the base is 0 (a mark is the base otherwise)
-            self.engine.fold_restart()
-        for _, mid in self._marks[len(keep):]:
-            self.engine.fold_unmark(mid)
-        del self._marks[len(keep):]
-        del self._folded[to:]
-        self._folded_set = set(self._folded)
-        del self._weights[to:]
-        self.folded_early = len(self._folded)
-        self.rewinds += 1
-        return True
-
-    def _drop_marks(self):
-        for _, mid in self._marks:
-            self.engine.fold_unmark(mid)
-        self._marks = []
 
     # ---- close (cycle_manager.py:217 -> _average_plan_diffs :240-303) ---------------------------
     def close(self, checkpoint: bytes, framing: str = "fresh", order: Optional[Sequence[Hashable]] = None,
@@ -537,7 +346,6 @@ class IncrementalCycle:
             if self._closed:
                 raise AggregationError("cycle already closed")
             self._closed = True
-            self._cancel_timer()
             if self._declined:
                 raise ModelNotAcceleratedError(self._declined)
             if order is None:
@@ -563,12 +371,12 @@ class IncrementalCycle:
     def _needs_fetch(self, order: List) -> bool:
         """Whether folding ``order`` reads any diff through ``fetch``: a stale or re-folded early
         fold, or a row whose diff is not in an HBM slot (parked, never seen; a full slab then also
-        gives up a later slot and re-reads it).  Rows between a rewind's mark and the common prefix
-        keep their slots (speculative folds free slots only before the base)."""
+        gives up a later slot and re-reads it).  ``finish`` reads through ``fetch`` exactly when
+        this is True (its ``fetch`` guard enforces it)."""
         if self._stale:
             return True
         common = _common_prefix(self._folded, order)
-        if common < len(self._folded) and common < self._base:
+        if common < len(self._folded):
             return True
         return any(w not in self._slot_of for w in order[common:])
 
@@ -582,7 +390,7 @@ class IncrementalCycle:
             self._close_order = None
             folded_before = len(self._folded)
             refold = self._stale
-            if not refold and not self._rewind(_common_prefix(self._folded, order)):
+            if not refold and _common_prefix(self._folded, order) < len(self._folded):
                 refold = f"the DB order's first {len(self._folded)} workers are not the ones folded early"
             k = 0 if refold else len(self._folded)
             rest = order if refold else order[k:]
@@ -606,76 +414,88 @@ class IncrementalCycle:
                 self._prep_thread = None
             prep = self._prepared[1] if self._prepared and self._prepared[0] is checkpoint else None
             self._prepared = None
-            # nothing left to fold and the last peek still matches: its result IS the new checkpoint
-            peeked = bool(not refold and not rest and framing == "fresh" and prep is not None and prep[1]
-                          and self._peek and self.engine.peek_patch_into(prep[1], len(prep[0])))
-            if peeked:
-                stats = {"from_hbm": 0, "from_host": 0, "from_db": 0}
-                new = prep[0]
-            else:
-                stats = self._fold_in_order(rest, fetch)
-            self._drop_marks()  # after the FINAL pass: it reads a rewound state from its mark in place
+            stats = self._fold_in_order(rest, fetch)
+            del stats["db_rows"]
             stats.update(refold=bool(refold), reason=refold or None, early=k, n=len(order),
-                         folded_before_close=folded_before, rewinds=self.rewinds, peeked=peeked)
+                         folded_before_close=folded_before)
             self.last_close = stats
-            if not peeked:
-                new = (state_codec.fresh_checkpoint(self.engine, checkpoint, prepared=prep) if framing == "fresh"
-                       else self.engine.ckpt_patch_state(checkpoint))
+            new = (state_codec.fresh_checkpoint(self.engine, checkpoint, prepared=prep) if framing == "fresh"
+                   else self.engine.ckpt_patch_state(checkpoint))
             self.engine.ckpt_owner = self
             self.engine.ckpt_bytes = new
             return new
 
-    def _fold(self, ws: Sequence, final: bool):
-        slots = [self._slot_of.pop(w) for w in ws]
-        if self.mode == WEIGHTED_MEAN and self._weights_by_worker is not None and (ws or final):
-            self._weights.extend(float(self._weights_by_worker[w]) for w in ws)
-            if self._weights:
-                self.engine.set_weights(self._weights)
-        if final:
-            self.engine.fold_slots_finish_resident(self.mode, slots)
-        else:
-            self.engine.fold_slots(self.mode, slots)
-        self._free.extend(reversed(slots))
+    def fetch_plan(self) -> List:
+        """After ``seal``: the workers whose diffs ``finish`` will read through ``fetch``, in the
+        order it reads them -- the rows to read while the DB snapshot still holds (the node reads
+        exactly these under its report gate).  Empty when ``seal`` returned False."""
+        with self._lock:
+            order = self._close_order
+            if order is None:
+                raise AggregationError("fetch_plan() without a successful seal()")
+            refold = self._stale or _common_prefix(self._folded, order) < len(self._folded)
+            return self._fold_in_order(order if refold else order[len(self._folded):], None, dry=True)["db_rows"]
+
+    def _fold(self, ws: Sequence, final: bool, slot_of: dict, free: list, dry: bool):
+        slots = [slot_of.pop(w) for w in ws]
+        if not dry:
+            if self.mode == WEIGHTED_MEAN and self._weights_by_worker is not None and (ws or final):
+                self._weights.extend(float(self._weights_by_worker[w]) for w in ws)
+                if self._weights:
+                    self.engine.set_weights(self._weights)
+            if final:
+                self.engine.fold_slots_finish_resident(self.mode, slots)
+            else:
+                self.engine.fold_slots(self.mode, slots)
+        free.extend(reversed(slots))
         return slots
 
-    def _fold_in_order(self, rest: List, fetch) -> dict:
+    def _fold_in_order(self, rest: List, fetch, dry: bool = False) -> dict:
         """Fold ``rest`` in order and finish into the resident checkpoint, within the slot budget:
         held slots are folded where they stand, other diffs are ingested into free slots; when none
         is free, the pending batch is folded, or -- when the batch is empty and every slot holds a
         later worker's diff -- the slot of the worker needed LAST is given up (its diff is fetched
-        from the DB when its turn comes)."""
+        from the DB when its turn comes).  ``dry``: the same decisions on copies of the slot maps,
+        no engine call and no fetch -- which rows it would read (``fetch_plan``)."""
+        slot_of = dict(self._slot_of) if dry else self._slot_of
+        free = list(self._free) if dry else self._free
         pos = {w: i for i, w in enumerate(rest)}
-        for w in [w for w in self._slot_of if w not in pos]:  # held (or folded and kept), not needed
-            self._free.append(self._slot_of.pop(w))
+        for w in [w for w in slot_of if w not in pos]:  # held, not needed
+            free.append(slot_of.pop(w))
         batch: List = []
-        from_hbm = from_host = from_db = 0
+        db_rows: List = []
+        from_hbm = from_host = 0
         for i, w in enumerate(rest):
-            if w in self._slot_of:
+            if w in slot_of:
                 batch.append(w)
                 from_hbm += 1
                 continue
             diff = self._parked.get(w)
             if diff is None:
-                if fetch is None:
+                if fetch is None and not dry:
                     raise AggregationError(f"worker {w!r}: no diff held here and no fetch= to read it from the DB")
-                diff = fetch(w)
-                from_db += 1
+                db_rows.append(w)
+                if not dry:
+                    diff = fetch(w)
             else:
                 from_host += 1
-            if not self._free:
+            if not free:
                 if batch:
-                    self._fold(batch, final=False)
+                    self._fold(batch, False, slot_of, free, dry)
                     batch = []
                 else:
-                    later = max((x for x in self._slot_of if pos[x] > i), key=pos.__getitem__)
-                    if fetch is None:
+                    later = max((x for x in slot_of if pos[x] > i), key=pos.__getitem__)
+                    if fetch is None and not dry:
                         raise AggregationError(f"slot budget exhausted and no fetch= to re-read {later!r}")
-                    self._free.append(self._slot_of.pop(later))
-            self._to_hbm(w, diff)
-            self._parked.pop(w, None)
+                    free.append(slot_of.pop(later))
+            if dry:
+                slot_of[w] = free.pop()
+            else:
+                self._to_hbm(w, diff)
+                self._parked.pop(w, None)
             batch.append(w)
-        self._fold(batch, final=True)
-        return {"from_hbm": from_hbm, "from_host": from_host, "from_db": from_db}
+        self._fold(batch, True, slot_of, free, dry)
+        return {"from_hbm": from_hbm, "from_host": from_host, "from_db": len(db_rows), "db_rows": db_rows}
 
     def abandon(self):
         """Another user takes the engine (its slab is re-laid): nothing held here survives.  Later
@@ -686,17 +506,10 @@ class IncrementalCycle:
             if self._closed:  # closed (or abandoned) already: its result may be the resident checkpoint
                 return
             self._closed = True
-            self._cancel_timer()
             self._slot_of.clear()
             self._parked.clear()
-            self._marks = []
             if getattr(self.engine, "ckpt_owner", None) is self:
                 self.engine.ckpt_owner = None
-
-    @property
-    def peek_enabled(self) -> bool:
-        """The speculative close (pgh_fold_peek_into) is on for this cycle."""
-        return bool(self._peek)
 
     @property
     def declined(self) -> Optional[str]:

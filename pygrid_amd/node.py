@@ -47,8 +47,13 @@ closes on Flask-Executor's thread, ``tasks/cycle.py:9-25``): a handler never wai
   completed rows and seals the cycle (``IncrementalCycle.seal``) -- the moment the reference's
   query at ``cycle_manager.py:243-250`` reads the diffs.  A re-report lands wholly before the
   snapshot (its diff is the one averaged) or wholly after it (ignored, as by the reference's close
-  that already read the rows).  Only a close that must read diffs from the DB (a re-fold, diffs
-  reported before a restart) keeps the gate until those reads are done;
+  that already read the rows).  A close that must read diffs from the DB (a re-fold, diffs
+  reported before a restart) reads exactly the rows its fold will need while it holds the gate
+  (``IncrementalCycle.fetch_plan``), then releases it before folding; a fold that asks for any
+  other row fails and the cycle closes through the close-time path instead.  Two closes
+  requested inline from two reports at once (a node that calls ``complete_cycle`` from inside
+  ``submit_worker_diff``) cannot both upgrade their report's shared hold: the second fails at once
+  (``GateUpgradeConflict``) instead of waiting for the first, which waits for it;
 * after the seal, reports and assignments of the closing cycle return at once (no cycle lock);
 * the **engine lock** serialises engine users: closes take it (blocking, on the executor); a
   handler that would prepare a cycle's report-time state while a close holds it skips that
@@ -75,6 +80,7 @@ log = logging.getLogger(__name__)
 
 _DECLINED = "declined"   # the engine does not average this cycle (plan / model): the node's code runs
 _ELSEWHERE = "elsewhere"  # report-time state not kept for this cycle: close-time path over the DB rows
+_BUSY = "busy"  # (_cycle_state only) another thread holds the engine: nothing decided for the cycle yet
 
 
 def completed_rows(cm, cycle_id):
@@ -117,7 +123,7 @@ class NodeEngine:
                  report_time: bool = True, close_trigger: str = "reference", deadline: bool = False,
                  keep_checkpoints: int = 4, slots: Optional[int] = None, fold_batch: int = 8,
                  mean_plans: Optional[str] = None, framing: str = "fresh", report_module=None,
-                 pinned_reports: int = 16, speculate: Optional[bool] = None, peek: Optional[bool] = None):
+                 pinned_reports: int = 16):
         if close_trigger not in ("reference", "replay"):
             raise AggregationError(f"close_trigger must be 'reference' or 'replay', not {close_trigger!r}")
         if deadline and close_trigger != "replay":
@@ -134,8 +140,6 @@ class NodeEngine:
         self.deadline = deadline
         self.slots = slots
         self.fold_batch = fold_batch
-        self.speculate = speculate
-        self.peek = peek
         self.framing = framing
         self.store = CheckpointStore(keep=keep_checkpoints) if keep_checkpoints else None
         self.report_module = report_module
@@ -148,8 +152,13 @@ class NodeEngine:
             else None
         self._cycles: Dict[object, object] = {}  # cycle id -> IncrementalCycle | _DECLINED | _ELSEWHERE
         # (worker id, request key) -> (WorkerCycle id, cycle id) of the rows assigned through this
-        # process: a report finds its row without a DB query (rows assigned before a restart: queried)
+        # process: a report finds its row without a DB query (rows assigned before a restart: queried).
+        # Kept per cycle (_assigned_keys), dropped when the cycle closes or loses its report-time state.
         self._assigned: Dict[tuple, tuple] = {}
+        self._assigned_keys: Dict[object, list] = {}
+        # assignments whose handler found the engine busy before the cycle had its state: recorded
+        # into the state when it is made (a cycle just created is built without a rows query)
+        self._pending_assign: Dict[object, list] = {}
         self._owner = None  # the cycle id whose IncrementalCycle holds the engine
         self._lock = threading.RLock()  # the maps above; held only briefly
         self._gate = _Gate()  # reports (shared) vs a close's snapshot of the rows (exclusive)
@@ -157,7 +166,7 @@ class NodeEngine:
         self._hold = threading.local()
         self._patched: list = []
         self.stats = {"closes_report_time": 0, "closes_close_time": 0, "closes_declined": 0, "refolds": 0,
-                      "diffs_from_db": 0, "report_errors": 0, "rewinds": 0}
+                      "diffs_from_db": 0, "report_errors": 0, "gate_conflicts": 0}
 
     # ---- patching ------------------------------------------------------------------------------
     def _patch(self, owner, name, value):
@@ -234,7 +243,7 @@ class NodeEngine:
 
     def uninstall(self):
         with self._lock:
-            self._abandon_others()  # stops their deferred-fold timers: nothing touches the engine after this
+            self._abandon_others()  # nothing of theirs touches the engine after this
         for owner, name, old in reversed(self._patched):
             if old is _MISSING:
                 delattr(owner, name)
@@ -265,32 +274,38 @@ class NodeEngine:
     # ---- report-time state -------------------------------------------------------------------
     def _cycle_state(self, cm, cycle, create: bool = True, fresh: bool = False):
         """The cycle's IncrementalCycle (made on first use, from its DB rows after a restart), or a
-        marker saying why there is none.  None (nothing recorded, retried on the next call) while
-        another thread's close holds the engine: a handler does not wait for it."""
+        marker saying why there is none.  _BUSY (nothing recorded, retried on the next call) while
+        another thread holds the engine -- a close, or this cycle's state being built: a handler
+        does not wait for it."""
         got = self._cycles.get(cycle.id)
         if got is not None or not create:
             return got
         if not self.report_time or getattr(cycle, "is_completed", False):
             return None
         if not self._engine_lock.acquire(blocking=False):
-            return None
-        try:
+            return _BUSY
+        try:  # the engine lock keeps builders and closes apart; self._lock is held only briefly
             with self._lock:
                 got = self._cycles.get(cycle.id)
                 if got is not None:
                     return got
                 if self._owner is not None and self._owner != cycle.id and \
                         isinstance(self._cycles.get(self._owner), IncrementalCycle):
-                    self._cycles[cycle.id] = _ELSEWHERE  # the engine serves another open cycle
+                    self._set_elsewhere(cycle.id)  # the engine serves another open cycle
                     return _ELSEWHERE
-                try:
-                    inc = self._new_cycle(cm, cycle, fresh)
-                except PlanNotAcceleratedError as e:
-                    log.info("cycle %s: %s -- the node averages it", cycle.id, e)
+            try:
+                inc = self._new_cycle(cm, cycle, fresh)
+            except PlanNotAcceleratedError as e:
+                log.info("cycle %s: %s -- the node averages it", cycle.id, e)
+                with self._lock:
                     self._cycles[cycle.id] = _DECLINED
-                    return _DECLINED
+                    self._drop_assigned(cycle.id)
+                return _DECLINED
+            with self._lock:
                 self._cycles[cycle.id] = inc
                 self._owner = cycle.id
+                for row_id, key in self._pending_assign.pop(cycle.id, ()):
+                    self._record_assign(inc, cycle.id, row_id, key)
                 return inc
         finally:
             self._engine_lock.release()
@@ -312,9 +327,9 @@ class NodeEngine:
                            shapes=lambda: _shapes(ckpt))
         self.aggregator._resident = None  # the report-time cycle takes over the engine's slab
         inc = IncrementalCycle(self.engine, numel, mode=mode, slots=self.slots, fold_batch=self.fold_batch,
-                               checkpoint=ckpt, speculate=self.speculate,
-                               **({} if self.peek is None else {"peek": self.peek}))
-        if not fresh:  # after a restart: the rows assigned before it (a cycle just created has none)
+                               checkpoint=ckpt)
+        if not fresh:  # after a restart: the rows assigned before it (a cycle just created has none;
+            # an assignment that lands while this state is built is recorded from _pending_assign)
             for row in _rows(cm, cycle_id=cycle.id):
                 inc.assigned(row.id, key=row.id)
         return inc
@@ -328,7 +343,7 @@ class NodeEngine:
         except Exception as e:  # noqa: BLE001 -- preparing early is an optimisation only
             log.warning("cycle %s: report-time state not prepared (%s); close-time path", cycle.id, e)
             with self._lock:
-                self._cycles[cycle.id] = _ELSEWHERE
+                self._set_elsewhere(cycle.id)
 
     def _task_fn(self):
         """The task ``submit_worker_diff`` hands to ``run_task_once`` (``tasks/cycle.py:28-37``,
@@ -337,11 +352,23 @@ class NodeEngine:
 
     def on_assign(self, cm, cycle, wc, key=None):
         st = self._cycle_state(cm, cycle)
+        if st is _BUSY:
+            with self._lock:
+                st = self._cycles.get(cycle.id)
+                if st is None:  # its state is not made yet: recorded into it when it is
+                    self._pending_assign.setdefault(cycle.id, []).append((wc.id, key))
+                    return
         if isinstance(st, IncrementalCycle):
-            st.assigned(wc.id, key=wc.id)
-            if key is not None and key[0] is not None:
-                with self._lock:
-                    self._assigned[key] = (wc.id, cycle.id)
+            with self._lock:
+                if self._cycles.get(cycle.id) is st:  # not closed or abandoned meanwhile
+                    self._record_assign(st, cycle.id, wc.id, key)
+
+    def _record_assign(self, inc, cycle_id, row_id, key):
+        """(under self._lock) the engine learns the row; the report finds it without a query."""
+        inc.assigned(row_id, key=row_id)
+        if key is not None and key[0] is not None:
+            self._assigned[key] = (row_id, cycle_id)
+            self._assigned_keys.setdefault(cycle_id, []).append(key)
 
     def on_report(self, cm, worker_id, request_key, diff):
         """After the reference's DB write.  Never raises: the response stays the reference's, and a
@@ -374,11 +401,16 @@ class NodeEngine:
             if isinstance(self._cycles.get(cycle.id), IncrementalCycle):
                 model = self.model_manager.get(fl_process_id=cycle.fl_process_id)
                 ckpt = self.model_manager.load(model_id=model.id)
-            self._gate.acquire_exclusive()  # no report is between its DB write and its ingest now
+            try:
+                self._gate.acquire_exclusive()  # no report is between its DB write and its ingest now
+            except GateUpgradeConflict as e:
+                self.stats["gate_conflicts"] += 1
+                log.warning("close of cycle %s not run: %s", cycle.id, e)
+                raise
             try:
                 with self._lock:
                     st = self._cycles.pop(cycle.id, None)
-                    self._assigned = {k: v for k, v in self._assigned.items() if v[1] != cycle.id}
+                    self._drop_assigned(cycle.id)
                     if self._owner == cycle.id:
                         self._owner = None
                     if not isinstance(st, IncrementalCycle) and st != _DECLINED:
@@ -399,11 +431,15 @@ class NodeEngine:
                     model = self.model_manager.get(fl_process_id=cycle.fl_process_id)
                     ckpt = self.model_manager.load(model_id=model.id)
                 rows = completed_rows(cm, cycle.id)
-                by_id = {r.id: r for r in rows}
-                if not st.seal(order=[r.id for r in rows]):
-                    self._gate.release_exclusive()  # every diff the fold needs is in HBM
-                    gated = False
-                new = st.finish(ckpt.value, framing=self.framing, fetch=lambda rid: by_id[rid].diff)
+                blobs = {}
+                if st.seal(order=[r.id for r in rows]):
+                    # the diffs the fold will read from the DB, read now -- as the reference's query
+                    # reads every diff -- so that no re-report lands between the snapshot and them
+                    by_id = {r.id: r for r in rows}
+                    blobs = {rid: by_id[rid].diff for rid in st.fetch_plan()}
+                self._gate.release_exclusive()  # the fold needs no DB row beyond `blobs`
+                gated = False
+                new = st.finish(ckpt.value, framing=self.framing, fetch=_only(blobs))
             except PlanNotAcceleratedError as e:  # incl. ModelNotAcceleratedError: a non-float32 diff
                 log.info("engine declined cycle %s (%s): running the reference averaging", cycle.id, e)
                 fallback = "original"
@@ -425,7 +461,6 @@ class NodeEngine:
             self.stats["closes_report_time"] += 1
             self.stats["refolds"] += int(st.last_close.get("refold", False))
             self.stats["diffs_from_db"] += st.last_close.get("from_db", 0)
-            self.stats["rewinds"] += st.last_close.get("rewinds", 0)
             self.aggregator._resident = None
             finish_cycle(cm, server_config, cycle, self.model_manager, model.id, new)
 
@@ -433,8 +468,35 @@ class NodeEngine:
         for cid, st in list(self._cycles.items()):
             if isinstance(st, IncrementalCycle):
                 st.abandon()
-                self._cycles[cid] = _ELSEWHERE
+                self._set_elsewhere(cid)
         self._owner = None
+
+    def _set_elsewhere(self, cycle_id):
+        self._cycles[cycle_id] = _ELSEWHERE
+        self._drop_assigned(cycle_id)
+
+    def _drop_assigned(self, cycle_id):
+        """Forget the row lookups of a cycle that closes or has no report-time state (its reports
+        then find their row with one query, as after a restart)."""
+        self._pending_assign.pop(cycle_id, None)
+        for k in self._assigned_keys.pop(cycle_id, ()):
+            if self._assigned.get(k, (None, None))[1] == cycle_id:
+                del self._assigned[k]
+
+
+def _only(blobs: dict):
+    """``fetch`` for a finish after the gate was released: the rows read under it, nothing else."""
+    def fetch(rid):
+        try:
+            return blobs[rid]
+        except KeyError:
+            raise AggregationError(f"the fold asked for row {rid!r}, which was not read under the report gate") \
+                from None
+    return fetch
+
+
+class GateUpgradeConflict(AggregationError):
+    """A second close tried to upgrade its report's shared hold while another upgrade was pending."""
 
 
 class _Gate:
@@ -442,13 +504,16 @@ class _Gate:
     waiting close keeps new reports out, so it waits only for the reports already in flight.  A
     close requested synchronously from inside a report (a node that runs ``complete_cycle`` inline
     instead of through the patched ``run_task_once``) upgrades: it waits for the OTHER reports in
-    flight, never for its own handler."""
+    flight, never for its own handler.  One upgrade at a time: two upgraders would each wait for
+    the other's shared hold, so a second one raises ``GateUpgradeConflict`` at once."""
 
     def __init__(self):
         self._cv = threading.Condition(threading.Lock())
         self._shared = 0
         self._exclusive = False
         self._waiting = 0
+        self._upgrading = False  # an upgrade is waiting for, or holds, the exclusive side
+        self._held_by_upgrade = False
         self._mine = threading.local()  # shared holds of this thread
 
     @contextlib.contextmanager
@@ -472,17 +537,27 @@ class _Gate:
     def acquire_exclusive(self):
         mine = getattr(self._mine, "n", 0)
         with self._cv:
+            if mine:
+                if self._upgrading:
+                    raise GateUpgradeConflict("another close is upgrading its report's hold on the report gate")
+                self._upgrading = True
             self._waiting += 1
             try:
                 while self._exclusive or self._shared - mine:
                     self._cv.wait()
+            except BaseException:
+                self._upgrading = self._upgrading and not mine
+                raise
             finally:
                 self._waiting -= 1
             self._exclusive = True
+            self._held_by_upgrade = bool(mine)
 
     def release_exclusive(self):
         with self._cv:
             self._exclusive = False
+            if self._held_by_upgrade:
+                self._upgrading = self._held_by_upgrade = False
             self._cv.notify_all()
 
     @contextlib.contextmanager

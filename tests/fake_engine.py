@@ -27,7 +27,6 @@ class NumpyEngine:
         self.slot = {}
         self.ckpt = None
         self.folded = []      # diffs folded into the running state, in order
-        self.marks = {}       # saved fold states (pgh_fold_mark)
         self.weights = []
         self.calls = []
 
@@ -108,25 +107,6 @@ class NumpyEngine:
         self.folded = []
         self.weights = []
         self.calls.append(("restart",))
-
-    def fold_slots_keep(self, mode, slots):
-        # the slot's diff as it is now goes into the state; a later overwrite of the slot does not
-        # change what was folded (ingest replaces the array object)
-        if len(set(slots)) != len(slots) or any(s not in self.slot for s in slots):
-            raise AggregationError(f"bad slot list {slots}")
-        self.folded.extend(self.slot[s] for s in slots)
-        self.calls.append(("fold_keep", len(slots)))
-
-    def fold_mark(self, m):
-        self.marks[m] = list(self.folded)
-        self.calls.append(("mark", m))
-
-    def fold_rewind(self, m):
-        self.folded = list(self.marks[m])
-        self.calls.append(("rewind", m))
-
-    def fold_unmark(self, m):
-        del self.marks[m]
 
     def ckpt_patch_state(self, template):
         return state.serialize_model_params(template, self.ckpt)

@@ -169,10 +169,9 @@ def test_group_subrange_and_stream(group2):
     assert np.array_equal(bits(got), bits(want))
 
 
-@pytest.mark.parametrize("speculate", [False, True])
-def test_group_report_time_cycle(group2, speculate):
+def test_group_report_time_cycle(group2):
     """IncrementalCycle over a group: shuffled reports with dropouts, folded through the row table
-    on every GPU (speculative folds: marks and rewinds fanned out to every child)."""
+    on every GPU."""
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast, parse_state
 
@@ -183,8 +182,7 @@ def test_group_report_time_cycle(group2, speculate):
     diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in reporters}
     ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
     ck_pb = build_state_fast(ckpt)
-    inc = IncrementalCycle(group2, [int(np.prod(s)) for s in shapes], slots=16, fold_batch=3, checkpoint=ck_pb,
-                           speculate=speculate, mark_every=2, lazy=False)
+    inc = IncrementalCycle(group2, [int(np.prod(s)) for s in shapes], slots=16, fold_batch=3, checkpoint=ck_pb)
     for w in range(n):
         inc.assigned(w)
     for w in rng.permutation(reporters):
@@ -426,8 +424,7 @@ def test_group8_secagg(group8, client_shard, N):
     assert np.array_equal(bits(dec), bits(O.fix_prec_decode(ws)))
 
 
-@pytest.mark.parametrize("speculate", [False, True])
-def test_group8_report_time_cycle(group8, speculate):
+def test_group8_report_time_cycle(group8):
     """Report-time folds fanned out to eight children: shuffled reports, dropouts, a re-report."""
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast, parse_state
@@ -439,8 +436,7 @@ def test_group8_report_time_cycle(group8, speculate):
     diffs = {w: [(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for w in reporters}
     ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
     ck_pb = build_state_fast(ckpt)
-    inc = IncrementalCycle(group8, [int(np.prod(s)) for s in shapes], slots=12, fold_batch=3, checkpoint=ck_pb,
-                           speculate=speculate, mark_every=2, lazy=False)
+    inc = IncrementalCycle(group8, [int(np.prod(s)) for s in shapes], slots=12, fold_batch=3, checkpoint=ck_pb)
     for w in range(n):
         inc.assigned(w)
     order = [int(w) for w in rng.permutation(reporters)]

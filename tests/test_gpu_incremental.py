@@ -14,11 +14,10 @@ def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
-@pytest.mark.parametrize("speculate", [True, False])
 @pytest.mark.parametrize("slots", [3, 8, 32])
 @pytest.mark.parametrize("ckpt_at_start", [False, True])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_incremental_cycle_matches_reference_order(engine, mode, ckpt_at_start, slots, speculate):
+def test_incremental_cycle_matches_reference_order(engine, mode, ckpt_at_start, slots):
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast, parse_state
 
@@ -32,9 +31,7 @@ def test_incremental_cycle_matches_reference_order(engine, mode, ckpt_at_start, 
     ckpt_pb = build_state_fast(ckpt)
     inc = IncrementalCycle(engine, [int(np.prod(s)) for s in shapes], mode=mode, slots=slots, fold_batch=2,
                            weights_by_worker=weights if mode == 2 else None,
-                           checkpoint=ckpt_pb if ckpt_at_start else None, speculate=speculate, mark_every=3,
-                           lazy=False)
-    assert inc.speculate == speculate
+                           checkpoint=ckpt_pb if ckpt_at_start else None)
     for w in range(n_assigned):
         inc.assigned(w)
     order = list(reporters)
@@ -85,15 +82,11 @@ def test_shared_engine_resident_checkpoint_is_not_trusted_after_another_user(eng
         assert np.array_equal(bits(got), bits(w))
 
 
-@pytest.mark.parametrize("speculate", [False, "eager", "lazy"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_dropouts_at_position_zero_shuffled_arrival(engine, mode, speculate):
+def test_dropouts_at_position_zero_shuffled_arrival(engine, mode):
     """routes.py:314: ~20 % of assigned workers never report, here including the very first one,
-    so nothing is ever certain before close.  Certain-only folds: every reporter waits in its HBM
-    slot and close folds them through the row table (> ROWTAB_MAX rows: several indexed launches).
-    Speculative folds: every report is folded as it arrives, rewound to a saved state whenever an
-    earlier worker reports after it (marks thinned to the budget), and close only finishes --
-    bit-exact either way."""
+    so nothing is ever certain before close: every reporter waits in its HBM slot and close folds
+    them through the row table (> ROWTAB_MAX rows: several indexed launches), bit-exact."""
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast, parse_state
 
@@ -105,22 +98,14 @@ def test_dropouts_at_position_zero_shuffled_arrival(engine, mode, speculate):
     weights = {w: float(rng.uniform(0.5, 3.0)) for w in range(n_assigned)}
     ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
     ckpt_pb = build_state_fast(ckpt)
-    P = sum(int(np.prod(s)) for s in shapes)
     inc = IncrementalCycle(engine, [int(np.prod(s)) for s in shapes], mode=mode, slots=n_assigned, fold_batch=8,
-                           weights_by_worker=weights if mode == 2 else None, checkpoint=ckpt_pb,
-                           speculate=bool(speculate), speculation_budget=24 * 4 * P, lazy=speculate == "lazy")
+                           weights_by_worker=weights if mode == 2 else None, checkpoint=ckpt_pb)
     for w in range(n_assigned):
         inc.assigned(w)
     for w in rng.permutation(reporters):
         inc.reported(int(w), build_state_fast(diffs[int(w)]))
-    assert inc.n_parked == 0
-    if speculate == "eager":
-        assert inc.n_folded == len(reporters)
-    elif not speculate:
-        assert inc.n_folded == 0
+    assert inc.n_parked == 0 and inc.n_folded == 0
     new = inc.close(ckpt_pb)
-    if speculate == "eager":
-        assert inc.last_close["early"] == len(reporters) and inc.rewinds > 0
     ref = [diffs[w] for w in sorted(reporters)]
     if mode == 0:
         want = O.fedavg_mean(ckpt, ref)
@@ -191,72 +176,3 @@ def test_slot_folds_tiny_and_ragged_shapes(engine, mode, shapes):
             O.fedavg_weighted(ckpt, ref, np.array([weights[w] for w in sorted(reporters)], F)))
     for got, w in zip(parse_state(new), want):
         assert np.array_equal(bits(got), bits(w))
-
-
-@pytest.mark.parametrize("P", [1000, 300_007, 2_000_000])
-@pytest.mark.parametrize("mode", [0, 1, 2])
-def test_fold_marks_random_sequences(engine, mode, P):
-    """pgh_fold_slots_keep / pgh_fold_mark / pgh_fold_rewind / pgh_fold_unmark in random sequences
-    (marks replaced, rewound twice, dropped while a rewind is pending, marks of an empty state),
-    finished into the resident checkpoint -- bit-exact against the oracle's fold of the sequence
-    the marks imply.  Sizes cover the auto variants of the row-table fold."""
-    rng = np.random.default_rng(900 + mode + P % 97)
-    N = 12
-    d = (rng.standard_normal((N, P)) * 1e-2).astype(F)
-    c = rng.standard_normal(P).astype(F)
-    w = rng.uniform(0.5, 2.0, N).astype(F)
-    slot_of = [int(x) for x in rng.permutation(N)]
-    for trial in range(4):
-        engine.set_layout([P])
-        engine.reserve(N)
-        engine.ckpt_upload(c)
-        for k in range(N):
-            engine.ingest(slot_of[k], d[k])
-        state, marks = [], {}
-        for step in range(int(rng.integers(4, 12))):
-            op = rng.random()
-            if op < 0.45:  # keep-fold a few clients not in the state yet
-                rest = [k for k in range(N) if k not in state]
-                ks = [int(x) for x in rng.permutation(rest)[:int(rng.integers(1, 4))]] if rest else []
-                if ks:
-                    if mode == 2:
-                        engine.set_weights(w[state + ks])
-                    engine.fold_slots_keep(mode, [slot_of[k] for k in ks])
-                    state = state + ks
-            elif op < 0.7:
-                m = int(rng.integers(0, 4))
-                engine.fold_mark(m)
-                marks[m] = list(state)
-            elif op < 0.9 and marks:
-                m = int(rng.choice(list(marks)))
-                engine.fold_rewind(m)
-                state = list(marks[m])
-            elif marks:
-                m = int(rng.choice(list(marks)))
-                engine.fold_unmark(m)
-                del marks[m]
-        rest = [k for k in range(N) if k not in state][:int(rng.integers(0 if state else 1, 4))]
-        if mode == 2:
-            engine.set_weights(w[state + rest])
-        engine.fold_slots_finish_resident(mode, [slot_of[k] for k in rest])
-        seq = state + rest
-        want = coracle.fedavg(mode, d[seq], c, w[seq] if mode == 2 else None)
-        assert np.array_equal(bits(engine.ckpt_download()), bits(want)), (trial, seq)
-
-
-def test_fold_mark_api_edges(engine):
-    from pygrid_amd.exceptions import AggregationError
-
-    engine.set_layout([256])
-    engine.reserve(4)
-    with pytest.raises(AggregationError):
-        engine.fold_rewind(7)      # never saved
-    with pytest.raises(AggregationError):
-        engine.fold_unmark(7)
-    with pytest.raises(AggregationError):
-        engine.fold_mark(-1)
-    engine.fold_mark(0)            # an empty state: rewinding to it starts the fold over
-    engine.fold_rewind(0)
-    engine.reset()                 # drops saved states
-    with pytest.raises(AggregationError):
-        engine.fold_rewind(0)

@@ -47,18 +47,16 @@ def test_close_time_knobs(monkeypatch, env):
             _check(CycleAggregator(eng).average_plan_diffs({}, ck_pb, d_pbs), O.fedavg_mean(ckpt, diffs))
 
 
-@pytest.mark.parametrize("speculate", [False, True])
-def test_report_time_close_in_output_ranges(speculate):
+def test_report_time_close_in_output_ranges():
     """The report-time close's FINAL pass runs as ranges of 4 MiB of output on one stream, the D2H
     pieces behind them (no knob since r04): a 1.1 M-param shard (two ranges, the second short)
-    closes bit-exact, with and without speculative folds."""
+    closes bit-exact."""
     from pygrid_amd import Engine
     from pygrid_amd.incremental import IncrementalCycle
 
     ckpt, diffs, ck_pb, d_pbs = _case(911, n=6)
     with Engine(0) as eng:
-        inc = IncrementalCycle(eng, [int(np.prod(s)) for s in SHAPES], slots=8, checkpoint=ck_pb,
-                               speculate=speculate, lazy=False)
+        inc = IncrementalCycle(eng, [int(np.prod(s)) for s in SHAPES], slots=8, checkpoint=ck_pb)
         for w in range(7):
             inc.assigned(w)
         for w in (5, 1, 3, 0, 2, 4):  # worker 6 never reports

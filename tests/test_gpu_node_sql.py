@@ -33,16 +33,15 @@ def mnist_diff(worker, version=0):
 
 
 @pytest.mark.parametrize("slots", [None, 2], ids=["slots-default", "slots-2"])
-@pytest.mark.parametrize("speculate", [False, True], ids=["certain-only", "speculative"])
 @pytest.mark.parametrize("threaded", [False, True], ids=["sync", "executor"])
-def test_installed_sql_node_with_pinned_reports_on_the_gpu(tmp_path, engine, speculate, slots, threaded):
+def test_installed_sql_node_with_pinned_reports_on_the_gpu(tmp_path, engine, slots, threaded):
     def fresh_engine():  # a (re)started node process has nothing resident in HBM
         engine.reset()
         engine.ckpt_owner = None
         return engine
 
     eng = run_both(tmp_path, script_three_cycles, engine=fresh_engine, ckpt=mnist_ckpt(), diff_fn=mnist_diff,
-                   threaded=threaded, pinned_reports=4, speculate=speculate, slots=slots)
+                   threaded=threaded, pinned_reports=4, slots=slots)
     st = eng.stats
     assert st["closes_report_time"] == 3 and st["closes_close_time"] == 0 and st["report_errors"] == 0, st
     gc.collect()
@@ -52,8 +51,7 @@ def test_installed_sql_node_with_pinned_reports_on_the_gpu(tmp_path, engine, spe
     assert CFG["num_cycles"] == 3
 
 
-@pytest.mark.parametrize("speculate", [False, True], ids=["certain-only", "speculative"])
-def test_installed_sql_node_on_a_group(tmp_path, speculate):
+def test_installed_sql_node_on_a_group(tmp_path):
     """The same node on a one-process group of two children sharing GPU 0 (what a node with
     several GPUs installs: ``install(devices=[...])``): each report's payload slices go to their
     child, every child folds its shard, the close frames one checkpoint -- byte-identical to the
@@ -67,15 +65,14 @@ def test_installed_sql_node_on_a_group(tmp_path, speculate):
             return grp
 
         eng = run_both(tmp_path, script_three_cycles, engine=fresh_group, ckpt=mnist_ckpt(), diff_fn=mnist_diff,
-                       pinned_reports=4, speculate=speculate)
+                       pinned_reports=4)
         st = eng.stats
         assert st["closes_report_time"] == 3 and st["report_errors"] == 0, st
     gc.collect()
     assert [(p.hits, p.misses, p.blocks) for p in eng.pools] == [(12, 0, 0), (2, 0, 0)]
 
 
-@pytest.mark.parametrize("speculate", [False, True], ids=["certain-only", "speculative"])
-def test_randomised_scripts_on_the_gpu_sql_node(tmp_path, engine, speculate):
+def test_randomised_scripts_on_the_gpu_sql_node(tmp_path, engine):
     """tests/test_node_sql.py's random scripts on the GPU engine with page-locked report blocks and
     the close on an executor thread: byte-identical checkpoints and DB diffs."""
     def fresh_engine():
@@ -86,6 +83,6 @@ def test_randomised_scripts_on_the_gpu_sql_node(tmp_path, engine, speculate):
     for trial in range(4):
         script, slots = random_script(600 + trial, f"g{trial}")
         eng = run_both(tmp_path / f"t{trial}", script, engine=fresh_engine, ckpt=mnist_ckpt(), diff_fn=mnist_diff,
-                       threaded=True, pinned_reports=4, speculate=speculate, slots=slots)
+                       threaded=True, pinned_reports=4, slots=slots)
         st = eng.stats
         assert st["closes_report_time"] == 3 and st["report_errors"] == 0, (trial, st)

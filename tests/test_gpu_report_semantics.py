@@ -36,9 +36,8 @@ def _check(new_pb, ckpt, rows, mode, weights=None):
         assert np.array_equal(bits(g), bits(w))
 
 
-@pytest.mark.parametrize("speculate", [False, True])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_re_reports_before_and_after_the_fold(engine, mode, speculate):
+def test_re_reports_before_and_after_the_fold(engine, mode):
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast
 
@@ -50,8 +49,7 @@ def test_re_reports_before_and_after_the_fold(engine, mode, speculate):
     ck = build_state_fast(ckpt)
     wts = {w: float(rng.uniform(0.5, 2)) for w in workers}
     inc = IncrementalCycle(engine, [int(np.prod(s)) for s in SHAPES], mode=mode, slots=4, fold_batch=1,
-                           weights_by_worker=wts if mode == 2 else None, checkpoint=ck, speculate=speculate,
-                           lazy=False)
+                           weights_by_worker=wts if mode == 2 else None, checkpoint=ck)
     for w in workers:
         inc.assigned(w, key=w)
     latest = {}

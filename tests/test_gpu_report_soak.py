@@ -1,7 +1,8 @@
 """GPU soak of report-time aggregation at a size where every mechanism engages: a >= 1 M-param model
-(the close's FINAL pass in ranges), reports arriving in random bursts and pauses (lazy skips, the
-deferred-fold timer, speculative folds, rewinds, peeks and their background copies), re-reports
-before and after their fold, dropouts, and closes at once or after a pause, in the DB's order.
+(the close's FINAL pass in ranges), reports arriving in random bursts and pauses, certain prefixes
+folded early, re-reports before and after their fold (re-folds read through the close's fetch
+plan, as the node does under its report gate), dropouts, and closes at once or after a pause, in
+the DB's order.
 Every cycle's new checkpoint is bit-exact against the oracle's fold in that order (reference:
 cycle_manager.py:243-296), chained over cycles through the resident checkpoint."""
 import time
@@ -34,14 +35,14 @@ def test_random_bursts_pauses_and_rereports_stay_bit_exact(mode, devices):
     ckpt = [rng.standard_normal(s).astype(F) for s in SHAPES]
     ck = build_state_fast(ckpt)
     want = ckpt
-    stats = {"peeked": 0, "rewinds": 0, "refold": 0}
+    stats = {"folded_early": 0, "from_db": 0, "refold": 0}
     with (Engine(devices=devices) if devices else Engine(0)) as eng:
         for cyc in range(5):
-            inc = IncrementalCycle(eng, numel, mode=mode, slots=n + 2, checkpoint=ck, speculate=True,
+            inc = IncrementalCycle(eng, numel, mode=mode, slots=n + 2, checkpoint=ck, fold_batch=2,
                                    weights_by_worker=weights if mode == 2 else None)
             for w in range(n):
                 inc.assigned(w)
-            reporters = [w for w in range(n) if rng.random() >= 0.2]
+            reporters = [w for w in range(n) if w < 6 or rng.random() >= 0.2]  # a certain prefix
             latest = {}
             events = [int(w) for w in rng.permutation(reporters)]
             events += [int(w) for w in rng.choice(reporters, size=3, replace=False)]  # re-reports
@@ -52,9 +53,11 @@ def test_random_bursts_pauses_and_rereports_stay_bit_exact(mode, devices):
                 time.sleep(float(rng.choice([0.0, 0.0005, 0.003, 0.008])))
             time.sleep(float(rng.choice([0.0, 0.002, 0.012])))
             order = sorted(latest)  # the completed-WorkerCycle rows in row (assignment) order
-            new = inc.close(ck, order=order, fetch=lambda w: build_state_fast(latest[w]))
-            stats["peeked"] += int(inc.last_close["peeked"])
-            stats["rewinds"] += inc.last_close["rewinds"]
+            plan = inc.fetch_plan() if inc.seal(order=order) else []
+            blobs = {w: build_state_fast(latest[w]) for w in plan}  # the rows read under the gate
+            new = inc.finish(ck, fetch=blobs.__getitem__)
+            stats["folded_early"] += inc.last_close["early"]
+            stats["from_db"] += inc.last_close["from_db"]
             stats["refold"] += int(inc.last_close["refold"])
             rows = [latest[w] for w in order]
             want = (O.fedavg_mean(want, rows) if mode == 0 else O.fedavg_iterative(want, rows) if mode == 1
@@ -66,3 +69,4 @@ def test_random_bursts_pauses_and_rereports_stay_bit_exact(mode, devices):
             want = [np.asarray(w, F) for w in want]
             ck = new
     print("soak", mode, devices, stats)
+    assert stats["folded_early"] > 0

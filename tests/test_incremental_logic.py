@@ -499,159 +499,36 @@ def test_float64_checkpoint_declined_at_cycle_start():
         IncrementalCycle(ScanningEngine(), [3], slots=4, checkpoint=_f64_diff())
 
 
-# ---- speculative folds (pgh_fold_slots_keep / pgh_fold_mark / pgh_fold_rewind) ----------------------
+# ---- the close's DB reads: exactly fetch_plan (what the node reads under its report gate) --------------
 
-class SpecEngine(RecordingEngine):
-    """RecordingEngine with the library's saved fold states: `state` is the running fold state as a
-    payload list; a kept fold appends the slots' current payloads without freeing them."""
+def close_like_the_node(inc, order, db):
+    """seal -> fetch_plan -> (the gate released) finish, with a fetch that refuses any row the plan
+    did not name: the node's flow (pygrid_amd.node.NodeEngine.average_plan_diffs)."""
+    needs = inc.seal(order=order)
+    plan = inc.fetch_plan() if needs else []
+    assert len(set(plan)) == len(plan)
+    read = []
 
-    def __init__(self, **kw):
-        super().__init__(**kw)
-        self.state = []
-        self.marks = {}
-        self.kept_rows = 0
-        self.max_marks_held = 0
-
-    def fold_slots(self, mode, slots):
-        self.state += [self.slot[s] for s in slots]
-        super().fold_slots(mode, slots)
-
-    def fold_slots_keep(self, mode, slots):
-        assert len(set(slots)) == len(slots) and all(s in self.slot for s in slots)
-        self.state += [self.slot[s] for s in slots]
-        self.kept_rows += len(slots)
-        self.calls.append(("keep", len(slots)))
-
-    def fold_mark(self, m):
-        self.marks[m] = list(self.state)
-        self.max_marks_held = max(self.max_marks_held, len(self.marks))
-
-    def fold_rewind(self, m):
-        self.state = list(self.marks[m])
-        self.calls.append(("rewind", len(self.state)))
-
-    def fold_unmark(self, m):
-        del self.marks[m]
-
-    def fold_restart(self):
-        self.state = []
-        super().fold_restart()
-
-    def fold_slots_finish_resident(self, mode, slots):
-        self.final_rows = len(slots)
-        self.state += [self.slot[s] for s in slots]
-        self.result = list(self.state)
-        self.state = []
-        super().fold_slots_finish_resident(mode, slots)
+    def fetch(w):
+        assert w in plan, f"finish read row {w!r}, which fetch_plan did not name ({plan})"
+        read.append(w)
+        return db[w]
+    new = inc.finish(b"ck", framing="template", fetch=fetch)
+    assert read == plan  # the plan is exact: every row it names is read, in its order
+    return new
 
 
-def test_speculation_folds_every_report_and_closes_with_nothing_left():
-    """Worker 0 never reports, so nothing is ever certain; every reported diff is folded as it
-    arrives anyway (in assignment order), rewound when an earlier worker reports after it, and the
-    close only finishes: no rows left to fold."""
-    rng = np.random.default_rng(11)
-    eng = SpecEngine()
-    n = 40
-    inc = IncrementalCycle(eng, [3], speculate=True, slots=n, fold_batch=8)
-    assert inc.speculate
-    for w in range(n):
-        inc.assigned(w)
-    reporters = [w for w in range(1, n) if rng.random() >= 0.2]
-    seen = []
-    for w in rng.permutation(reporters):
-        inc.reported(int(w), bytes([int(w)]))
-        seen.append(int(w))
-        assert eng.state == [bytes([x]) for x in sorted(seen)]  # the fold state is the plan so far
-    assert eng.marks and any(c[0] == "rewind" for c in eng.calls)
-    inc.close(b"ck", framing="template")
-    assert eng.result == [bytes([w]) for w in sorted(reporters)]
-    assert eng.final_rows == 0 and inc.last_close["early"] == len(reporters) and not inc.last_close["refold"]
-    assert eng.marks == {}  # every saved state released at close
-
-
-def test_speculation_frees_certain_slots_and_rewinds_only_after_the_base():
-    eng = SpecEngine()
-    inc = IncrementalCycle(eng, [3], speculate=True, slots=6)
-    for w in "abcdefgh":
-        inc.assigned(w)
-    for w in "abd":            # a, b certain; d speculative (c outstanding)
-        inc.reported(w, w.encode())
-    assert eng.state == [b"a", b"b", b"d"] and inc._base == 2 and len(inc._free) == 6 - 1
-    inc.reported("c", b"c")    # lands before d: back to the mark after b, refold c, d
-    assert eng.state == [b"a", b"b", b"c", b"d"] and eng.calls[-2][0] == "rewind" or ("rewind", 2) in eng.calls
-    assert inc._base == 4 and len(inc._free) == 6
-    inc.reported("b", b"b2")   # re-report of a certain (freed) diff: the close re-folds from the DB
-    assert inc.stale
-    db = {"a": b"a", "b": b"b2", "c": b"c", "d": b"d"}
-    inc.close(b"ck", framing="template", order=list("abcd"), fetch=db.__getitem__)
-    assert eng.result == [b"a", b"b2", b"c", b"d"] and inc.last_close["refold"]
-
-
-def test_speculative_re_report_rewinds_and_folds_the_latest_diff():
-    eng = SpecEngine()
-    inc = IncrementalCycle(eng, [3], speculate=True, slots=8)
-    for w in range(6):
-        inc.assigned(w)
-    for w, v in ((2, b"2a"), (4, b"4a"), (3, b"3a"), (4, b"4b"), (2, b"2b")):
-        inc.reported(w, v)
-    assert eng.state == [b"2b", b"3a", b"4b"]  # worker 0 outstanding: all speculative, kept
-    inc.reported(0, b"0")
-    inc.close(b"ck", framing="template", order=[0, 2, 3, 4], fetch=None)
-    assert eng.result == [b"0", b"2b", b"3a", b"4b"] and not inc.last_close["refold"]
-
-
-def test_close_rewinds_to_the_db_order():
-    """The DB returns another order than assignment: the close goes back to the last saved state
-    inside the common prefix and folds the rest from the kept slots -- no DB reads."""
-    eng = SpecEngine()
-    inc = IncrementalCycle(eng, [3], speculate=True, slots=8, mark_every=1)
-    for w in range(6):
-        inc.assigned(w)
-    for w in (5, 1, 2, 4):
-        inc.reported(w, bytes([w]))
-    assert eng.state == [bytes([w]) for w in (1, 2, 4, 5)]
-    inc.close(b"ck", framing="template", order=[1, 2, 5, 4], fetch=lambda w: pytest.fail("DB read"))
-    assert eng.result == [bytes([w]) for w in (1, 2, 5, 4)]
-    assert inc.last_close["early"] == 2 and inc.last_close["from_hbm"] == 2 and not inc.last_close["refold"]
-
-
-def test_mark_budget_thins_saved_states():
-    rng = np.random.default_rng(12)
-    eng = SpecEngine()
-    n = 60
-    inc = IncrementalCycle(eng, [1000], speculate=True, slots=n, speculation_budget=5 * 4000)
-    assert inc.max_marks == 5
-    for w in range(n):
-        inc.assigned(w)
-    reporters = [w for w in range(1, n) if rng.random() >= 0.2]
-    for w in rng.permutation(reporters):
-        inc.reported(int(w), bytes([int(w)]))
-    assert eng.max_marks_held <= 5
-    inc.close(b"ck", framing="template")
-    assert eng.result == [bytes([w]) for w in sorted(reporters)]
-
-
-def test_no_speculation_without_budget():
-    with pytest.raises(AggregationError):  # room for one saved state only
-        IncrementalCycle(SpecEngine(), [1000], slots=4, speculation_budget=4000, speculate=True)
-    assert not IncrementalCycle(SpecEngine(), [10], slots=4).speculate  # opt-in (r04)
-    assert not IncrementalCycle(SpecEngine(), [10], slots=4, speculate=False).speculate
-    with pytest.raises(AggregationError):
-        IncrementalCycle(RecordingEngine(), [10], slots=4, speculate=True)
-
-
-@pytest.mark.parametrize("seed", range(30))
-def test_randomised_speculation_matches_the_reference_order(seed):
+@pytest.mark.parametrize("seed", range(40))
+def test_randomised_scripts_fold_the_db_order_and_read_only_the_planned_rows(seed):
     """Random scripts -- assignments (some announced behind the fold), shuffled reports, re-reports,
-    malformed re-reports, parked diffs under slot pressure, thinned marks, random DB orders -- fold
-    exactly the DB order's latest diffs, and speculation rewinds instead of reading the DB whenever
-    the order was the assignment order."""
+    malformed re-reports, parked diffs under slot pressure, random DB orders -- fold exactly the DB
+    order's latest diffs, and the close reads from the DB exactly the rows ``fetch_plan`` named
+    (the node releases its report gate before folding)."""
     rng = np.random.default_rng(1000 + seed)
     n = int(rng.integers(3, 30))
     slots = int(rng.integers(2, n + 3))
-    eng = SpecEngine(fail_on=b"bad")
-    inc = IncrementalCycle(eng, [3], speculate=True, slots=slots, fold_batch=int(rng.integers(1, 4)),
-                           speculation_budget=int(rng.integers(2, 12)) * 12)
+    eng = RecordingEngine(fail_on=b"bad")
+    inc = IncrementalCycle(eng, [3], slots=slots, fold_batch=int(rng.integers(1, 4)))
     late = set(int(x) for x in rng.choice(n, size=int(rng.integers(0, n // 3 + 1)), replace=False))
     for w in range(n):
         if w not in late:
@@ -669,8 +546,11 @@ def test_randomised_speculation_matches_the_reference_order(seed):
         version[w] = version.get(w, 0) + 1
         if rng.random() < 0.05:
             db[w] = b"bad"
-            with pytest.raises(StateParseError):
+            if w in inc._folded_set:  # folded already: the early fold goes stale, the close reads the DB
                 inc.reported(w, b"bad")
+            else:
+                with pytest.raises(StateParseError):
+                    inc.reported(w, b"bad")
         else:
             db[w] = mk(100 * version[w] + w)
             inc.reported(w, db[w])
@@ -681,133 +561,49 @@ def test_randomised_speculation_matches_the_reference_order(seed):
         order = [order[i] for i in rng.permutation(len(order))]
     if any(db[w] == b"bad" for w in order):
         with pytest.raises(StateParseError):
-            inc.close(b"ck", framing="template", order=order, fetch=db.__getitem__)
+            close_like_the_node(inc, order, db)
         return
-    inc.close(b"ck", framing="template", order=order, fetch=db.__getitem__)
-    assert eng.result == [db[w] for w in order]
+    close_like_the_node(inc, order, db)
+    assert folded(eng) == [db[w] for w in order]
 
 
 @pytest.mark.parametrize("slots", [2, 3, 5])
-@pytest.mark.parametrize("seed", range(8))
-def test_speculation_under_slot_pressure_closes_without_the_db(slots, seed):
-    """Few slots: speculative folds keep their slots, so the reserved slot of the fold front must
-    still come free (a mark at the certain point frees the certain diffs) -- every diff stays in
-    HBM or on the host and the close needs no DB read."""
-    rng = np.random.default_rng(50 + seed)
-    eng = SpecEngine()
-    n = 24
-    inc = IncrementalCycle(eng, [3], speculate=True, slots=slots, fold_batch=2, mark_every=3)
+@pytest.mark.parametrize("seed", range(6))
+def test_fetch_plan_covers_evictions_under_slot_pressure(slots, seed):
+    """Few slots and a DB order unlike the assignment order: the close gives up slots of diffs
+    needed later and re-reads them -- fetch_plan names those rows too."""
+    rng = np.random.default_rng(70 + seed)
+    eng = RecordingEngine()
+    n = 16
+    inc = IncrementalCycle(eng, [3], slots=slots, fold_batch=2)
     for w in range(n):
-        inc.assigned(w)
+        inc.assigned(w, key=w)
     reporters = [w for w in range(n) if w % 5 != 3]
+    db = {w: mk(w) for w in reporters}
     for w in rng.permutation(reporters):
-        inc.reported(int(w), mk(int(w)))
-        assert len([s for s in eng.slot]) <= slots
-    inc.close(b"ck", framing="template")
-    assert eng.result == [mk(w) for w in reporters]
+        inc.reported(int(w), db[int(w)])
+    order = [reporters[i] for i in rng.permutation(len(reporters))]
+    close_like_the_node(inc, order, db)
+    assert folded(eng) == [db[w] for w in order]
 
 
-class BusySpecEngine(SpecEngine):
-    """SpecEngine with pgh_fold_busy: `busy` says whether the GPU is still folding."""
-
-    busy = False
-
-    def fold_busy(self):
-        return self.busy
-
-
-@pytest.mark.parametrize("gap_ms,busy,folds_during_reports", [(5.0, False, True), (0.5, False, False),
-                                                              (5.0, True, False)])
-def test_lazy_speculation_waits_for_slow_reports_and_an_idle_gpu(monkeypatch, gap_ms, busy, folds_during_reports):
-    """Lazy speculation (the default with a real engine): a report is folded at once only when the
-    previous one came at least min_gap_ms before and the GPU is idle; otherwise it waits for a later
-    report or the close -- the result is the same either way."""
-    import pygrid_amd.incremental as inc_mod
-
-    clock = [100.0]
-    monkeypatch.setattr(inc_mod.time, "monotonic", lambda: clock[0])
-    eng = BusySpecEngine()
-    eng.busy = busy
-    inc = IncrementalCycle(eng, [3], speculate=True, slots=16)
-    assert inc.speculate and inc._lazy
-    for w in range(8):
-        inc.assigned(w)
-    for w in (3, 1, 6, 2, 5, 7, 4):   # worker 0 never reports
-        clock[0] += gap_ms / 1e3
-        inc.reported(w, bytes([w]))
-    assert (len(eng.state) > 1) == folds_during_reports
-    inc.close(b"ck", framing="template")
-    assert eng.result == [bytes([w]) for w in range(1, 8)]
-
-
-def test_out_of_hbm_for_saved_states_degrades_not_fails():
-    """pgh_fold_mark failing (no HBM for another saved state) keeps speculating with fewer saved
-    states; reports never fail for it and the close is still the reference's order."""
-    class TightEngine(SpecEngine):
-        def fold_mark(self, m):
-            if len(self.marks) >= 3:
-                raise AggregationError("fold state buffer allocation failed")
-            super().fold_mark(m)
-
-    rng = np.random.default_rng(77)
-    eng = TightEngine()
-    inc = IncrementalCycle(eng, [3], speculate=True, slots=40, mark_every=2)
-    for w in range(40):
-        inc.assigned(w)
-    reporters = [w for w in range(1, 40) if rng.random() >= 0.2]
-    for w in rng.permutation(reporters):
-        inc.reported(int(w), bytes([int(w)]))
-    assert len(eng.marks) <= 3 and inc.max_marks <= 3
-    inc.close(b"ck", framing="template")
-    assert eng.result == [bytes([w]) for w in sorted(reporters)]
-
-
-def test_lazy_skips_are_folded_by_a_timer_once_reports_pause(monkeypatch):
-    """Reports back to back leave their folds to a later report; when none comes within min_gap (the
-    close comes later, e.g. at the cycle's end), a timer folds them -- and waits while the GPU is
-    still busy -- so the close finds the fold done.  The result is unchanged."""
-    import time as _time
-
-    import pygrid_amd.incremental as inc_mod
-
-    clock = [100.0]
-    monkeypatch.setattr(inc_mod.time, "monotonic", lambda: clock[0])
-    eng = BusySpecEngine()
-    eng.busy = True
-    inc = IncrementalCycle(eng, [3], speculate=True, slots=16, min_gap_ms=2.0)
-    for w in range(8):
-        inc.assigned(w)
-    for w in (3, 1, 0, 6, 2, 5, 7, 4):
-        clock[0] += 0.5e-3
-        inc.reported(w, bytes([w]))
-    assert len(eng.state) <= 1  # nothing folded while the reports came back to back
-    _time.sleep(0.05)
-    assert len(eng.state) <= 1  # the fake clock says the reports are still arriving
-    clock[0] += 0.01
-    _time.sleep(0.05)
-    assert len(eng.state) <= 1  # paused, but the GPU is still busy
-    eng.busy = False
-    deadline = _time.time() + 5
-    while len(eng.state) < 8 and _time.time() < deadline:
-        _time.sleep(0.01)
-    assert len(eng.state) == 8, eng.state  # folded by the timer
-    inc.close(b"ck", framing="template")
-    assert inc.last_close["folded_before_close"] == 8
-    assert eng.result == [bytes([w]) for w in range(8)]
-    assert inc._timer is None
+def test_fetch_plan_needs_a_seal():
+    inc = IncrementalCycle(RecordingEngine(), [3], slots=4)
+    with pytest.raises(AggregationError):
+        inc.fetch_plan()
 
 
 @pytest.mark.parametrize("seed", range(4))
-def test_concurrent_reports_and_timer_folds_never_overlap_engine_calls(seed):
-    """Report handlers on several threads, the deferred-fold timer and re-reports: every engine call
-    happens under the cycle's lock (no two at once), and the close is the reference's order."""
+def test_concurrent_reports_never_overlap_engine_calls(seed):
+    """Report handlers on several threads with re-reports: every engine call happens under the
+    cycle's lock (no two at once), and the close is the reference's order."""
     import threading
     import time as _time
 
-    class GuardedEngine(BusySpecEngine):
+    class GuardedEngine(RecordingEngine):
         def __getattribute__(self, name):
             attr = object.__getattribute__(self, name)
-            if callable(attr) and not name.startswith("_") and name not in ("fold_busy",):
+            if callable(attr) and not name.startswith("_"):
                 def guarded(*a, **k):
                     lock = object.__getattribute__(self, "_guard")
                     assert lock.acquire(blocking=False), f"engine call {name} overlapped another"
@@ -823,7 +619,7 @@ def test_concurrent_reports_and_timer_folds_never_overlap_engine_calls(seed):
     eng = GuardedEngine()
     object.__setattr__(eng, "_guard", threading.Lock())
     n = 40
-    inc = IncrementalCycle(eng, [3], speculate=True, slots=48, min_gap_ms=1.0, mark_every=4)
+    inc = IncrementalCycle(eng, [3], slots=48)
     for w in range(n):
         inc.assigned(w)
     reporters = [w for w in range(n) if rng.random() >= 0.2]
@@ -837,7 +633,6 @@ def test_concurrent_reports_and_timer_folds_never_overlap_engine_calls(seed):
             for w, d in zip(ws, delays):
                 _time.sleep(d)
                 inc.reported(w, mk(w + 1000) if w in rereport else mk(w))
-                eng.busy = bool(rng.random() < 0.3)
             for w in ws:
                 if w in rereport:
                     inc.reported(w, mk(w))  # the latest diff wins
@@ -849,39 +644,32 @@ def test_concurrent_reports_and_timer_folds_never_overlap_engine_calls(seed):
         t.start()
     for t in ts:
         t.join()
-    eng.busy = False
-    _time.sleep(0.05)
     assert not errors, errors
-    # a re-report after its diff was folded for good is read from the DB (fetch) at close
+    # a re-report after its diff was folded is read from the DB (fetch) at close
     inc.close(b"ck", framing="template", order=sorted(reporters), fetch=mk)
-    assert eng.result == [mk(w) for w in sorted(reporters)]
+    assert folded(eng) == [mk(w) for w in sorted(reporters)]
 
 
-def test_a_dropped_open_cycle_is_abandoned_by_the_next_one(monkeypatch):
-    """A cycle dropped without close while its deferred-fold timer is armed: the next cycle on the
-    engine abandons it (timer cancelled), so nothing of the old cycle touches the new one's slots;
-    a cycle that was closed keeps its resident checkpoint for the next one."""
-    import time as _time
-
-    eng = BusySpecEngine()
-    eng.busy = True
-    a = IncrementalCycle(eng, [3], speculate=True, slots=8, min_gap_ms=1.0)
+def test_a_dropped_open_cycle_is_abandoned_by_the_next_one():
+    """A cycle dropped without close: the next cycle on the engine abandons it, so nothing of the
+    old cycle touches the new one's slots; a cycle that was closed keeps its resident checkpoint for
+    the next one."""
+    eng = RecordingEngine()
+    a = IncrementalCycle(eng, [3], slots=8)
     for w in range(4):
         a.assigned(w)
     for w in (2, 1, 3):
         a.reported(w, mk(w))
-    assert a._timer is not None
-    b = IncrementalCycle(eng, [3], speculate=True, slots=8, min_gap_ms=1.0)
-    assert a._closed and a._timer is None
-    eng.busy = False
+    b = IncrementalCycle(eng, [3], slots=8)
+    assert a._closed
     for w in range(3):
         b.assigned(w)
     for w in (1, 0, 2):
         b.reported(w, mk(10 + w))
-    _time.sleep(0.03)
+    a.reported(0, mk(0))  # the abandoned cycle ignores it
     b.close(b"ck", framing="template")
-    assert eng.result == [mk(10), mk(11), mk(12)]
+    assert folded(eng) == [mk(10), mk(11), mk(12)]
     with pytest.raises(AggregationError):
         a.close(b"ck", framing="template")
-    c = IncrementalCycle(eng, [3], speculate=True, slots=8)  # b was closed: abandoning it is a no-op
+    c = IncrementalCycle(eng, [3], slots=8)  # b was closed: abandoning it is a no-op
     assert eng.cycle_owner is c and b.last_close

@@ -311,3 +311,97 @@ def test_close_run_inline_from_a_report_does_not_deadlock():
     for w in (1, 2, 3):
         ref.cycle_manager.submit_worker_diff(w, rkeys[w], diff_bytes(w))
     assert checkpoints(mod) == checkpoints(ref) and len(checkpoints(mod)) == 2
+
+
+def test_two_inline_closers_do_not_deadlock_the_gate():
+    """two reports holding the gate shared both run a close inline and upgrade.  Each
+    would wait for the other's shared hold forever; the second upgrader fails at once instead
+    (GateUpgradeConflict), its handler goes on and releases its hold, and the first upgrade
+    completes."""
+    g = pnode._Gate()
+    both_in = threading.Barrier(2)
+    first_waiting = threading.Event()
+    got, errors = [], []
+
+    def handler(name, delay):
+        with g.shared():
+            both_in.wait(10)
+            time.sleep(delay)
+            try:
+                if name == "a":
+                    first_waiting.set()
+                else:
+                    first_waiting.wait(10)
+                    while not g._upgrading:
+                        time.sleep(0.001)
+                g.acquire_exclusive()
+            except pnode.GateUpgradeConflict:
+                errors.append(name)
+                return
+            try:
+                got.append(name)
+            finally:
+                g.release_exclusive()
+
+    ts = [threading.Thread(target=handler, args=("a", 0.0)), threading.Thread(target=handler, args=("b", 0.01))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(10)
+    assert not any(t.is_alive() for t in ts), "deadlock: two upgraders waited for each other"
+    assert got == ["a"] and errors == ["b"]
+    # the gate is whole again: a plain close and a later upgrade both get it
+    with g.exclusive():
+        pass
+    with g.shared():
+        g.acquire_exclusive()
+        g.release_exclusive()
+    assert not g._upgrading and not g._exclusive
+
+
+def test_assignment_while_the_cycle_state_is_built_is_recorded(monkeypatch):
+    """a cycle the node just created is prepared under the engine lock without a rows
+    query; an assign handler that runs meanwhile finds the lock taken.  Its assignment is recorded
+    into the state when the state is made (fold order, and the report's row lookup without a
+    query) -- then the cycle closes byte-identical to the reference."""
+    mod = make_node()
+    node = pnode.install(mod, engine=NumpyEngine(), framing="template", fold_batch=1)
+    real = node._new_cycle
+    built = []
+
+    def build_with_an_assign_racing(cm, cycle, fresh=False):
+        inc = real(cm, cycle, fresh)
+        if not built:  # the first cycle: a worker is assigned (DB row written) while this runs
+            t = threading.Thread(target=lambda: built.append(("key", assign(mod, 1, proc_box[0]))))
+            t.start()
+            t.join(10)
+            assert not t.is_alive()
+            assert not inc._key_of  # not recorded yet: the handler found the engine lock taken
+        return inc
+
+    proc_box = []
+    monkeypatch.setattr(node, "_new_cycle", build_with_an_assign_racing)
+    orig_create = mod.CycleManager.create
+
+    def create_after_the_process_exists(cm, *a):
+        if not proc_box:
+            import types
+
+            proc_box.append(types.SimpleNamespace(id=a[0]))
+        return orig_create(cm, *a)
+    monkeypatch.setattr(mod.CycleManager, "create", create_after_the_process_exists)
+    proc, _, _ = host_process(mod, CFG3, ckpt_bytes())
+    inc = next(st for st in node._cycles.values() if isinstance(st, pnode.IncrementalCycle))
+    assert len(inc._key_of) == 1 and not node._pending_assign  # recorded when the state was made
+    keys = {1: built[0][1]}
+    keys.update({w: assign(mod, w, proc) for w in (2, 3)})
+    for w in (1, 2, 3):
+        mod.cycle_manager.submit_worker_diff(w, keys[w], diff_bytes(w))
+    assert node.stats["closes_report_time"] == 1 and node.stats["diffs_from_db"] == 0, node.stats
+    node.uninstall()
+    ref = make_node()
+    rproc, _, _ = host_process(ref, CFG3, ckpt_bytes())
+    rkeys = {w: assign(ref, w, rproc) for w in (1, 2, 3)}
+    for w in (1, 2, 3):
+        ref.cycle_manager.submit_worker_diff(w, rkeys[w], diff_bytes(w))
+    assert checkpoints(mod) == checkpoints(ref)

@@ -306,15 +306,14 @@ def random_script(seed: int, prefix: str):
     return script, int(rng.integers(2, 7))
 
 
-@pytest.mark.parametrize("speculate", [False, True], ids=["certain-only", "speculative"])
 @pytest.mark.parametrize("threaded", [False, True], ids=["sync", "executor"])
-def test_randomised_scripts_on_the_sql_node(tmp_path, threaded, speculate):
+def test_randomised_scripts_on_the_sql_node(tmp_path, threaded):
     """Random scripts (``random_script``) through the reference's storage and handler, random slot
     budgets: installed and shipped nodes save identical checkpoints and hold identical diff blobs."""
     totals = collections.Counter()
     for trial in range(8):
         script, slots = random_script(500 + trial, f"t{trial}")
-        eng = run_both(tmp_path / f"t{trial}", script, threaded=threaded, speculate=speculate, slots=slots)
+        eng = run_both(tmp_path / f"t{trial}", script, threaded=threaded, slots=slots)
         totals.update(eng.stats)
     assert totals["report_errors"] == 0, totals
     assert totals["closes_report_time"] == 24 and totals["diffs_from_db"] >= 1, totals  # restarts read the DB

@@ -213,12 +213,10 @@ def test_malformed_diff_fails_the_close_like_the_reference():
     assert errs == [1, 1]
 
 
-@pytest.mark.parametrize("speculate", [True, False])
-def test_randomised_report_sequences(speculate):
-    """Random assignment / report / re-report / late-report / restart scripts, random DB orders;
-    with speculative folds (every reported diff folded at once, rewound when an earlier worker
-    reports) and with certain-only folds."""
-    totals = {"closes_report_time": 0, "refolds": 0, "diffs_from_db": 0, "rewinds": 0}
+def test_randomised_report_sequences():
+    """Random assignment / report / re-report / late-report / restart scripts, random DB orders:
+    the installed node (certain-only report-time folds) saves the shipped node's checkpoints."""
+    totals = {"closes_report_time": 0, "refolds": 0, "diffs_from_db": 0}
     for trial in range(40):
         rng = np.random.default_rng(100 + trial)
         n = int(rng.integers(3, 9))
@@ -250,7 +248,7 @@ def test_randomised_report_sequences(speculate):
         res = []
         for installed in (False, True):
             sc = Scenario(cfg, installed, row_order=(lambda r: r[::-1]) if reverse else None,
-                          **({"fold_batch": fb, "slots": slots, "speculate": speculate} if installed else {}))
+                          **({"fold_batch": fb, "slots": slots} if installed else {}))
             script(sc)
             res.append(sc.checkpoints())
         assert len(res[0]) >= 2 and res[0] == res[1], trial
@@ -258,7 +256,6 @@ def test_randomised_report_sequences(speculate):
             totals[k] += sc.node.stats[k]
     # the scripts did exercise every path
     assert totals["closes_report_time"] >= 40 and totals["refolds"] >= 3 and totals["diffs_from_db"] >= 3, totals
-    assert (totals["rewinds"] >= 10) if speculate else (totals["rewinds"] == 0), totals
 
 
 def test_checkpoint_cache_serves_get_model_and_stays_bounded():
