@@ -138,6 +138,9 @@ def parse():
                     help="default workload: skip the config lines (mnist-state --check on one GPU; resnet18-secagg, "
                          "c4-stream, c5-ingest --check over the same --gpus; each in a fresh child run) attached "
                          "under `config1` / `config3` / `config4` / `config5`")
+    ap.add_argument("--config-clients", type=int, default=None,
+                    help="rehearsal on one GPU only (tools/rehearse_multi.sh): clients of the config-3/4/5 child "
+                         "lines (default: each config's own count)")
     ap.add_argument("--budget-s", type=float, default=None,
                     help=f"deadline of the whole run, seconds (default: PGH_BENCH_BUDGET_S or {DEFAULT_BUDGET_S:.0f}, "
                          "under the driver's 600 s).  Every child line gets min(its own limit, what is left minus "
@@ -461,6 +464,8 @@ def config_line(args, key: str, limit_s: int = 420) -> dict:
            "--cpu-seconds", str(args.cpu_seconds)]
     if not cpu or args.no_cpu_baseline:
         cmd.append("--no-cpu-baseline")
+    if args.config_clients and workload != "mnist-state":
+        cmd += ["--clients", str(args.config_clients)]
     if args.dry_run:
         cmd.append("--dry-run")
     r, err = run_child(args, key, cmd, limit_s, stdout=subprocess.PIPE)
