@@ -3,7 +3,7 @@
 rule 24: alternate the arms in one lease, never compare runs from different boxes).
 
     python tools/ab_env.py --tag r02l --rounds 3 --arm PGH_FINAL_RANGES=1 --arm PGH_FINAL_RANGES=4 \
-        -- python3 -u tools/time_report_close.py 12
+        -- python3 -u bench.py --workload resnet18-report --steps 5 --no-cpu-baseline
 
 Each --arm is a space-separated list of VAR=VALUE ("" = the defaults).  Every run is its own child
 process under `timeout -k 10 <--timeout>`; the first failure ends the A/B (no retries).  Output:
