@@ -382,7 +382,7 @@ def wants_group_line(args) -> bool:
     return args.gpus > 1 and not args.group and not args.no_group_line and args.workload in GROUP_WORKLOADS
 
 
-def group_line(args, limit_s: int = 300) -> dict:
+def group_line(args, limit_s: int = 240) -> dict:
     """The path the node deploys at N > 1 (its single process drives every GPU through one library
     context, ``pgh_create_group``), measured on the same GPUs before the
     per-rank world forms: ``bench.py --group --gpus N`` in a FRESH child (no process that touched a
@@ -425,11 +425,12 @@ def group_line(args, limit_s: int = 300) -> dict:
     return out
 
 
-# key: (workload, GPUs (None: this run's --gpus), steps cap, with its cpu_baseline).  In run order:
-# the cheap config-1 close first, then the configs only a multi-GPU run exercises in their stated
-# form (4, 5), then config 3 (187.7 GB resident per GPU).
-CONFIG_LINES = {"config1": ("mnist-state", 1, None, True), "config4": ("c4-stream", None, 5, False),
-                "config5": ("c5-ingest", None, 5, False), "config3": ("resnet18-secagg", None, 10, True)}
+# key: (workload, GPUs (None: this run's --gpus), steps cap, with its cpu_baseline, time limit s).
+# In run order: the cheap config-1 close first, then the configs only a multi-GPU run exercises in
+# their stated form (4, 5), then config 3 (187.7 GB resident per GPU).  Each limit is ~10x what the
+# child took at N = 1 (profiles/r05b: 9 / 4 / 9 / 18 s), so one hung child cannot starve the others.
+CONFIG_LINES = {"config1": ("mnist-state", 1, None, True, 120), "config4": ("c4-stream", None, 5, False, 180),
+                "config5": ("c5-ingest", None, 5, False, 180), "config3": ("resnet18-secagg", None, 10, True, 240)}
 FOLD_BYTES_NOTE = {
     "c5-ingest": "fold batch 2: each fold launch also reads and writes the running state (4 B + 4 B per param "
                  "per 2 clients), so the fold kernel moves 2x its diff bytes; fold_frac counts those bytes, "
@@ -447,7 +448,7 @@ def wants_config_lines(args) -> bool:
     return args.workload == "resnet18-fedavg" and not args.group and not args.no_config_lines and not under_profiler()
 
 
-def config_line(args, key: str, limit_s: int = 420) -> dict:
+def config_line(args, key: str) -> dict:
     """One BASELINE config as a fresh child run (``bench.py --gpus N --workload <w> --check``: it
     forms its own N ranks; no process that touched a GPU re-execs), summarised for this line: what
     ran (ranks, backend), its value with ``e2e_frac`` = value / (GPUs x HBM peak), the dominant
@@ -455,7 +456,7 @@ def config_line(args, key: str, limit_s: int = 420) -> dict:
     bit-exact check and, where the config has one, its cpu_baseline."""
     import subprocess
 
-    workload, gpus, steps_cap, cpu = CONFIG_LINES[key]
+    workload, gpus, steps_cap, cpu, limit_s = CONFIG_LINES[key]
     gpus = gpus or args.gpus
     steps = min(args.steps, steps_cap) if steps_cap else args.steps
     cmd = [sys.executable, str(Path(__file__).resolve()), "--gpus", str(gpus), "--workload", workload,
