@@ -212,10 +212,14 @@ int h2d_range(pgh_ctx* c, const Dest& d, int64_t i0, const uint8_t* src, int64_t
     return PGH_OK;
 }
 
+// Timing events (timed_launch) only measure: no system-scope fence when they complete.  With the
+// default flags each one made the kernel after it start 15-22 us after the one before, against 5-7
+// without (tools/exp_close_pipeline.hip, profiles/r05e/): 12 range launches of a report-time close
+// lost ~0.15 ms to them.  Every host read of a result still goes through a copy with its own sync.
 hipEvent_t take_event(pgh_ctx* c) {
     if (!c->pool.empty()) { hipEvent_t e = c->pool.back(); c->pool.pop_back(); return e; }
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
     return e;
 }
 
@@ -403,50 +407,62 @@ int final_ranges(const pgh_ctx* c) { return c->final_split > 1 && c->pg >= (1 <<
 int64_t range_edge(const pgh_ctx* c, int k, int K) { return k >= K ? c->pg : (c->pg * k / K) & ~(int64_t)3; }
 
 // HBM bytes at `src` (after the work already on stream `s`) -> host pieces, through the pinned
-// ring: the DMA of one slot overlaps the host copy-out of the previous one.  `overlap`, if given,
-// is host work run while the first DMA is in flight (the checkpoint template's framing copy).
-// marks: src is the resident checkpoint: when its last fold left range marks, the DMAs run on the
-// copy stream, each behind the range that wrote its bytes (the rest of the fold continues).
+// ring, in pieces of at most D2H_PIECE.  Every piece that fits the ring (both slots: 2 x 128 MiB by
+// default, so any ResNet-18-sized result) is queued at once, each with an event, and the host copies
+// piece k out as soon as its event fires while the later pieces' DMAs run.  Queuing them all up
+// front keeps them on the SDMA engines: a D2H queued while another one still ran went to a blit
+// kernel (__amd_rocclr_copyBuffer), whose host writes then held back the end of every fold range
+// running beside it (48 -> 183-190 us, profiles/r05d/); queued before any ran they all went to SDMA
+// (profiles/r05e/).  `overlap`, if given, is host work run while the first DMA is in flight (the
+// checkpoint template's framing copy).  marks: src is the resident checkpoint: when its last fold
+// left range marks, the DMAs run on the copy stream, each behind the ranges that wrote its bytes
+// (the rest of the fold continues).
 int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>& pieces, hipStream_t s,
                      const std::function<void()>& overlap, bool marks) {
     size_t total = 0;
     for (auto& p : pieces) total += p.n;
+    if (total == 0) return PGH_OK;
     const bool piped = marks && !c->final_marks.empty();
     if (piped) s = c->copy;
-    size_t off = 0;
-    int prev_slot = -1;
-    size_t prev_off = 0, prev_len = 0;
-    while (off < total || prev_slot >= 0) {
-        int cur_slot = -1;
-        size_t cur_len = 0;
-        if (off < total) {
-            cur_slot = c->pin_next;
-            c->pin_next ^= 1;
-            if (c->pin_used[cur_slot]) CK(c, hipEventSynchronize(c->pin_ev[cur_slot]));
-            cur_len = std::min({total - off, c->pin_slot, D2H_PIECE});
-            if (piped) {  // wait for EVERY fold range the piece's floats come from: the ranges
-                          // alternate over two streams, so the last one's mark orders nothing else
-                const int64_t first = (int64_t)(off / 4), last = (int64_t)((off + cur_len + 3) / 4);
-                int64_t start = 0;
-                for (auto& m : c->final_marks) {
-                    if (start >= last) break;
-                    if (m.end > first) CK(c, hipStreamWaitEvent(s, m.ev, 0));
-                    start = m.end;
-                }
+    const size_t piece = std::min(c->pin_slot, D2H_PIECE);
+    const size_t per_slot = c->pin_slot / piece;  // >= 1 (pin_slot >= 4096)
+    const size_t cells = 2 * per_slot;            // ring cells, one piece each
+    for (int k = 0; k < 2; ++k)                   // an earlier staged ingest may still read a slot
+        if (c->pin_used[k]) {
+            CK(c, hipEventSynchronize(c->pin_ev[k]));
+            c->pin_used[k] = false;
+        }
+    while (c->d2h_ev.size() < std::min<size_t>(cells, (total + piece - 1) / piece)) {
+        hipEvent_t e = nullptr;
+        CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->d2h_ev.push_back(e);
+    }
+    auto cell_ptr = [&](size_t j) { return c->h_pin[(j / per_slot) % 2] + (j % per_slot) * piece; };
+    size_t queued = 0, done = 0;  // pieces queued / copied out
+    const size_t n_pieces = (total + piece - 1) / piece;
+    auto queue = [&](size_t j) -> int {
+        const size_t off = j * piece, len = std::min(piece, total - off);
+        if (piped) {  // wait for EVERY fold range the piece's floats come from
+            const int64_t first = (int64_t)(off / 4), last = (int64_t)((off + len + 3) / 4);
+            int64_t start = 0;
+            for (auto& m : c->final_marks) {
+                if (start >= last) break;
+                if (m.end > first) CK(c, hipStreamWaitEvent(s, m.ev, 0));
+                start = m.end;
             }
-            CK(c, hipMemcpyAsync(c->h_pin[cur_slot], src + off, cur_len, hipMemcpyDeviceToHost, s));
-            CK(c, hipEventRecord(c->pin_ev[cur_slot], s));
-            c->pin_used[cur_slot] = true;
         }
-        if (overlap && off == 0) overlap();
-        if (prev_slot >= 0) {
-            CK(c, hipEventSynchronize(c->pin_ev[prev_slot]));
-            scatter_out(c->h_pin[prev_slot], prev_off, prev_len, pieces, *c->pool_copy);
-        }
-        prev_slot = cur_slot;
-        prev_off = off;
-        prev_len = cur_len;
-        off += cur_len;
+        CK(c, hipMemcpyAsync(cell_ptr(j % cells), src + off, len, hipMemcpyDeviceToHost, s));
+        CK(c, hipEventRecord(c->d2h_ev[j % cells], s));
+        return PGH_OK;
+    };
+    while (queued < n_pieces && queued < cells) RC(queue(queued++));
+    if (overlap) overlap();
+    while (done < n_pieces) {
+        const size_t off = done * piece, len = std::min(piece, total - off);
+        CK(c, hipEventSynchronize(c->d2h_ev[done % cells]));
+        scatter_out(cell_ptr(done % cells), off, len, pieces, *c->pool_copy);
+        ++done;
+        if (queued < n_pieces) RC(queue(queued++));  // into the cell just copied out
     }
     return PGH_OK;
 }
@@ -1073,6 +1089,7 @@ void pgh_destroy(pgh_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (auto e : c->fold_ev_pool) (void)hipEventDestroy(e);
     for (auto e : c->rmark_pool) (void)hipEventDestroy(e);
+    for (auto e : c->d2h_ev) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
     if (c->aux) (void)hipStreamDestroy(c->aux);

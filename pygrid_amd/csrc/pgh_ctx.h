@@ -232,6 +232,7 @@ struct pgh_ctx {
     hipEvent_t pin_ev[2] = {nullptr, nullptr};
     bool pin_used[2] = {false, false};
     int pin_next = 0;
+    std::vector<hipEvent_t> d2h_ev;  // one per ring cell of a staged D2H (stage_d2h_pieces)
     int copy_threads = 8;
     std::vector<int> local_cpus;  // PGH_NUMA (default on): the GPU's socket, for the copy pool + pinned ring
     std::unique_ptr<CopyPool> pool_copy;
@@ -393,9 +394,9 @@ struct OutPiece {
     size_t n;
 };
 
-// HBM -> host results move in pieces of at most D2H_PIECE, the DMA of piece i + 1 beside the host
-// copy-out of piece i (r01ac: 4, 8, 16 MiB within the noise of the 47 MB report-time close; with the
-// parallel pre-fault, r01ak, 8 MiB pieces closed in 2.3-2.4 ms vs 2.6-2.7 for one piece).
+// HBM -> host results move in pieces of at most D2H_PIECE, the later pieces' DMAs beside the host
+// copy-out of the earlier ones (r01ac: 4, 8, 16 MiB within the noise of the 47 MB report-time close;
+// with the parallel pre-fault, r01ak, 8 MiB pieces closed in 2.3-2.4 ms vs 2.6-2.7 for one piece).
 constexpr size_t D2H_PIECE = 8u << 20;
 
 bool is_pinned(const void* p);

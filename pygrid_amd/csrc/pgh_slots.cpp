@@ -66,10 +66,11 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
         a.mode = mode;
         a.variant = c->variant;
         // The FINAL pass of a report-time close (a short fold of the rows left) as ranges of 4 MiB of
-        // output, one after another on one stream, each followed by its mark: the D2H pieces (8 MiB)
-        // start behind the first two instead of behind the whole fold.  Ranges aligned to the pieces on
-        // one stream closed 0.1-0.15 ms sooner than 8 equal ranges alternating over two streams
-        // (profiles/r04m/: 2.04 vs 2.19 ms, close start -> new checkpoint bytes).
+        // output, one after another on one stream, a mark behind every second one: each 8 MiB D2H
+        // piece starts behind the two ranges that wrote it instead of behind the whole fold.  Ranges
+        // aligned to the pieces on one stream closed 0.1-0.15 ms sooner than 8 equal ranges
+        // alternating over two streams (profiles/r04m/: 2.04 vs 2.19 ms, close start -> new
+        // checkpoint bytes); a mark (a system-scope release) only where a piece ends (r05).
         const int64_t RF = (int64_t)(D2H_PIECE / 8);
         const int K = (a.flags & pgh::FL_FINAL) && c->pg >= (1 << 20) ? (int)((c->pg + RF - 1) / RF) : 1;
         if (a.flags & pgh::FL_FINAL) clear_final_marks(c);
@@ -85,7 +86,7 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
             const uint64_t rp = (uint64_t)(hi - lo);
             const uint64_t bytes = 4ull * (uint64_t)m * rp + (first ? 0 : 4 * rp) + ((a.flags & pgh::FL_FINAL) ? 8 * rp : 4 * rp);
             RC(timed_launch(c, rs, bytes, [&] { return pgh::launch_fedavg_rows(ar, tab, rs); }));
-            if (K > 1) RC(add_final_mark(c, rs, hi));
+            if (K > 1 && (hi % (2 * RF) == 0 || hi == c->pg)) RC(add_final_mark(c, rs, hi));
         }
         done += m;
     } while (done < n);
