@@ -473,10 +473,10 @@ def config_line(args, key: str) -> dict:
     if err:
         return err
     lines = json_lines(r.stdout)
-    if r.returncode != 0 or not lines:
-        return {"error": f"{workload} child exited {r.returncode} (its stderr is above)", "stage": key,
-                "command": " ".join(cmd[1:])}
-    g = json.loads(lines[-1])
+    g = json.loads(lines[-1]) if lines else {}
+    if r.returncode != 0 or not lines:  # the child's own watchdog line says where it stopped
+        return {"error": g.get("error") or f"{workload} child exited {r.returncode} (its stderr is above)",
+                "stage": key, "child_stage": g.get("stage"), "command": " ".join(cmd[1:])}
     if g.get("dry_run"):
         return g
     if g.get("error"):

@@ -47,6 +47,28 @@ def test_close_time_knobs(monkeypatch, env):
             _check(CycleAggregator(eng).average_plan_diffs({}, ck_pb, d_pbs), O.fedavg_mean(ckpt, diffs))
 
 
+@pytest.mark.parametrize("pinned", [0, 2 << 20, 2 * 81_920], ids=["ring-default", "ring-2MiB", "ring-160KiB"])
+def test_d2h_pieces_wrap_a_small_pinned_ring(pinned):
+    """stage_d2h_pieces queues every D2H piece that fits the pinned ring at once and refills a cell
+    as soon as its piece is copied out: a 4.4 MB checkpoint through a ring of 2 x 1 MiB (5 pieces
+    over 2 cells) or 2 x 80 KiB (55 pieces), after a report-time close (its pieces wait on the
+    FINAL ranges' marks) and after a close-time fold, bit-exact."""
+    from pygrid_amd import Engine
+    from pygrid_amd.cycle import CycleAggregator
+    from pygrid_amd.incremental import IncrementalCycle
+
+    ckpt, diffs, ck_pb, d_pbs = _case(915, n=4)
+    want = O.fedavg_mean(ckpt, diffs)
+    with Engine(0, pinned_bytes=pinned) as eng:
+        inc = IncrementalCycle(eng, [int(np.prod(s)) for s in SHAPES], slots=6, checkpoint=ck_pb)
+        for w in range(5):
+            inc.assigned(w)
+        for w in (3, 1, 2, 4):  # worker 0 never reports: every row folds at close, in ranges
+            inc.reported(w, d_pbs[w - 1])
+        _check(inc.close(ck_pb), want)
+        _check(CycleAggregator(eng).average_plan_diffs({}, ck_pb, d_pbs), want)
+
+
 def test_report_time_close_in_output_ranges():
     """The report-time close's FINAL pass runs as ranges of 4 MiB of output on one stream, the D2H
     pieces behind them (no knob since r04): a 1.1 M-param shard (two ranges, the second short)
