@@ -384,7 +384,7 @@ def _probed_plan(*_a, **_k):  # stands in for a hosted plan whose verdict is cac
 
 
 def make_average_plan_diffs(aggregator: CycleAggregator, model_manager, process_manager, plan_manager,
-                            original: Callable, gate: Optional[Callable] = None) -> Callable:
+                            original: Callable, gate: Optional[Callable] = None, framing: str = "fresh") -> Callable:
     """Build a drop-in ``CycleManager._average_plan_diffs(self, server_config, cycle)``.
 
     DB I/O mirrors ``cycle_manager.py:234-245`` and ``:304-323``; the arithmetic slice
@@ -394,6 +394,7 @@ def make_average_plan_diffs(aggregator: CycleAggregator, model_manager, process_
     ``tasks.complete_cycle`` logs (``tasks/cycle.py:28-37``), like any failed cycle close.
     ``gate()``: a context manager held while the completed rows and their diffs are read (the
     node's report gate: a re-report's DB write lands wholly before or after that read).
+    ``framing``: the new checkpoint's framing (``CycleAggregator.average_plan_diffs``).
     """
 
     def _average_plan_diffs(self, server_config: dict, cycle):
@@ -406,7 +407,7 @@ def make_average_plan_diffs(aggregator: CycleAggregator, model_manager, process_
             avg_plan, plan_key = hosted_plan(server_config, cycle, process_manager, plan_manager,
                                              getattr(aggregator, "mean_plans", None))
             new_ckpt = aggregator.average_plan_diffs(server_config, _checkpoint.value, diffs, avg_plan,
-                                                     plan_key=plan_key)
+                                                     plan_key=plan_key, framing=framing)
         except PlanNotAcceleratedError as e:
             logging.info("engine declined (%s): running the reference averaging", e)
             return original(self, server_config, cycle)

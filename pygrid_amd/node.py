@@ -182,7 +182,7 @@ class NodeEngine:
         orig_run = self.mod.run_task_once
         close_time = make_average_plan_diffs(self.aggregator, self.model_manager, self.process_manager,
                                              self.plan_manager, original=orig["_average_plan_diffs"],
-                                             gate=self._gate.exclusive)
+                                             gate=self._gate.exclusive, framing=self.framing)
 
         def assign(cm, worker, cycle, hash_key):
             wc = orig["assign"](cm, worker, cycle, hash_key)
@@ -351,7 +351,16 @@ class NodeEngine:
         return self.mod.complete_cycle
 
     def on_assign(self, cm, cycle, wc, key=None):
-        st = self._cycle_state(cm, cycle)
+        """After the reference's DB write of the assignment.  Never raises: the response stays the
+        reference's (a cycle whose report-time state cannot be made closes from its DB rows)."""
+        try:
+            st = self._cycle_state(cm, cycle)
+        except Exception as e:  # noqa: BLE001
+            log.warning("cycle %s: report-time state not prepared at an assignment (%s); close-time path",
+                        cycle.id, e)
+            with self._lock:
+                self._set_elsewhere(cycle.id)
+            return
         if st is _BUSY:
             with self._lock:
                 st = self._cycles.get(cycle.id)

@@ -405,3 +405,27 @@ def test_assignment_while_the_cycle_state_is_built_is_recorded(monkeypatch):
     for w in (1, 2, 3):
         ref.cycle_manager.submit_worker_diff(w, rkeys[w], diff_bytes(w))
     assert checkpoints(mod) == checkpoints(ref)
+
+
+def test_assignment_never_raises_when_the_cycle_state_cannot_be_made(monkeypatch):
+    """A cycle that existed before install (a restart) gets its report-time state at its first
+    assignment; if making it fails, the assign handler still returns the reference's result and
+    the cycle closes through the close-time path over its DB rows, byte-identical."""
+    mod = make_node()
+    proc, _, _ = host_process(mod, CFG3, ckpt_bytes())  # created before install: no state yet
+    node = pnode.install(mod, engine=NumpyEngine(), framing="template", fold_batch=1)
+
+    def broken(cm, cycle, fresh=False):
+        raise RuntimeError("model load failed")
+    monkeypatch.setattr(node, "_new_cycle", broken)
+    keys = {w: assign(mod, w, proc) for w in (1, 2, 3)}  # no exception reaches the handler
+    for w in (1, 2, 3):
+        mod.cycle_manager.submit_worker_diff(w, keys[w], diff_bytes(w))
+    assert node.stats["closes_close_time"] == 1 and node.stats["closes_report_time"] == 0, node.stats
+    node.uninstall()
+    ref = make_node()
+    rproc, _, _ = host_process(ref, CFG3, ckpt_bytes())
+    rkeys = {w: assign(ref, w, rproc) for w in (1, 2, 3)}
+    for w in (1, 2, 3):
+        ref.cycle_manager.submit_worker_diff(w, rkeys[w], diff_bytes(w))
+    assert checkpoints(mod) == checkpoints(ref)
