@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PGH_ABI_VERSION 8
+#define PGH_ABI_VERSION 9
 
 typedef struct pgh_ctx pgh_ctx;
 
@@ -213,6 +213,13 @@ int pgh_fold_slots_finish_resident(pgh_ctx* ctx, int mode, const int32_t* slots,
  * assumed, or a folded worker re-reported (submit_worker_diff overwrites its diff, :162-174):
  * the caller then re-folds every diff in the query's order, bit-identical to the reference. */
 int pgh_fold_slots_restart(pgh_ctx* ctx);
+/* Report-time ingest (on != 0; default off): every State diff of a shard of >= 1M params is
+ * copied to HBM in param ranges with an event each, and the close's fold
+ * (pgh_fold_slots_finish_resident) starts each range as soon as the LAST report's copy of that
+ * range has landed instead of waiting for the whole copy -- the close overlaps the tail of the
+ * last report's DMA.  Costs a few % of H2D throughput per diff (more, smaller copies), so it is
+ * for report-time aggregation, not for a close that ingests every diff at once. */
+int pgh_set_ingest_ranges(pgh_ctx* ctx, int on);
 
 /* Z_2^64 share sum over all clients x parties, then decode float32(sum) / base**prec.
  * sum_out (int64) and dec_out (float32) are host arrays of P_shard; either may be NULL. */

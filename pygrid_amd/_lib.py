@@ -93,6 +93,7 @@ SIGNATURES = {
     # report buffers, pygrid_amd.report.PinnedPool)
     "pgh_ingest_state": (_i, [_vp, _i, _vp, _sz]),
     "pgh_set_synth_kind": (_i, [_vp, _i]),
+    "pgh_set_ingest_ranges": (_i, [_vp, _i]),
     "pgh_ingest_state_shares": (_i, [_vp, _i, _i, C.POINTER(C.c_char_p), C.POINTER(_sz)]),
     "pgh_synth_fill": (_i, [_vp, _u64, _i]),
     "pgh_synth_ingest": (_i, [_vp, _u64, _i, _i]),
@@ -137,7 +138,7 @@ SIGNATURES = {
     "pgh_b64_decode_clean": (_i, [_vp, _sz, _vp, _sz, C.POINTER(_sz), _i]),
 }
 
-ABI_VERSION = 8  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
+ABI_VERSION = 9  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
 _LIB = None
 
 

@@ -188,6 +188,7 @@ void slab_geometry(int64_t pg, size_t es, size_t block_bytes, int64_t* bw, int64
 int h2d_range(pgh_ctx* c, const Dest& d, int64_t i0, const uint8_t* src, int64_t n, hipStream_t s) {
     const size_t es = d.es;
     if (n <= 0) return PGH_OK;
+    ++c->copy_seq;
     if (d.map.bshift == 62) {
         CK(c, hipMemcpyAsync(d.base + (size_t)i0 * es, src, (size_t)n * es, hipMemcpyHostToDevice, s));
         return PGH_OK;
@@ -259,6 +260,51 @@ bool is_pinned(const void* p) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) { (void)hipGetLastError(); return false; }
     return attr.type == hipMemoryTypeHost;
+}
+
+// Ranged report ingest (pgh_set_ingest_ranges) of concatenated fp32 host pieces holding the whole
+// shard row: one pinned slot, filled and DMA'd chunk by chunk (INGEST_CHUNK params each, the host
+// copy of chunk k + 1 beside the DMA of chunk k), rng_ev[k] behind chunk k's DMA.
+int stage_pieces_h2d_ranged(pgh_ctx* c, const Dest& dst, const std::vector<Piece>& pieces, size_t total) {
+    const double t0 = now_ms();
+    const int K = (int)((c->pg + INGEST_CHUNK - 1) / INGEST_CHUNK);
+    while ((int)c->rng_ev.size() < K) {
+        hipEvent_t e = nullptr;
+        CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->rng_ev.push_back(e);
+    }
+    const int slot = c->pin_next;
+    c->pin_next ^= 1;
+    if (c->pin_used[slot]) CK(c, hipEventSynchronize(c->pin_ev[slot]));
+    size_t pi = 0, poff = 0;
+    for (int k = 0; k < K; ++k) {
+        const size_t a = (size_t)k * INGEST_CHUNK * 4, b = std::min(total, (size_t)(k + 1) * INGEST_CHUNK * 4);
+        std::vector<CopyPool::Seg> segs;
+        for (size_t at = a; at < b;) {
+            const size_t m = std::min(pieces[pi].n - poff, b - at);
+            segs.push_back({c->h_pin[slot] + at, pieces[pi].src + poff, m});
+            at += m;
+            poff += m;
+            if (poff == pieces[pi].n) { ++pi; poff = 0; }
+        }
+        c->pool_copy->run(segs);
+        RC(h2d_range(c, dst, (int64_t)(a / 4), c->h_pin[slot] + a, (int64_t)((b - a) / 4), c->copy));
+        CK(c, hipEventRecord(c->rng_ev[(size_t)k], c->copy));
+    }
+    CK(c, hipEventRecord(c->pin_ev[slot], c->copy));
+    c->pin_used[slot] = true;
+    c->rng_seq = c->copy_seq;
+    c->rng_n = K;
+    c->st.h2d_ms_total += now_ms() - t0;
+    c->st.h2d_bytes_total += total;
+    c->st.h2d_staged_bytes_total += total;
+    return PGH_OK;
+}
+
+// Whether the FINAL pass of a slot fold may wait per param range on the latest ranged ingest
+// instead of on every copy issued (order_after_ingest): nothing else went to the copy stream since.
+bool ranged_ingest_valid(const pgh_ctx* c) {
+    return c->ingest_ranges && c->rng_seq == c->copy_seq && c->rng_n == (int)((c->pg + INGEST_CHUNK - 1) / INGEST_CHUNK);
 }
 
 // Concatenated host pieces -> HBM at `dst`, through the pinned ring: each slot is filled by
@@ -373,6 +419,7 @@ void prefault_parallel(uint8_t* p, size_t n, CopyPool& pool) {
 void clear_final_marks(pgh_ctx* c) {
     for (auto& m : c->final_marks) c->rmark_pool.push_back(m.ev);
     c->final_marks.clear();
+    c->marks_after_ranges = false;
 }
 
 int add_final_mark(pgh_ctx* c, hipStream_t s, int64_t end) {
@@ -423,21 +470,37 @@ int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>
     for (auto& p : pieces) total += p.n;
     if (total == 0) return PGH_OK;
     const bool piped = marks && !c->final_marks.empty();
-    if (piped) s = c->copy;
+    // behind a ranged close (pgh_set_ingest_ranges) the copy stream still holds the last report's
+    // H2D: the pieces go on aux (idle in a slot fold), so the D2H runs beside that DMA
+    if (piped) s = c->marks_after_ranges ? c->aux : c->copy;
     const size_t piece = std::min(c->pin_slot, D2H_PIECE);
     const size_t per_slot = c->pin_slot / piece;  // >= 1 (pin_slot >= 4096)
-    const size_t cells = 2 * per_slot;            // ring cells, one piece each
-    for (int k = 0; k < 2; ++k)                   // an earlier staged ingest may still read a slot
+    // an earlier staged ingest may still read a slot: use the free ones, wait only if neither is
+    int free_slot[2], n_free = 0;
+    for (int k = 0; k < 2; ++k) {
         if (c->pin_used[k]) {
-            CK(c, hipEventSynchronize(c->pin_ev[k]));
+            const hipError_t q = hipEventQuery(c->pin_ev[k]);
+            if (q == hipErrorNotReady) continue;
+            CK(c, q);
             c->pin_used[k] = false;
         }
+        free_slot[n_free++] = k;
+    }
+    if (n_free == 0) {
+        for (int k = 0; k < 2; ++k) {
+            CK(c, hipEventSynchronize(c->pin_ev[k]));
+            c->pin_used[k] = false;
+            free_slot[k] = k;
+        }
+        n_free = 2;
+    }
+    const size_t cells = (size_t)n_free * per_slot;  // ring cells, one piece each
     while (c->d2h_ev.size() < std::min<size_t>(cells, (total + piece - 1) / piece)) {
         hipEvent_t e = nullptr;
         CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         c->d2h_ev.push_back(e);
     }
-    auto cell_ptr = [&](size_t j) { return c->h_pin[(j / per_slot) % 2] + (j % per_slot) * piece; };
+    auto cell_ptr = [&](size_t j) { return c->h_pin[free_slot[j / per_slot]] + (j % per_slot) * piece; };
     size_t queued = 0, done = 0;  // pieces queued / copied out
     const size_t n_pieces = (total + piece - 1) / piece;
     auto queue = [&](size_t j) -> int {
@@ -1090,6 +1153,7 @@ void pgh_destroy(pgh_ctx* c) {
     for (auto e : c->fold_ev_pool) (void)hipEventDestroy(e);
     for (auto e : c->rmark_pool) (void)hipEventDestroy(e);
     for (auto e : c->d2h_ev) (void)hipEventDestroy(e);
+    for (auto e : c->rng_ev) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
     if (c->aux) (void)hipStreamDestroy(c->aux);

@@ -270,6 +270,17 @@ struct pgh_ctx {
     hipEvent_t gdma_ev = nullptr;    // the last message DMA (the caller's buffer is free after it)
     bool gtab_used = false;
     bool pinned_gather = true;
+    // Ranged report ingest (pgh_set_ingest_ranges): a State diff goes to HBM in chunks of
+    // INGEST_CHUNK params, each followed by rng_ev[k] on the copy stream, so that the FINAL pass of
+    // a report-time close that starts while the last report's DMA is still in flight folds each
+    // param range as soon as its bytes have landed.  copy_seq counts the data operations issued on
+    // the copy stream; the ranged close applies only while rng_seq == copy_seq (nothing issued on
+    // the copy stream since the latest ranged ingest) and rng_n chunks cover the shard.
+    bool ingest_ranges = false;
+    std::vector<hipEvent_t> rng_ev;
+    uint64_t copy_seq = 0, rng_seq = ~0ull;
+    int rng_n = 0;
+    bool marks_after_ranges = false;  // final_marks came from a slot fold that waited on rng_ev
     bool warmup_skipped = false;  // pgh_create's warm-up failed (e.g. no device memory left): skipped
     int64_t vec_min = 0;      // [P_shard] device vectors at least this long (group collectives)
     // Pipelined close: a resident fold's FINAL pass runs as final_split param ranges, each followed by
@@ -398,10 +409,15 @@ struct OutPiece {
 // copy-out of the earlier ones (r01ac: 4, 8, 16 MiB within the noise of the 47 MB report-time close;
 // with the parallel pre-fault, r01ak, 8 MiB pieces closed in 2.3-2.4 ms vs 2.6-2.7 for one piece).
 constexpr size_t D2H_PIECE = 8u << 20;
+// Ranged report ingest (pgh_set_ingest_ranges): one chunk = the params of one D2H piece = two
+// 4 MiB FINAL ranges of a report-time close (pgh_slots.cpp).
+constexpr int64_t INGEST_CHUNK = (int64_t)(D2H_PIECE / 4);
 
 bool is_pinned(const void* p);
 int h2d_range(pgh_ctx* c, const Dest& d, int64_t i0, const uint8_t* src, int64_t n, hipStream_t s);
 int stage_pieces_h2d(pgh_ctx* c, const Dest& dst, const std::vector<Piece>& pieces);
+int stage_pieces_h2d_ranged(pgh_ctx* c, const Dest& dst, const std::vector<Piece>& pieces, size_t total);
+bool ranged_ingest_valid(const pgh_ctx* c);
 int stage_h2d(pgh_ctx* c, const Dest& dst, const uint8_t* src, size_t n, bool pinned_src);
 void scatter_out(const uint8_t* src, size_t off, size_t len, const std::vector<OutPiece>& pieces, CopyPool& pool);
 void prefault_small_any(uint8_t* p, size_t n);

@@ -718,6 +718,10 @@ int set_synth_kind(pgh_ctx* c, int kind) {
     return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_set_synth_kind(k, kind); }, (int)G(c)->kids.size());
 }
 
+int set_ingest_ranges(pgh_ctx* c, int on) {
+    return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_set_ingest_ranges(k, on); }, (int)G(c)->kids.size());
+}
+
 int set_weights(pgh_ctx* c, const float* w, int n) {
     if (!w || n <= 0) return fail(c, PGH_E_ARG, "need a non-empty weight vector");
     return fan(c, [&](int, pgh_ctx* k) -> int { return pgh_set_weights(k, w, n); });

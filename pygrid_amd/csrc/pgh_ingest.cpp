@@ -32,7 +32,7 @@ int pgh_ingest_raw(pgh_ctx* c, int client, const void* flat, size_t nbytes, int 
 }
 
 namespace {
-int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>& pieces, int slot);
+int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>& pieces, int slot, bool ranged);
 }
 
 int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
@@ -49,6 +49,9 @@ int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
     DeviceGuard g(c->device);
     int slot = 0;
     RC(claim_slot(c, client, &slot));
+    // report-time ingest (pgh_set_ingest_ranges): in chunks with an event each, so a close that
+    // starts while this DMA is in flight folds each param range as soon as it has landed
+    const bool ranged = c->ingest_ranges && !c->streaming && c->pg >= (1 << 20);
     if (n && !pieces.empty() && c->pinned_gather && is_pinned(pb)) {
         // Page-locked message (a report decoded straight into pgh_host_alloc memory,
         // pygrid_amd.report.PinnedPool): no staging copy.  The part of the message holding this
@@ -56,7 +59,7 @@ int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
         // k_gather_f32 moves the payloads into the slab row; the call waits for the DMA only (the
         // buffer is borrowed), the gather runs on behind it on the copy stream.
         const double t0 = now_ms();
-        RC(pinned_gather_ingest(c, pb, pieces, slot));
+        RC(pinned_gather_ingest(c, pb, pieces, slot, ranged));
         c->st.h2d_ms_total += now_ms() - t0;
         return mark_ingested(c, client, slot);
     }
@@ -75,7 +78,12 @@ int pgh_ingest_state(pgh_ctx* c, int client, const uint8_t* pb, size_t n) {
         c->st.h2d_bytes_total += off;
         return mark_ingested(c, client, slot);
     }
-    RC(stage_pieces_h2d(c, row_dest(c, slot, 0), pieces));
+    size_t total = 0;
+    for (auto& p : pieces) total += p.n;
+    if (ranged && total == (size_t)c->pg * 4 && total <= c->pin_slot)
+        RC(stage_pieces_h2d_ranged(c, row_dest(c, slot, 0), pieces, total));
+    else
+        RC(stage_pieces_h2d(c, row_dest(c, slot, 0), pieces));
     return mark_ingested(c, client, slot);
 }
 
@@ -193,6 +201,7 @@ int stage_share_msg(pgh_ctx* c, ShareMsg& m, uint8_t* dev) {
             uint8_t* dst = pin + ((size_t)m.chunks[q].off - s0);
             m.st[q] = pgh_state::varint_copy_stats(dst, m.src[q], (size_t)m.chunks[q].n);
         });
+        ++c->copy_seq;
         CK(c, hipMemcpyAsync(dev + s0, pin, fill, hipMemcpyHostToDevice, c->copy));
         CK(c, hipEventRecord(c->pin_ev[ps], c->copy));
         c->pin_used[ps] = true;
@@ -205,8 +214,10 @@ int stage_share_msg(pgh_ctx* c, ShareMsg& m, uint8_t* dev) {
 }
 
 // pgh_ingest_state of a page-locked message: [first payload, last payload end) of this shard in one
-// DMA to d_vbytes, the gather table behind it, then k_gather_f32 into the slot's row.
-int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>& pieces, int slot) {
+// DMA to d_vbytes, the gather table behind it, then k_gather_f32 into the slot's row.  `ranged`
+// (pgh_set_ingest_ranges): the table's chunks are cut at INGEST_CHUNK param boundaries and the DMA +
+// gather run chunk by chunk, rng_ev[k] behind chunk k's gather.
+int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>& pieces, int slot, bool ranged) {
     const size_t a = (size_t)(pieces.front().src - pb) & ~(size_t)63;
     const size_t b = (size_t)(pieces.back().src - pb) + pieces.back().n;
     std::vector<pgh::GChunk> tab;
@@ -215,11 +226,16 @@ int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>
     for (auto& p : pieces) {
         const int64_t nf = (int64_t)(p.n / 4);
         const int64_t src = (int64_t)((size_t)(p.src - pb) - a);
-        for (int64_t k = 0; k < nf; k += pgh::GATHER_CHUNK)
-            tab.push_back({src + 4 * k, dst + k, (int32_t)std::min<int64_t>(pgh::GATHER_CHUNK, nf - k), 0});
+        for (int64_t k = 0; k < nf;) {
+            int64_t len = std::min<int64_t>(pgh::GATHER_CHUNK, nf - k);
+            if (ranged) len = std::min(len, (((dst + k) / INGEST_CHUNK) + 1) * INGEST_CHUNK - (dst + k));
+            tab.push_back({src + 4 * k, dst + k, (int32_t)len, 0});
+            k += len;
+        }
         dst += nf;
         total += p.n;
     }
+    ranged = ranged && dst == c->pg;
     if (tab.empty()) return PGH_OK;
     RC(grow_device(c, (void**)&c->d_vbytes, &c->vbytes_cap, b - a + 16, "pinned message buffer"));
     const size_t tb = tab.size() * sizeof(pgh::GChunk);
@@ -242,17 +258,45 @@ int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>
         c->gtab_used = false;
     }
     std::memcpy(c->h_gtab, tab.data(), tb);
+    ++c->copy_seq;
     CK(c, hipMemcpyAsync(c->d_gtab, c->h_gtab, tb, hipMemcpyHostToDevice, c->copy));
     CK(c, hipEventRecord(c->gtab_ev, c->copy));
     c->gtab_used = true;
-    CK(c, hipMemcpyAsync(c->d_vbytes, pb + a, b - a, hipMemcpyHostToDevice, c->copy));
-    const bool async = host_async(pb + a, b - a);
-    if (async) RC(host_dma_queued(c, pb + a, b - a, c->copy));  // the block's owner waits (pgh_host_wait)
-    else CK(c, hipEventRecord(c->gdma_ev, c->copy));
     const Dest d = row_dest(c, slot, 0);
-    const hipError_t e = pgh::launch_gather_f32(c->d_vbytes, c->d_gtab, (int)tab.size(), (float*)d.base, d.map,
-                                                c->copy);
-    if (e != hipSuccess) return fail(c, PGH_E_HIP, "gather launch failed: %s", hipGetErrorString(e));
+    const bool async = host_async(pb + a, b - a);
+    if (ranged) {
+        const int K = (int)((c->pg + INGEST_CHUNK - 1) / INGEST_CHUNK);
+        while ((int)c->rng_ev.size() < K) {
+            hipEvent_t ev = nullptr;
+            CK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            c->rng_ev.push_back(ev);
+        }
+        size_t e0 = 0;
+        for (int k = 0; k < K; ++k) {
+            size_t e1 = e0;
+            while (e1 < tab.size() && tab[e1].dst < (int64_t)(k + 1) * INGEST_CHUNK) ++e1;
+            if (e1 > e0) {
+                const size_t lo = (size_t)tab[e0].src, hi = (size_t)tab[e1 - 1].src + 4 * (size_t)tab[e1 - 1].n;
+                CK(c, hipMemcpyAsync(c->d_vbytes + lo, pb + a + lo, hi - lo, hipMemcpyHostToDevice, c->copy));
+                const hipError_t e = pgh::launch_gather_f32(c->d_vbytes, c->d_gtab + e0, (int)(e1 - e0),
+                                                            (float*)d.base, d.map, c->copy);
+                if (e != hipSuccess) return fail(c, PGH_E_HIP, "gather launch failed: %s", hipGetErrorString(e));
+            }
+            CK(c, hipEventRecord(c->rng_ev[(size_t)k], c->copy));
+            e0 = e1;
+        }
+        if (async) RC(host_dma_queued(c, pb + a, b - a, c->copy));  // behind every chunk's DMA
+        else CK(c, hipEventRecord(c->gdma_ev, c->copy));
+        c->rng_seq = c->copy_seq;
+        c->rng_n = K;
+    } else {
+        CK(c, hipMemcpyAsync(c->d_vbytes, pb + a, b - a, hipMemcpyHostToDevice, c->copy));
+        if (async) RC(host_dma_queued(c, pb + a, b - a, c->copy));  // the block's owner waits (pgh_host_wait)
+        else CK(c, hipEventRecord(c->gdma_ev, c->copy));
+        const hipError_t e = pgh::launch_gather_f32(c->d_vbytes, c->d_gtab, (int)tab.size(), (float*)d.base, d.map,
+                                                    c->copy);
+        if (e != hipSuccess) return fail(c, PGH_E_HIP, "gather launch failed: %s", hipGetErrorString(e));
+    }
     if (!async) CK(c, hipEventSynchronize(c->gdma_ev));
     c->st.h2d_bytes_total += total;
     return PGH_OK;
@@ -302,6 +346,7 @@ int decode_share_msgs(pgh_ctx* c, std::vector<ShareMsg>& msgs, int slot, pgh_ctx
         std::memcpy(c->h_vtab + at, m.chunks.data(), m.chunks.size() * sizeof(pgh::VChunk));
         at += m.chunks.size();
     }
+    ++c->copy_seq;
     CK(c, hipMemcpyAsync(b.tab, c->h_vtab, tb, hipMemcpyHostToDevice, c->copy));
     CK(c, hipEventRecord(c->vtab_ev, c->copy));
     c->vtab_used = true;
@@ -380,6 +425,7 @@ int pgh_synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n) {
         // (beside the fold on the copy stream, the write-heavy fill and the read-only fold shared
         // HBM 13 % worse, r02p), grid capped at 8192 workgroups (r01t), non-temporal stores
         const hipStream_t gs = c->streaming ? c->stream : c->copy;
+        ++c->copy_seq;
         if (c->dtype == PGH_F32)
             e = pgh::launch_synth_f32((float*)slot_row(c, slot, 0), slab_map(c), c->nb * c->bw, run, c->pg, seed,
                                       pgh::STREAM_DIFF, c->client_base + client, c->lo, pgh::DIFF_SCALE, gs,
@@ -403,6 +449,13 @@ int pgh_set_synth_kind(pgh_ctx* c, int kind) {
     if (!c) return PGH_E_ARG;
     if (kind != 0 && kind != 1) return fail(c, PGH_E_ARG, "synthetic generator kind %d is not 0 or 1", kind);
     c->synth_kind = kind;
+    return PGH_OK;
+}
+
+int pgh_set_ingest_ranges(pgh_ctx* c, int on) {
+    if (c && c->grp) return pgh_group_api::set_ingest_ranges(c, on);
+    if (!c) return PGH_E_ARG;
+    c->ingest_ranges = on != 0;
     return PGH_OK;
 }
 

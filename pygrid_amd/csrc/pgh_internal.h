@@ -57,6 +57,7 @@ int ingest_state_shares(pgh_ctx* c, int client, int n_parties, const uint8_t* co
 int synth_fill(pgh_ctx* c, uint64_t seed, int n_clients);
 int synth_ingest(pgh_ctx* c, uint64_t seed, int client0, int n);
 int set_synth_kind(pgh_ctx* c, int kind);
+int set_ingest_ranges(pgh_ctx* c, int on);
 int set_weights(pgh_ctx* c, const float* w, int n);
 int fedavg(pgh_ctx* c, int mode, const float* ckpt, float* out);
 int ckpt_upload(pgh_ctx* c, const float* ckpt, size_t nbytes);

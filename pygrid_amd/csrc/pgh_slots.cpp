@@ -36,7 +36,11 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
     }
     DeviceGuard g(c->device);
     const hipStream_t s = c->stream;
-    RC(order_after_ingest(c, s));
+    // a close right behind a ranged ingest (pgh_set_ingest_ranges) orders each FINAL range after the
+    // chunk of the last report it reads instead of after the whole copy stream
+    const bool ranged = final && n > 0 && n <= pgh::ROWTAB_MAX && c->pg >= (1 << 20) && ranged_ingest_valid(c);
+    if (ranged && c->dec_last) CK(c, hipStreamWaitEvent(s, c->dec_last, 0));
+    else RC(order_after_ingest(c, s));
     if (mode == PGH_WEIGHTED_MEAN && n > 0) {
         if ((int64_t)c->weights.size() < total)
             return fail(c, PGH_E_STATE, "weighted mean: %zu weights for %lld clients", c->weights.size(),
@@ -77,6 +81,12 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
         for (int r = 0; r < K; ++r) {
             const hipStream_t rs = s;
             const int64_t lo = std::min(c->pg, RF * r), hi = K == 1 ? c->pg : std::min(c->pg, RF * (r + 1));
+            if (ranged && K > 1) {  // every chunk this range reads has landed ...
+                for (int64_t k = lo / INGEST_CHUNK; k <= (hi - 1) / INGEST_CHUNK; ++k)
+                    CK(c, hipStreamWaitEvent(rs, c->rng_ev[(size_t)k], 0));
+            } else if (ranged && r == 0) {
+                CK(c, hipStreamWaitEvent(rs, c->rng_ev[(size_t)(c->rng_n - 1)], 0));  // ... or all of it
+            }
             pgh::FedavgArgs ar = a;
             ar.map.off = lo;
             ar.p = hi - lo;
@@ -88,6 +98,7 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
             RC(timed_launch(c, rs, bytes, [&] { return pgh::launch_fedavg_rows(ar, tab, rs); }));
             if (K > 1 && (hi % (2 * RF) == 0 || hi == c->pg)) RC(add_final_mark(c, rs, hi));
         }
+        if (ranged && K > 1) c->marks_after_ranges = true;
         done += m;
     } while (done < n);
     RC(record_fold(c, s));

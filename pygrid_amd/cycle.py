@@ -277,6 +277,8 @@ class CycleAggregator:
             self._resident = None
         else:
             eng.reset()
+        if hasattr(eng, "set_ingest_ranges"):
+            eng.set_ingest_ranges(False)  # every diff at once: whole-message copies keep the PCIe rate
         self._numel, self._cap, self._dtype, self._parties = numel, eng.max_clients, dtype, parties
 
     # ---- bytes in / bytes out: the replaceable slice cycle_manager.py:240-303 -------------------

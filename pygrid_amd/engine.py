@@ -408,6 +408,11 @@ class Engine:
         self._check(self._lib.pgh_sync(self._h), "sync")
 
     # ---- observability -------------------------------------------------------------------------
+    def set_ingest_ranges(self, on: bool):
+        """Report-time ingest (pgh_set_ingest_ranges): each State diff goes to HBM in param ranges
+        with an event each, so the close's fold starts on the last report's ranges as they land."""
+        self._check(self._lib.pgh_set_ingest_ranges(self._h, int(bool(on))), "set_ingest_ranges")
+
     def set_variant(self, v: int):
         """Kernel variant (csrc/pgh_kernels.hip table); -1 restores the default."""
         self._check(self._lib.pgh_set_variant(self._h, int(v)), "set_variant")

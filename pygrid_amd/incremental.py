@@ -60,6 +60,7 @@ from __future__ import annotations
 import bisect
 import itertools
 import logging
+import os
 import threading
 from typing import Callable, Dict, Hashable, List, Optional, Sequence
 
@@ -124,6 +125,9 @@ class IncrementalCycle:
             engine.reserve(self.slots)
         else:
             engine.reset()
+        if hasattr(engine, "set_ingest_ranges"):
+            # the close overlaps the tail of the last report's copy (pgh_set_ingest_ranges)
+            engine.set_ingest_ranges(os.environ.get("PGH_INGEST_RANGES", "1") != "0")
         self._ckpt: Optional[bytes] = None  # checkpoint bytes whose payloads are resident in HBM
         if checkpoint is not None and getattr(engine, "ckpt_owner", None) is not None \
                 and getattr(engine, "ckpt_bytes", None) is checkpoint:

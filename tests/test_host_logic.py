@@ -142,9 +142,11 @@ class FakeAggregator:
     def __init__(self):
         self.calls = []
 
-    def average_plan_diffs(self, server_config, checkpoint, diffs, avg_plan=None, plan_key=None):
+    def average_plan_diffs(self, server_config, checkpoint, diffs, avg_plan=None, weights=None, framing="fresh",
+                           plan_key=None):  # CycleAggregator.average_plan_diffs's signature
         cycle.select_mode(server_config, avg_plan, plan_key=plan_key)  # same dispatch as the real one
         self.calls.append((checkpoint, list(diffs), avg_plan))
+        self.framing = framing
         return b"NEW"
 
 

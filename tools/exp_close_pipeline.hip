@@ -11,7 +11,13 @@
 //
 // Variants (one letter each): timing events around every range: n = none, d = default flags,
 //   f = hipEventDisableSystemFence, v = hipEventReleaseToDevice; marks: d / f / v; wait: g = the
-//   copy stream waits on the marks (GPU side), h = the host waits for each mark, then issues.
+//   copy stream waits on the marks (GPU side), h = the host waits for each mark, then issues;
+//   optional 4th letter, the last report's 47 MB H2D into row 0 issued just before the close
+//   (the close's trigger comes while it is in flight): w = the fold waits for all of it,
+//   c = it is issued as 12 range-aligned chunks with an event each and fold range k waits only
+//   for chunk k, a = the same with the chunks alternating over two streams (the D2H pieces on
+//   their own stream either way).  Also reported: the 47 MB H2D alone as one copy, as 12 or 6
+//   chunks on one stream and as 12 chunks alternating over two streams.
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/exp_close_pipeline.hip -o tools/_exp_close_pipeline
 // Run:   tools/_exp_close_pipeline [reps] [variant ...]   -> one JSON line
 #include <hip/hip_runtime.h>
@@ -90,13 +96,36 @@ int main(int argc, char** argv) {
         for (int r = 0; r < ROWS; ++r) CK(hipMemcpy(rows + (size_t)r * ld, h.data(), ld * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy(ckpt, h.data(), ld * 4, hipMemcpyHostToDevice));
     }
-    uint8_t *host = nullptr, *want = nullptr;
+    uint8_t *host = nullptr, *want = nullptr, *report = nullptr;
     const size_t bytes = P * 4;
     CK(hipHostMalloc((void**)&host, bytes, hipHostMallocDefault));
     CK(hipHostMalloc((void**)&want, bytes, hipHostMallocDefault));
-    hipStream_t sf, sc;
+    CK(hipHostMalloc((void**)&report, bytes, hipHostMallocDefault));
+    {
+        std::vector<float> h(P);
+        for (size_t i = 0; i < P; ++i) h[i] = (float)((i * 2654435761u) % 1000) * 1e-3f;
+        std::memcpy(report, h.data(), bytes);
+    }
+    hipStream_t sf, sc, sh, sh2;
     CK(hipStreamCreateWithFlags(&sf, hipStreamNonBlocking));
     CK(hipStreamCreateWithFlags(&sc, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&sh, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&sh2, hipStreamNonBlocking));
+    std::map<std::string, std::vector<double>> h2d_ms;
+    for (int rep = 0; rep < 11; ++rep) {
+        for (const char* how : {"whole", "chunks12", "chunks6", "chunks12_2streams"}) {
+            const std::string hw = how;
+            const size_t chunk = hw == "whole" ? bytes : hw == "chunks6" ? (8u << 20) : (4u << 20);
+            CK(hipDeviceSynchronize());
+            const auto a = std::chrono::steady_clock::now();
+            for (size_t off = 0, k = 0; off < bytes; off += chunk, ++k)
+                CK(hipMemcpyAsync((uint8_t*)rows + off, report + off, std::min(chunk, bytes - off),
+                                  hipMemcpyHostToDevice, (hw == "chunks12_2streams" && (k & 1)) ? sh2 : sh));
+            CK(hipStreamSynchronize(sh));
+            CK(hipStreamSynchronize(sh2));
+            if (rep) h2d_ms[hw].push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count());
+        }
+    }
     const int K = (int)((P + RANGE - 1) / RANGE);
     const int NP = (int)((bytes + PIECE - 1) / PIECE);
     std::map<std::string, std::vector<double>> span;
@@ -119,10 +148,26 @@ int main(int argc, char** argv) {
             }
             hipEvent_t done;
             CK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+            std::vector<hipEvent_t> hv(K);
+            for (auto& e : hv) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             std::memset(host, 0, bytes);
+            const char h2d = v.size() > 3 ? v[3] : 'x';
             const auto t0 = std::chrono::steady_clock::now();
+            if (h2d == 'w') {
+                CK(hipMemcpyAsync(rows, report, bytes, hipMemcpyHostToDevice, sh));
+                CK(hipEventRecord(hv[0], sh));
+                CK(hipStreamWaitEvent(sf, hv[0], 0));
+            } else if (h2d == 'c' || h2d == 'a') {
+                for (int k = 0; k < K; ++k) {
+                    const size_t lo = k * RANGE, hi = std::min(P, (k + 1) * RANGE);
+                    hipStream_t st = (h2d == 'a' && (k & 1)) ? sh2 : sh;
+                    CK(hipMemcpyAsync(rows + lo, report + lo * 4, (hi - lo) * 4, hipMemcpyHostToDevice, st));
+                    CK(hipEventRecord(hv[k], st));
+                }
+            }
             for (int k = 0; k < K; ++k) {
                 const size_t lo = k * RANGE, hi = std::min(P, (k + 1) * RANGE);
+                if (h2d == 'c' || h2d == 'a') CK(hipStreamWaitEvent(sf, hv[k], 0));
                 if (v[0] != 'n') CK(hipEventRecord(ta[k], sf));
                 k_range<<<1024, 256, 0, sf>>>((const float4*)rows, (const float4*)ckpt, (float4*)out, lo / 4,
                                               (hi + 3) / 4, ld4);
@@ -147,6 +192,7 @@ int main(int argc, char** argv) {
             if (std::memcmp(host, want, bytes) != 0) ++bad[v];
             if (rep) span[v].push_back(ms);
             for (auto e : mk) CK(hipEventDestroy(e));
+            for (auto e : hv) CK(hipEventDestroy(e));
             for (auto e : ta) CK(hipEventDestroy(e));
             for (auto e : tb) CK(hipEventDestroy(e));
             CK(hipEventDestroy(done));
@@ -160,6 +206,15 @@ int main(int argc, char** argv) {
         std::sort(s.begin(), s.end());
         std::printf("%s\"%s\": {\"median_ms\": %.4f, \"min_ms\": %.4f, \"max_ms\": %.4f, \"stale_runs\": %d}",
                     first ? "" : ", ", kv.first.c_str(), s[s.size() / 2], s.front(), s.back(), bad[kv.first]);
+        first = false;
+    }
+    std::printf("}, \"h2d_47MB\": {");
+    first = true;
+    for (auto& kv : h2d_ms) {
+        auto s2 = kv.second;
+        std::sort(s2.begin(), s2.end());
+        std::printf("%s\"%s\": {\"median_ms\": %.4f, \"GBps\": %.1f}", first ? "" : ", ", kv.first.c_str(),
+                    s2[s2.size() / 2], bytes / (s2[s2.size() / 2] * 1e6));
         first = false;
     }
     std::printf("}}\n");
