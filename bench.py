@@ -1590,7 +1590,7 @@ def e2e_close(ctx, args, eng, n_clients: int, steps: int = 2):
                           "State bytes in host memory -> new checkpoint bytes (BASELINE.md cycle close; PCIe-inclusive)"}
 
 
-def report_close(ctx, args, eng, cycles: int = 4, assigned: int = 100):
+def report_close(ctx, args, eng, cycles: int = 8, assigned: int = 100):
     """The close as a node running report-time aggregation sees it, triggered
     the way the reference triggers it: the report that completes the cycle requests the close
     (``submit_worker_diff`` -> ``run_task_once("complete_cycle", ...)``, cycle_manager.py:176-178)
