@@ -14,10 +14,12 @@ the reference's own storage types and report handler code (VERDICT r3 next #1-#2
 
 ResNet-18, 100 workers assigned per cycle, 80 report (worker 0 and 19 others never do,
 routes.py:314; ``max_diffs`` = 80), shuffled arrival.  Arms: reports ``paced`` ``--gap-ms`` apart
-(default 5) or back to back (``b2b``), x the product default / speculative folds with the peeked
-close (``peek``) / without (``spec``) / certain-only folds (``certain``).
+(default 5) or back to back (``b2b``), x the product default (``default``: report-time
+aggregation) / the close-time path only (``closetime``: ``install(report_time=False)``, every diff
+read from the DB and folded at the close).  (The speculative arms of r04 went with the speculative
+close in r05.)
 
-    python tools/node_sim.py [cycles] [--gap-ms=5] [--no-pinned] [--db=PATH] [--arms=paced_spec,...] [--cpu]
+    python tools/node_sim.py [cycles] [--gap-ms=5] [--no-pinned] [--db=PATH] [--arms=paced_default,b2b_closetime,...] [--cpu]
                              [--devices=0,0]   (a one-process group, as install(devices=[...]))
 
 Prints one JSON line: per arm the report handler latency (p50 / p99 / max) and its phases (the
@@ -128,7 +130,7 @@ def run_arm(eng, cycles, gap_ms, opts, pinned, db, rng, ckpt, texts, framing="fr
             return finish(self, *a, **k)
         finally:
             engine_close.append((time.perf_counter() - t0) * 1e3)
-            close_info.append({k_: self.last_close.get(k_) for k_ in ("peeked", "early", "n", "from_db", "refold")})
+            close_info.append({k_: self.last_close.get(k_) for k_ in ("early", "n", "from_db", "refold")})
     incremental.IncrementalCycle.finish = timed_finish
     try:
         cfg = {"min_diffs": REPORTERS, "max_diffs": REPORTERS, "num_cycles": 0}
@@ -212,7 +214,7 @@ def main():
     gap = float(opt.get("gap-ms", 5.0))
     pinned = "--no-pinned" not in sys.argv
     db = f"sqlite:///{opt['db']}" if "db" in opt else "sqlite://"
-    want = opt.get("arms", "paced_default,paced_peek,paced_spec,paced_certain,b2b_default,b2b_certain").split(",")
+    want = opt.get("arms", "paced_default,b2b_default").split(",")
     rng = np.random.default_rng(2024)
     ckpt = build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in RESNET18_SHAPES])
     texts = [base64.b64encode(build_state_fast([rng.standard_normal(s, dtype=np.float32) * np.float32(1e-2)
@@ -220,8 +222,7 @@ def main():
     arms = {}
     if "--cpu" in sys.argv:  # dev check of this tool on a GPU-less box: the tests' numpy engine
         from fake_engine import NumpyEngine
-    kinds = {"default": {}, "peek": {"speculate": True, "peek": True}, "spec": {"speculate": True, "peek": False},
-             "certain": {"speculate": False}}
+    kinds = {"default": {}, "closetime": {"report_time": False}}
     framing = "template" if "--cpu" in sys.argv else "fresh"
     devices = [int(d) for d in opt["devices"].split(",")] if "devices" in opt else None
     with (_nullctx(NumpyEngine()) if "--cpu" in sys.argv else Engine(devices=devices) if devices else Engine(0)) as eng:
