@@ -4,9 +4,12 @@
 * K5 ``k_gather_f32``: a report decoded into a page-locked block (``report.PinnedPool``) is DMA'd
   whole and gathered into its slab row -- algorithmic bytes per launch 8 * P (the float payloads
   read once from the DMA'd message, written once into the row);
-* the speculative one-row fold ``k_fedavg_rows`` (``pgh_fold_slots_keep`` of one reported diff):
-  reads the row and the saved fold state, writes the new state -- 12 * P per launch (the close's
-  FINAL pass and the peek read the state + checkpoint and write P floats: also 12 * P).
+* the one-row fold ``k_fedavg_rows`` (workers report in assignment order, so each report's
+  position is certain at once; ``fold_batch=1`` folds it alone): reads the row and the running
+  state, writes the state -- 12 * P per launch (the first row: 8 * P; the close's FINAL pass reads
+  the state + checkpoint and writes P floats: also 12 * P).
+K5 is profiled on whole reports (``PGH_INGEST_RANGES=0``): with ranged report ingest (r05) each
+report's gather runs as one launch per 8 MiB chunk instead.
 
     python tools/prof_report_path.py run [cycles] [reports]       the workload (run it under rocprofv3)
     python tools/prof_report_path.py summarize <gpurun dir> <profiles dir>
@@ -35,6 +38,8 @@ KERNELS = {"k_gather_f32": 8 * P, "k_fedavg_rows<": 12 * P}
 
 
 def run(cycles: int, reports: int):
+    import os
+
     import numpy as np
 
     from pygrid_amd import Engine
@@ -52,7 +57,8 @@ def run(cycles: int, reports: int):
     pool = PinnedPool(max_blocks=8)
     with Engine(0) as eng:
         for cyc in range(cycles):
-            inc = IncrementalCycle(eng, numel, slots=reports + 2, checkpoint=ck, speculate=True)
+            os.environ.setdefault("PGH_INGEST_RANGES", "0")  # one K5 launch per report (docstring)
+            inc = IncrementalCycle(eng, numel, slots=reports + 2, fold_batch=1, checkpoint=ck)
             for w in range(reports):
                 inc.assigned(w)
             for w in range(reports):
