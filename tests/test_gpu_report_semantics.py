@@ -3,7 +3,9 @@
 re-folds from the DB (pgh_fold_slots_restart), the close follows the DB's order -- bit-exact
 against the oracle over the diffs the reference's close would read (cycle_manager.py:243-296);
 and the whole node wiring (pygrid_amd.node.install) on the GPU saves the same bytes as the
-reference node (tests/fake_node.py)."""
+reference node (tests/fake_node.py).  Every test runs twice: on a small model and on one of > 1 M
+params, where each diff goes to HBM in ranges and the close waits per range on the last report's
+copy (ranged report ingest, pgh_set_ingest_ranges)."""
 import numpy as np
 import pytest
 
@@ -12,6 +14,13 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 F = np.float32
 SHAPES = [(300, 17), (17,), (1000,)]
+RANGED_SHAPES = [(2100, 2000), (1000,), (3, 333_333), (7,)]  # 5.3 M params: 3 ingest ranges, the last short
+
+
+@pytest.fixture(autouse=True, params=["small", "ranged"])
+def _model(request, monkeypatch):
+    if request.param == "ranged":
+        monkeypatch.setitem(globals(), "SHAPES", RANGED_SHAPES)
 
 
 def bits(a):
