@@ -1369,8 +1369,6 @@ pgh_ctx* new_group_ctx(pgh_group* g, int device) {
 void free_group_ctx(pgh_ctx* c) { delete c; }
 int device_of(const pgh_ctx* c) { return c->device; }
 hipStream_t stream_of(const pgh_ctx* c) { return c->stream; }
-int64_t shard_lo(const pgh_ctx* c) { return c->lo; }
-int64_t shard_len(const pgh_ctx* c) { return c->pg; }
 int set_vec_min(pgh_ctx* c, int64_t n) {
     if (n < 0) return fail(c, PGH_E_ARG, "negative vector length");
     c->vec_min = n;

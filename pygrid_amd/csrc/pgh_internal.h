@@ -24,8 +24,6 @@ void free_group_ctx(pgh_ctx* c);                    // the shell only (the group
 // per-context internals the group driver uses
 int device_of(const pgh_ctx* c);
 hipStream_t stream_of(const pgh_ctx* c);
-int64_t shard_lo(const pgh_ctx* c);
-int64_t shard_len(const pgh_ctx* c);
 // [P_shard] device vectors at least n elements long from the next pgh_reserve on (collectives send
 // equal padded shards).
 int set_vec_min(pgh_ctx* c, int64_t n);
