@@ -37,3 +37,19 @@ def test_store_returns_the_same_object_for_resident_reuse():
     blob = bytes(1000)
     st.save(3, blob)
     assert st.latest(3) is blob  # CycleAggregator reuses the HBM copy on identity
+
+
+def test_invalidate_and_cached_bytes():
+    """``invalidate`` (one model or all) makes the next lookup fall through to the DB; ``keep``
+    bounds what ``cached_bytes`` counts."""
+    st = CheckpointStore(keep=2)
+    for k in range(4):
+        st.save(1, bytes(100 + k))
+    st.save(2, bytes(50))
+    assert st.cached_bytes == 102 + 103 + 50  # model 1 keeps its newest two
+    assert st.lookup(model_id=1, alias="latest").value == bytes(103)
+    st.invalidate(1)
+    assert st.lookup(model_id=1) is None and st.lookup(model_id=2).value == bytes(50)
+    assert st.cached_bytes == 50
+    st.invalidate()
+    assert st.cached_bytes == 0 and st.lookup(model_id=2) is None
