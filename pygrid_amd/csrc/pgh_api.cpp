@@ -185,7 +185,8 @@ void slab_geometry(int64_t pg, size_t es, size_t block_bytes, int64_t* bw, int64
 
 // Elements [i0, i0 + n) of one row from contiguous host memory: the partial first block, the
 // whole blocks as ONE 2-D copy (block rows bstride apart), the partial last block.
-int h2d_range(pgh_ctx* c, const Dest& d, int64_t i0, const uint8_t* src, int64_t n, hipStream_t s) {
+int h2d_range(pgh_ctx* c, const Dest& d, int64_t i0, const uint8_t* src, int64_t n, hipStream_t s,
+              size_t src_room) {
     const size_t es = d.es;
     if (n <= 0) return PGH_OK;
     ++c->copy_seq;
@@ -201,12 +202,15 @@ int h2d_range(pgh_ctx* c, const Dest& d, int64_t i0, const uint8_t* src, int64_t
         src += (size_t)(e - i) * es;
         i = e;
     }
-    const int64_t full = (i1 - i) / bw;
+    int64_t full = (i1 - i) / bw;
+    const int64_t rest = (i1 - i) - full * bw;
+    const bool pad = rest > 0 && d.len > 0 && i1 == d.len && src_room >= (size_t)(bw - rest) * es;
+    if (pad) ++full;  // the row's partial last block as a whole one: one copy less per row
     if (full > 0) {
         CK(c, hipMemcpy2DAsync(d.base + (size_t)d.map.at(i) * es, (size_t)d.map.bstride * es, src, (size_t)bw * es,
                                (size_t)bw * es, (size_t)full, hipMemcpyHostToDevice, s));
         src += (size_t)(full * bw) * es;
-        i += full * bw;
+        i = std::min(i1, i + full * bw);
     }
     if (i < i1)  // tail
         CK(c, hipMemcpyAsync(d.base + (size_t)d.map.at(i) * es, src, (size_t)(i1 - i) * es, hipMemcpyHostToDevice, s));
@@ -288,7 +292,8 @@ int stage_pieces_h2d_ranged(pgh_ctx* c, const Dest& dst, const std::vector<Piece
             if (poff == pieces[pi].n) { ++pi; poff = 0; }
         }
         c->pool_copy->run(segs);
-        RC(h2d_range(c, dst, (int64_t)(a / 4), c->h_pin[slot] + a, (int64_t)((b - a) / 4), c->copy));
+        RC(h2d_range(c, dst, (int64_t)(a / 4), c->h_pin[slot] + a, (int64_t)((b - a) / 4), c->copy,
+                     b == total ? c->pin_slot - b : 0));
         CK(c, hipEventRecord(c->rng_ev[(size_t)k], c->copy));
     }
     CK(c, hipEventRecord(c->pin_ev[slot], c->copy));
@@ -328,7 +333,8 @@ int stage_pieces_h2d(pgh_ctx* c, const Dest& dst, const std::vector<Piece>& piec
         }
         c->pool_copy->run(segs);
         // slot fills are whole multiples of 4 KiB but the last, so `done` stays element-aligned
-        RC(h2d_range(c, dst, (int64_t)(done / dst.es), c->h_pin[slot], (int64_t)(fill / dst.es), c->copy));
+        RC(h2d_range(c, dst, (int64_t)(done / dst.es), c->h_pin[slot], (int64_t)(fill / dst.es), c->copy,
+                     c->pin_slot - fill));
         CK(c, hipEventRecord(c->pin_ev[slot], c->copy));
         c->pin_used[slot] = true;
         done += fill;

@@ -370,8 +370,11 @@ struct Dest {
     uint8_t* base;       // row start in block 0 / vector start
     pgh::SlabMap map;
     size_t es;
+    int64_t len = 0;     // a slab row: its elements (the last block's columns past it are padding)
 };
-inline Dest row_dest(pgh_ctx* c, int slot, int party) { return Dest{slot_row(c, slot, party), slab_map(c), esize(c->dtype)}; }
+inline Dest row_dest(pgh_ctx* c, int slot, int party) {
+    return Dest{slot_row(c, slot, party), slab_map(c), esize(c->dtype), c->pg};
+}
 inline Dest vec_dest(void* v, int64_t n, size_t es) { return Dest{(uint8_t*)v, pgh::single_block(n), es}; }
 
 // ---- kernel timing -------------------------------------------------------------------------------
@@ -414,7 +417,11 @@ constexpr size_t D2H_PIECE = 8u << 20;
 constexpr int64_t INGEST_CHUNK = (int64_t)(D2H_PIECE / 4);
 
 bool is_pinned(const void* p);
-int h2d_range(pgh_ctx* c, const Dest& d, int64_t i0, const uint8_t* src, int64_t n, hipStream_t s);
+// src_room: bytes readable at src past the n elements (a staging slot's unused rest); a range that
+// ends a slab row whose last block is partial then goes as full blocks in one 2D copy (the padding
+// columns take whatever follows in the slot) instead of a 2D copy plus a tail copy.
+int h2d_range(pgh_ctx* c, const Dest& d, int64_t i0, const uint8_t* src, int64_t n, hipStream_t s,
+              size_t src_room = 0);
 int stage_pieces_h2d(pgh_ctx* c, const Dest& dst, const std::vector<Piece>& pieces);
 int stage_pieces_h2d_ranged(pgh_ctx* c, const Dest& dst, const std::vector<Piece>& pieces, size_t total);
 bool ranged_ingest_valid(const pgh_ctx* c);
