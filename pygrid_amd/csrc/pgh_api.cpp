@@ -127,6 +127,7 @@ void free_slab(pgh_ctx* c) {
     c->ckpt_valid = false;
     for (auto& m : c->final_marks) c->rmark_pool.push_back(m.ev);
     c->final_marks.clear();
+    c->pre_d2h_valid = false;
     (void)hipFree(c->d_acc); c->d_acc = nullptr;
     (void)hipFree(c->d_uacc); c->d_uacc = nullptr;
     (void)hipFree(c->d_sum); c->d_sum = nullptr;
@@ -277,9 +278,8 @@ int stage_pieces_h2d_ranged(pgh_ctx* c, const Dest& dst, const std::vector<Piece
         CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         c->rng_ev.push_back(e);
     }
-    const int slot = c->pin_next;
-    c->pin_next ^= 1;
-    if (c->pin_used[slot]) CK(c, hipEventSynchronize(c->pin_ev[slot]));
+    int slot = 0;
+    RC(take_pin_slot(c, &slot));
     size_t pi = 0, poff = 0;
     for (int k = 0; k < K; ++k) {
         const size_t a = (size_t)k * INGEST_CHUNK * 4, b = std::min(total, (size_t)(k + 1) * INGEST_CHUNK * 4);
@@ -319,9 +319,8 @@ int stage_pieces_h2d(pgh_ctx* c, const Dest& dst, const std::vector<Piece>& piec
     size_t total = 0, done = 0, pi = 0, poff = 0;
     for (auto& p : pieces) total += p.n;
     while (done < total) {
-        const int slot = c->pin_next;
-        c->pin_next ^= 1;
-        if (c->pin_used[slot]) CK(c, hipEventSynchronize(c->pin_ev[slot]));
+        int slot = 0;
+        RC(take_pin_slot(c, &slot));
         size_t fill = 0;
         std::vector<CopyPool::Seg> segs;
         while (fill < c->pin_slot && pi < pieces.size()) {
@@ -425,7 +424,7 @@ void prefault_parallel(uint8_t* p, size_t n, CopyPool& pool) {
 void clear_final_marks(pgh_ctx* c) {
     for (auto& m : c->final_marks) c->rmark_pool.push_back(m.ev);
     c->final_marks.clear();
-    c->marks_after_ranges = false;
+    c->pre_d2h_valid = false;
 }
 
 int add_final_mark(pgh_ctx* c, hipStream_t s, int64_t end) {
@@ -459,30 +458,24 @@ int join_aux(pgh_ctx* c, hipStream_t s) {
 int final_ranges(const pgh_ctx* c) { return c->final_split > 1 && c->pg >= (1 << 20) ? c->final_split : 1; }
 int64_t range_edge(const pgh_ctx* c, int k, int K) { return k >= K ? c->pg : (c->pg * k / K) & ~(int64_t)3; }
 
-// HBM bytes at `src` (after the work already on stream `s`) -> host pieces, through the pinned
-// ring, in pieces of at most D2H_PIECE.  Every piece that fits the ring (both slots: 2 x 128 MiB by
-// default, so any ResNet-18-sized result) is queued at once, each with an event, and the host copies
-// piece k out as soon as its event fires while the later pieces' DMAs run.  Queuing them all up
-// front keeps them on the SDMA engines: a D2H queued while another one still ran went to a blit
-// kernel (__amd_rocclr_copyBuffer), whose host writes then held back the end of every fold range
-// running beside it (48 -> 183-190 us, profiles/r05d/); queued before any ran they all went to SDMA
-// (profiles/r05e/).  `overlap`, if given, is host work run while the first DMA is in flight (the
-// checkpoint template's framing copy).  marks: src is the resident checkpoint: when its last fold
-// left range marks, the DMAs run on the copy stream, each behind the ranges that wrote its bytes
-// (the rest of the fold continues).
-int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>& pieces, hipStream_t s,
-                     const std::function<void()>& overlap, bool marks) {
-    size_t total = 0;
-    for (auto& p : pieces) total += p.n;
-    if (total == 0) return PGH_OK;
-    const bool piped = marks && !c->final_marks.empty();
-    // behind a ranged close (pgh_set_ingest_ranges) the copy stream still holds the last report's
-    // H2D: the pieces go on aux (idle in a slot fold), so the D2H runs beside that DMA
-    if (piped) s = c->marks_after_ranges ? c->aux : c->copy;
-    const size_t piece = std::min(c->pin_slot, D2H_PIECE);
-    const size_t per_slot = c->pin_slot / piece;  // >= 1 (pin_slot >= 4096)
+int take_pin_slot(pgh_ctx* c, int* slot) {
+    *slot = c->pin_next;
+    c->pin_next ^= 1;
+    if (c->pin_used[*slot]) CK(c, hipEventSynchronize(c->pin_ev[*slot]));
+    c->pre_d2h_valid = false;  // (conservative) its cells may be overwritten now
+    return PGH_OK;
+}
+
+int d2h_ring_begin(pgh_ctx* c, pgh_ctx::D2HRing* r, const uint8_t* src, size_t total, hipStream_t s, bool piped,
+                   bool may_wait) {
+    *r = pgh_ctx::D2HRing{};
+    r->src = src;
+    r->total = total;
+    r->piped = piped;
+    r->s = piped ? c->copy : s;
+    r->piece = std::min(c->pin_slot, D2H_PIECE);
+    r->per_slot = c->pin_slot / r->piece;  // >= 1 (pin_slot >= 4096)
     // an earlier staged ingest may still read a slot: use the free ones, wait only if neither is
-    int free_slot[2], n_free = 0;
     for (int k = 0; k < 2; ++k) {
         if (c->pin_used[k]) {
             const hipError_t q = hipEventQuery(c->pin_ev[k]);
@@ -490,49 +483,138 @@ int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>
             CK(c, q);
             c->pin_used[k] = false;
         }
-        free_slot[n_free++] = k;
+        r->free_slot[r->n_free++] = k;
     }
-    if (n_free == 0) {
+    if (r->n_free == 0 && !may_wait) return PGH_OK;
+    if (r->n_free == 0) {
         for (int k = 0; k < 2; ++k) {
             CK(c, hipEventSynchronize(c->pin_ev[k]));
             c->pin_used[k] = false;
-            free_slot[k] = k;
+            r->free_slot[k] = k;
         }
-        n_free = 2;
+        r->n_free = 2;
     }
-    const size_t cells = (size_t)n_free * per_slot;  // ring cells, one piece each
-    while (c->d2h_ev.size() < std::min<size_t>(cells, (total + piece - 1) / piece)) {
+    r->cells = (size_t)r->n_free * r->per_slot;  // ring cells, one piece each
+    r->n_pieces = (total + r->piece - 1) / r->piece;
+    while (c->d2h_ev.size() < std::min(r->cells, r->n_pieces)) {
         hipEvent_t e = nullptr;
         CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         c->d2h_ev.push_back(e);
     }
-    auto cell_ptr = [&](size_t j) { return c->h_pin[free_slot[j / per_slot]] + (j % per_slot) * piece; };
-    size_t queued = 0, done = 0;  // pieces queued / copied out
-    const size_t n_pieces = (total + piece - 1) / piece;
-    auto queue = [&](size_t j) -> int {
-        const size_t off = j * piece, len = std::min(piece, total - off);
-        if (piped) {  // wait for EVERY fold range the piece's floats come from
-            const int64_t first = (int64_t)(off / 4), last = (int64_t)((off + len + 3) / 4);
-            int64_t start = 0;
-            for (auto& m : c->final_marks) {
-                if (start >= last) break;
-                if (m.end > first) CK(c, hipStreamWaitEvent(s, m.ev, 0));
-                start = m.end;
+    return PGH_OK;
+}
+
+static uint8_t* d2h_cell(const pgh_ctx* c, const pgh_ctx::D2HRing& r, size_t j) {
+    return c->h_pin[r.free_slot[(j % r.cells) / r.per_slot]] + (j % r.per_slot) * r.piece;
+}
+
+// Piece j of a piped ring: have all the fold ranges its floats come from finished?  (wait: block
+// until they have.)  Marks may come from two streams (a split resident FINAL pass): every mark
+// overlapping the piece is checked.
+static int d2h_piece_ready(pgh_ctx* c, const pgh_ctx::D2HRing& r, size_t j, bool wait, bool* ready) {
+    *ready = true;
+    if (!r.piped) return PGH_OK;
+    const size_t off = j * r.piece, len = std::min(r.piece, r.total - off);
+    const int64_t first = (int64_t)(off / 4), last = (int64_t)((off + len + 3) / 4);
+    int64_t start = 0;
+    for (auto& m : c->final_marks) {
+        if (start >= last) break;
+        if (m.end > first) {
+            if (wait) {
+                CK(c, hipEventSynchronize(m.ev));
+            } else {
+                const hipError_t q = hipEventQuery(m.ev);
+                if (q == hipErrorNotReady) { *ready = false; return PGH_OK; }
+                CK(c, q);
             }
         }
-        CK(c, hipMemcpyAsync(cell_ptr(j % cells), src + off, len, hipMemcpyDeviceToHost, s));
-        CK(c, hipEventRecord(c->d2h_ev[j % cells], s));
-        return PGH_OK;
-    };
-    while (queued < n_pieces && queued < cells) RC(queue(queued++));
-    if (overlap) overlap();
-    while (done < n_pieces) {
-        const size_t off = done * piece, len = std::min(piece, total - off);
-        CK(c, hipEventSynchronize(c->d2h_ev[done % cells]));
-        scatter_out(cell_ptr(done % cells), off, len, pieces, *c->pool_copy);
-        ++done;
-        if (queued < n_pieces) RC(queue(queued++));  // into the cell just copied out
+        start = m.end;
     }
+    return PGH_OK;
+}
+
+static int d2h_issue(pgh_ctx* c, pgh_ctx::D2HRing* r) {
+    const size_t j = r->queued, off = j * r->piece, len = std::min(r->piece, r->total - off);
+    CK(c, hipMemcpyAsync(d2h_cell(c, *r, j), r->src + off, len, hipMemcpyDeviceToHost, r->s));
+    CK(c, hipEventRecord(c->d2h_ev[j % r->cells], r->s));
+    ++r->queued;
+    return PGH_OK;
+}
+
+int d2h_issue_ready(pgh_ctx* c, pgh_ctx::D2HRing* r) {
+    while (r->queued < r->n_pieces && r->queued < r->done + r->cells) {
+        bool ok = false;
+        RC(d2h_piece_ready(c, *r, r->queued, false, &ok));
+        if (!ok) break;
+        RC(d2h_issue(c, r));
+    }
+    return PGH_OK;
+}
+
+// HBM bytes at `src` (after the work already on stream `s`) -> host pieces, through the pinned
+// ring, in pieces of at most D2H_PIECE; the host copies piece k out as soon as it has landed while
+// the later pieces' DMAs run.  `overlap`, if given, is host work run while the first DMA is in
+// flight (the checkpoint template's framing copy).
+//   Not piped: every piece that fits the ring (2 x 128 MiB by default) is queued at once on `s`.
+//   marks (src is the resident checkpoint and its last fold left range marks): the pieces go on the
+// copy stream, each issued once the host sees the ranges that wrote it finished (hipEventQuery /
+// hipEventSynchronize), the first before the framing copy.  Issued that way the D2H runs on the
+// SDMA engines beside the fold: queued with device-side waits on the marks, the runtime ran them as
+// blit kernels (__amd_rocclr_copyBuffer) -- on the copy stream only after a stall, on any other
+// stream always -- and each blit held the fold range beside it to a quarter of its speed (48 ->
+// 182 us, profiles/r05d/, r05k/-r05m/).  The FINAL pass of a report-time close starts this itself
+// (pre_d2h), issuing the pieces whose ranges are done while it issues the rest.
+int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>& pieces, hipStream_t s,
+                     const std::function<void()>& overlap, bool marks) {
+    size_t total = 0;
+    for (auto& p : pieces) total += p.n;
+    if (total == 0) return PGH_OK;
+    const bool piped = marks && !c->final_marks.empty();
+    pgh_ctx::D2HRing r;
+    if (piped && c->pre_d2h_valid && c->pre_d2h.src == src && c->pre_d2h.total == total) {
+        r = c->pre_d2h;  // started by the FINAL pass (its slots marked busy until now)
+    } else {
+        RC(d2h_ring_begin(c, &r, src, total, s, piped));
+    }
+    c->pre_d2h_valid = false;
+    auto copy_out = [&](size_t j) {
+        const size_t off = j * r.piece, len = std::min(r.piece, total - off);
+        scatter_out(d2h_cell(c, r, j), off, len, pieces, *c->pool_copy);
+    };
+    if (!piped) {
+        while (r.queued < r.n_pieces && r.queued < r.cells) RC(d2h_issue(c, &r));
+        if (overlap) overlap();
+        for (; r.done < r.n_pieces; ++r.done) {
+            CK(c, hipEventSynchronize(c->d2h_ev[r.done % r.cells]));
+            copy_out(r.done);
+            if (r.queued < r.n_pieces) RC(d2h_issue(c, &r));  // into the cell just copied out
+        }
+    } else {
+        RC(d2h_issue_ready(c, &r));
+        if (r.queued == r.done) {  // the first piece before the framing copy
+            bool ok = false;
+            RC(d2h_piece_ready(c, r, r.queued, true, &ok));
+            RC(d2h_issue(c, &r));
+        }
+        if (overlap) overlap();
+        while (r.done < r.n_pieces) {
+            RC(d2h_issue_ready(c, &r));  // whatever finished, before a copy-out takes the thread
+            if (r.done < r.queued) {
+                const hipError_t q = hipEventQuery(c->d2h_ev[r.done % r.cells]);
+                if (q == hipSuccess) {
+                    copy_out(r.done++);
+                    continue;
+                }
+                if (q != hipErrorNotReady) CK(c, q);
+                std::this_thread::yield();
+            } else {  // nothing in flight: wait for the next piece's ranges
+                bool ok = false;
+                RC(d2h_piece_ready(c, r, r.queued, true, &ok));
+                RC(d2h_issue(c, &r));
+            }
+        }
+    }
+    for (int k = 0; k < r.n_free; ++k) c->pin_used[r.free_slot[k]] = false;  // every piece landed
     return PGH_OK;
 }
 

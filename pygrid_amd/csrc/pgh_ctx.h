@@ -233,6 +233,25 @@ struct pgh_ctx {
     bool pin_used[2] = {false, false};
     int pin_next = 0;
     std::vector<hipEvent_t> d2h_ev;  // one per ring cell of a staged D2H (stage_d2h_pieces)
+    // A staged D2H through the pinned ring: pieces of `piece` bytes of [src, src + total) into the
+    // cells of the free pinned slots, each followed by d2h_ev[cell].  piped: src is a fold's result
+    // with range marks; each piece is issued (on the copy stream) once the host sees every mark
+    // covering it complete -- no cross-stream wait on the device, which sent the pieces to blit
+    // kernels that slowed the ranges beside them (profiles/r05k/-r05m/, r05aa/).
+    struct D2HRing {
+        const uint8_t* src = nullptr;
+        size_t total = 0, piece = 0, per_slot = 0, cells = 0, n_pieces = 0, queued = 0, done = 0;
+        int free_slot[2] = {0, 1};
+        int n_free = 0;
+        hipStream_t s = nullptr;
+        bool piped = false;
+    };
+    // The new checkpoint's D2H as the FINAL pass of a report-time close starts it: the pieces whose
+    // ranges finished while the later ranges were still being issued (pgh_slots.cpp); the patch /
+    // download that follows adopts the ring.  Dropped with the marks (clear_final_marks) or when a
+    // staging copy takes a pinned slot (take_pin_slot).
+    D2HRing pre_d2h;
+    bool pre_d2h_valid = false;
     int copy_threads = 8;
     std::vector<int> local_cpus;  // PGH_NUMA (default on): the GPU's socket, for the copy pool + pinned ring
     std::unique_ptr<CopyPool> pool_copy;
@@ -280,7 +299,6 @@ struct pgh_ctx {
     std::vector<hipEvent_t> rng_ev;
     uint64_t copy_seq = 0, rng_seq = ~0ull;
     int rng_n = 0;
-    bool marks_after_ranges = false;  // final_marks came from a slot fold that waited on rng_ev
     bool warmup_skipped = false;  // pgh_create's warm-up failed (e.g. no device memory left): skipped
     int64_t vec_min = 0;      // [P_shard] device vectors at least this long (group collectives)
     // Pipelined close: a resident fold's FINAL pass runs as final_split param ranges, each followed by
@@ -431,6 +449,11 @@ void prefault_small_any(uint8_t* p, size_t n);
 void prefault_parallel(uint8_t* p, size_t n, CopyPool& pool);
 int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>& pieces, hipStream_t s,
                      const std::function<void()>& overlap = nullptr, bool marks = false);
+// may_wait = false: both pinned slots still busy -> r->n_free == 0 (nothing set up) instead of waiting
+int d2h_ring_begin(pgh_ctx* c, pgh_ctx::D2HRing* r, const uint8_t* src, size_t total, hipStream_t s, bool piped,
+                   bool may_wait = true);
+int d2h_issue_ready(pgh_ctx* c, pgh_ctx::D2HRing* r);  // piped: every piece whose marks have fired, no wait
+int take_pin_slot(pgh_ctx* c, int* slot);  // the next pinned staging slot, free of earlier DMAs
 int state_shard_spans(pgh_ctx* c, const uint8_t* pb, size_t n, std::vector<std::pair<size_t, size_t>>* out,
                       const char* what);
 // page-locked blocks marked async (pgh_host_async): DMAs from them are recorded, not waited for

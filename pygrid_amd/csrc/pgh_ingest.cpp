@@ -186,9 +186,8 @@ int stage_share_msg(pgh_ctx* c, ShareMsg& m, uint8_t* dev) {
     const size_t nk = m.chunks.size();
     size_t k = 0;
     while (k < nk) {
-        const int ps = c->pin_next;
-        c->pin_next ^= 1;
-        if (c->pin_used[ps]) CK(c, hipEventSynchronize(c->pin_ev[ps]));
+        int ps = 0;
+        RC(take_pin_slot(c, &ps));
         const size_t s0 = (size_t)m.chunks[k].off;
         const size_t cap = c->pin_slot;  // whole-slot fills (r01z: smaller fills were slower)
         size_t k1 = k;

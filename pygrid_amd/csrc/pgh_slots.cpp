@@ -49,6 +49,7 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
     }
     if (mode == PGH_ITERATIVE_MEAN && n > 0) RC(ensure_recips(c, total, s));
     int done = 0;
+    bool prequeued = false;
     do {
         const int m = std::min(n - done, pgh::ROWTAB_MAX);
         pgh::RowTab tab;
@@ -78,6 +79,15 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
         const int64_t RF = (int64_t)(D2H_PIECE / 8);
         const int K = (a.flags & pgh::FL_FINAL) && c->pg >= (1 << 20) ? (int)((c->pg + RF - 1) / RF) : 1;
         if (a.flags & pgh::FL_FINAL) clear_final_marks(c);
+        // the new checkpoint's D2H starts here: after each mark, the pieces whose ranges have
+        // finished go out while the later ranges are still being issued (stage_d2h_pieces adopts the
+        // ring).  The result is d_out until the swap below.
+        pgh_ctx::D2HRing& pre = c->pre_d2h;
+        bool prequeue = false;
+        if (K > 1 && (a.flags & pgh::FL_FINAL)) {
+            RC(d2h_ring_begin(c, &pre, (const uint8_t*)c->d_out, 4 * (size_t)c->pg, s, true, false));
+            prequeue = pre.n_free > 0;
+        }
         for (int r = 0; r < K; ++r) {
             const hipStream_t rs = s;
             const int64_t lo = std::min(c->pg, RF * r), hi = K == 1 ? c->pg : std::min(c->pg, RF * (r + 1));
@@ -96,9 +106,18 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
             const uint64_t rp = (uint64_t)(hi - lo);
             const uint64_t bytes = 4ull * (uint64_t)m * rp + (first ? 0 : 4 * rp) + ((a.flags & pgh::FL_FINAL) ? 8 * rp : 4 * rp);
             RC(timed_launch(c, rs, bytes, [&] { return pgh::launch_fedavg_rows(ar, tab, rs); }));
-            if (K > 1 && (hi % (2 * RF) == 0 || hi == c->pg)) RC(add_final_mark(c, rs, hi));
+            if (K > 1 && (hi % (2 * RF) == 0 || hi == c->pg)) {
+                RC(add_final_mark(c, rs, hi));
+                if (prequeue) RC(d2h_issue_ready(c, &pre));
+            }
         }
-        if (ranged && K > 1) c->marks_after_ranges = true;
+        if (prequeue) {  // its slots are busy until its pieces land (a staging copy syncs on this)
+            for (int k = 0; k < pre.n_free; ++k) {
+                CK(c, hipEventRecord(c->pin_ev[pre.free_slot[k]], pre.s));
+                c->pin_used[pre.free_slot[k]] = true;
+            }
+            prequeued = true;
+        }
         done += m;
     } while (done < n);
     RC(record_fold(c, s));
@@ -109,6 +128,7 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
     c->slot_mode = mode;
     if (final) {
         std::swap(c->d_ckpt, c->d_out);  // the new checkpoint is the next cycle's input
+        c->pre_d2h_valid = prequeued && c->pre_d2h.src == (const uint8_t*)c->d_ckpt;
         c->folded = 0;  // the next cycle folds from scratch
         c->slot_mode = -1;
     }
