@@ -108,16 +108,16 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
             RC(timed_launch(c, rs, bytes, [&] { return pgh::launch_fedavg_rows(ar, tab, rs); }));
             if (K > 1 && (hi % (2 * RF) == 0 || hi == c->pg)) {
                 RC(add_final_mark(c, rs, hi));
+                const size_t before = prequeue ? pre.queued : 0;
                 if (prequeue) RC(d2h_issue_ready(c, &pre));
+                if (prequeue && pre.queued > before)  // its slots are busy until these pieces land
+                    for (int k = 0; k < pre.n_free; ++k) {
+                        CK(c, hipEventRecord(c->pin_ev[pre.free_slot[k]], pre.s));
+                        c->pin_used[pre.free_slot[k]] = true;
+                    }
             }
         }
-        if (prequeue) {  // its slots are busy until its pieces land (a staging copy syncs on this)
-            for (int k = 0; k < pre.n_free; ++k) {
-                CK(c, hipEventRecord(c->pin_ev[pre.free_slot[k]], pre.s));
-                c->pin_used[pre.free_slot[k]] = true;
-            }
-            prequeued = true;
-        }
+        prequeued = prequeued || prequeue;
         done += m;
     } while (done < n);
     RC(record_fold(c, s));
