@@ -581,41 +581,45 @@ int stage_d2h_pieces(pgh_ctx* c, const uint8_t* src, const std::vector<OutPiece>
         const size_t off = j * r.piece, len = std::min(r.piece, total - off);
         scatter_out(d2h_cell(c, r, j), off, len, pieces, *c->pool_copy);
     };
-    if (!piped) {
-        while (r.queued < r.n_pieces && r.queued < r.cells) RC(d2h_issue(c, &r));
-        if (overlap) overlap();
-        for (; r.done < r.n_pieces; ++r.done) {
-            CK(c, hipEventSynchronize(c->d2h_ev[r.done % r.cells]));
-            copy_out(r.done);
-            if (r.queued < r.n_pieces) RC(d2h_issue(c, &r));  // into the cell just copied out
-        }
-    } else {
-        RC(d2h_issue_ready(c, &r));
-        if (r.queued == r.done) {  // the first piece before the framing copy
-            bool ok = false;
-            RC(d2h_piece_ready(c, r, r.queued, true, &ok));
-            RC(d2h_issue(c, &r));
-        }
-        if (overlap) overlap();
-        while (r.done < r.n_pieces) {
-            RC(d2h_issue_ready(c, &r));  // whatever finished, before a copy-out takes the thread
-            if (r.done < r.queued) {
-                const hipError_t q = hipEventQuery(c->d2h_ev[r.done % r.cells]);
-                if (q == hipSuccess) {
-                    copy_out(r.done++);
-                    continue;
-                }
-                if (q != hipErrorNotReady) CK(c, q);
-                std::this_thread::yield();
-            } else {  // nothing in flight: wait for the next piece's ranges
+    const int rc = [&]() -> int {  // (on failure: drain the stream below)
+        if (!piped) {
+            while (r.queued < r.n_pieces && r.queued < r.cells) RC(d2h_issue(c, &r));
+            if (overlap) overlap();
+            for (; r.done < r.n_pieces; ++r.done) {
+                CK(c, hipEventSynchronize(c->d2h_ev[r.done % r.cells]));
+                copy_out(r.done);
+                if (r.queued < r.n_pieces) RC(d2h_issue(c, &r));  // into the cell just copied out
+            }
+        } else {
+            RC(d2h_issue_ready(c, &r));
+            if (r.queued == r.done) {  // the first piece before the framing copy
                 bool ok = false;
                 RC(d2h_piece_ready(c, r, r.queued, true, &ok));
                 RC(d2h_issue(c, &r));
             }
+            if (overlap) overlap();
+            while (r.done < r.n_pieces) {
+                RC(d2h_issue_ready(c, &r));  // whatever finished, before a copy-out takes the thread
+                if (r.done < r.queued) {
+                    const hipError_t q = hipEventQuery(c->d2h_ev[r.done % r.cells]);
+                    if (q == hipSuccess) {
+                        copy_out(r.done++);
+                        continue;
+                    }
+                    if (q != hipErrorNotReady) CK(c, q);
+                    std::this_thread::yield();
+                } else {  // nothing in flight: wait for the next piece's ranges
+                    bool ok = false;
+                    RC(d2h_piece_ready(c, r, r.queued, true, &ok));
+                    RC(d2h_issue(c, &r));
+                }
+            }
         }
-    }
+        return PGH_OK;
+    }();
+    if (rc != PGH_OK) (void)hipStreamSynchronize(r.s);  // no piece may still land in a slot handed out later
     for (int k = 0; k < r.n_free; ++k) c->pin_used[r.free_slot[k]] = false;  // every piece landed
-    return PGH_OK;
+    return rc;
 }
 
 // The shard's slice of every tensor payload of a State message, as byte ranges of the message.
