@@ -145,3 +145,71 @@ def test_ranged_report_close_on_a_group():
         new = inc.close(ck)
     for g, w_ in zip(parse_state(new), O.fedavg_mean(ckpt, diffs)):
         assert np.array_equal(bits(g), bits(w_))
+
+
+def _slot_close_setup(engine, rng, n=5, ranges=True):
+    """Engine-level report-time close: n State diffs in slots 0..n-1 (ranged or not), the resident
+    checkpoint uploaded; returns (ckpt flat, diffs flat [n, P])."""
+    from pygrid_amd.state_schema import build_state_fast
+
+    numel = [int(np.prod(s)) for s in SHAPES]
+    ck = [rng.standard_normal(s).astype(F) for s in SHAPES]
+    diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES] for _ in range(n)]
+    engine.set_layout(numel)
+    engine.reserve(n)
+    engine.set_ingest_ranges(ranges)
+    engine.ckpt_upload_state(build_state_fast(ck))
+    for k in range(n):
+        engine.ingest_state(k, build_state_fast(diffs[k]))
+    flat = lambda ts: np.concatenate([t.reshape(-1) for t in ts])  # noqa: E731
+    return flat(ck), np.stack([flat(d) for d in diffs])
+
+
+def _patched(engine):
+    from pygrid_amd.state_schema import build_state_fast, parse_state
+
+    out = engine.ckpt_patch_state(build_state_fast([np.zeros(s, F) for s in SHAPES]))
+    return np.concatenate([t.reshape(-1) for t in parse_state(out)])
+
+
+@pytest.mark.parametrize("ranges", [False, True])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_final_pass_starts_the_d2h_and_the_patch_adopts_it(engine, ranges, mode):
+    """The FINAL pass of a slot fold issues the D2H pieces whose ranges are done (pre_d2h); the
+    patch right after adopts the ring.  Its bytes, and a download after it (a fresh D2H), are the
+    fold's, in every mode, ranged ingest on and off."""
+    from oracle import coracle
+
+    rng = np.random.default_rng(970 + mode + 10 * ranges)
+    c, d = _slot_close_setup(engine, rng, ranges=ranges)
+    w = rng.uniform(0.5, 2.0, 5).astype(F)
+    order = [3, 0, 4, 1, 2]
+    if mode == 2:
+        engine.set_weights(w[order])
+    engine.fold_slots_finish_resident(mode, order)
+    want = coracle.fedavg(mode, d[order], c, w[order] if mode == 2 else None)
+    assert np.array_equal(bits(_patched(engine)), bits(want))
+    assert np.array_equal(bits(engine.ckpt_download()), bits(want))
+
+
+def test_started_d2h_dropped_by_an_upload_or_a_staged_ingest(engine):
+    """A D2H the FINAL pass started and nobody adopted must not leak into a later read: after a
+    checkpoint upload the download and the patch return the uploaded floats; after one or two
+    staged ingests (which take the pinned slots) the patch still returns the fold's result."""
+    from oracle import coracle
+    from pygrid_amd.state_schema import build_state_fast
+
+    rng = np.random.default_rng(980)
+    c, d = _slot_close_setup(engine, rng)
+    engine.fold_slots_finish_resident(0, [0, 1, 2, 3, 4])
+    other = rng.standard_normal(c.size).astype(F)
+    engine.ckpt_upload(other)
+    assert np.array_equal(bits(engine.ckpt_download()), bits(other))
+    assert np.array_equal(bits(_patched(engine)), bits(other))
+    for staged in range(2):
+        c, d = _slot_close_setup(engine, rng)
+        engine.fold_slots_finish_resident(0, [4, 3, 2, 1, 0])
+        want = coracle.fedavg(0, d[[4, 3, 2, 1, 0]], c, None)
+        for k in range(staged + 1):
+            engine.ingest_state(k, build_state_fast([(rng.standard_normal(s) * 1e-2).astype(F) for s in SHAPES]))
+        assert np.array_equal(bits(_patched(engine)), bits(want)), staged
