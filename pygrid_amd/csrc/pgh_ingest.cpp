@@ -277,6 +277,10 @@ int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>
             if (e1 > e0) {
                 const size_t lo = (size_t)tab[e0].src, hi = (size_t)tab[e1 - 1].src + 4 * (size_t)tab[e1 - 1].n;
                 CK(c, hipMemcpyAsync(c->d_vbytes + lo, pb + a + lo, hi - lo, hipMemcpyHostToDevice, c->copy));
+                if (e1 == tab.size()) {  // the message's last DMA: the host block is read once this is done
+                    if (async) RC(host_dma_queued(c, pb + a, b - a, c->copy));
+                    else CK(c, hipEventRecord(c->gdma_ev, c->copy));
+                }
                 const hipError_t e = pgh::launch_gather_f32(c->d_vbytes, c->d_gtab + e0, (int)(e1 - e0),
                                                             (float*)d.base, d.map, c->copy);
                 if (e != hipSuccess) return fail(c, PGH_E_HIP, "gather launch failed: %s", hipGetErrorString(e));
@@ -284,8 +288,6 @@ int pinned_gather_ingest(pgh_ctx* c, const uint8_t* pb, const std::vector<Piece>
             CK(c, hipEventRecord(c->rng_ev[(size_t)k], c->copy));
             e0 = e1;
         }
-        if (async) RC(host_dma_queued(c, pb + a, b - a, c->copy));  // behind every chunk's DMA
-        else CK(c, hipEventRecord(c->gdma_ev, c->copy));
         c->rng_seq = c->copy_seq;
         c->rng_n = K;
     } else {
@@ -503,7 +505,6 @@ int pgh_set_weights(pgh_ctx* c, const float* w, int n) {
     }
     c->weights.assign(w, w + n);
     c->weights_on_device = false;
-   
     return PGH_OK;
 }
 

@@ -53,7 +53,9 @@ closes on Flask-Executor's thread, ``tasks/cycle.py:9-25``): a handler never wai
   other row fails and the cycle closes through the close-time path instead.  Two closes
   requested inline from two reports at once (a node that calls ``complete_cycle`` from inside
   ``submit_worker_diff``) cannot both upgrade their report's shared hold: the second fails at once
-  (``GateUpgradeConflict``) instead of waiting for the first, which waits for it;
+  (``GateUpgradeConflict``) instead of waiting for the first, which waits for it -- and so does an
+  inline close that finds the engine lock taken while another close waits for the gate (it
+  would otherwise block on the lock while holding the very hold that close waits for);
 * after the seal, reports and assignments of the closing cycle return at once (no cycle lock);
 * the **engine lock** serialises engine users: closes take it (blocking, on the executor); a
   handler that would prepare a cycle's report-time state while a close holds it skips that
@@ -405,7 +407,7 @@ class NodeEngine:
     def average_plan_diffs(self, cm, server_config, cycle, close_time: Callable, original: Callable):
         """The close (executor thread).  Holds the engine lock throughout, the report gate only for
         the snapshot of the completed rows (see the module docstring)."""
-        with self._engine_lock:
+        with self._engine_for_close():
             model = ckpt = None
             if isinstance(self._cycles.get(cycle.id), IncrementalCycle):
                 model = self.model_manager.get(fl_process_id=cycle.fl_process_id)
@@ -472,6 +474,28 @@ class NodeEngine:
             self.stats["diffs_from_db"] += st.last_close.get("from_db", 0)
             self.aggregator._resident = None
             finish_cycle(cm, server_config, cycle, self.model_manager, model.id, new)
+
+    @contextlib.contextmanager
+    def _engine_for_close(self):
+        """The engine lock for a close.  A close on the executor waits for it.  A close run inline
+        inside a report holds that report's shared gate hold: blocking on the engine lock there
+        deadlocks against a close that holds the lock and waits for the exclusive gate -- i.e. for
+        this very hold.  So an inline close polls the lock and gives up (``GateUpgradeConflict``)
+        as soon as another close is waiting for the gate; its handler then ends and lets that close
+        run."""
+        if not self._gate.held_here():
+            with self._engine_lock:
+                yield
+            return
+        while not self._engine_lock.acquire(timeout=0.002):
+            if self._gate.exclusive_wanted():
+                self.stats["gate_conflicts"] += 1
+                raise GateUpgradeConflict("another close holds the engine and waits for this report's hold on "
+                                          "the report gate")
+        try:
+            yield
+        finally:
+            self._engine_lock.release()
 
     def _abandon_others(self):
         for cid, st in list(self._cycles.items()):
@@ -542,6 +566,15 @@ class _Gate:
                     self._cv.notify_all()
                 elif self._waiting:
                     self._cv.notify_all()
+
+    def held_here(self) -> bool:
+        """Whether this thread holds the gate shared (a report handler, or a close run inside one)."""
+        return getattr(self._mine, "n", 0) > 0
+
+    def exclusive_wanted(self) -> bool:
+        """Whether a close waits for (or holds) the exclusive side."""
+        with self._cv:
+            return bool(self._waiting or self._exclusive)
 
     def acquire_exclusive(self):
         mine = getattr(self._mine, "n", 0)

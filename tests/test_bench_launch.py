@@ -11,10 +11,21 @@ import sys
 from conftest import ROOT
 
 
-def _run(args, env_extra=None, timeout=240):
+# the cpu_baseline children (a CPU torch loop of ~15 s each) stand in as stubs except where a test
+# is about them (test_cpu_baseline_on_the_n8_line)
+NO_CPU = "cpu_baseline=0"
+
+
+def _env(env_extra=None) -> dict:
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     env.update(env_extra or {})
+    env["PGH_BENCH_STUB"] = ",".join(x for x in (env.get("PGH_BENCH_STUB"), NO_CPU) if x)
+    return env
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = _env(env_extra)
     return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], cwd=str(ROOT), env=env,
                           capture_output=True, text=True, timeout=timeout)
 
@@ -93,7 +104,7 @@ def test_launcher_world_mismatch_fails_loudly():
 
 
 def test_torchrun_launch_forms_two_ranks():
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env = _env()
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29517", str(ROOT / "bench.py"),
                         "--gpus", "2", "--dry-run"], cwd=str(ROOT), env=env, capture_output=True, text=True,
@@ -127,7 +138,9 @@ def test_roofline_quotes_live_traffic_over_the_committed_file(monkeypatch):
     import importlib
 
     monkeypatch.setattr(sys, "argv", ["bench.py"])
-    bench = importlib.import_module("bench")
+    importlib.import_module("bench")
+    bench = importlib.import_module("benchlib.roofline")
+    monkeypatch.delenv("PGH_BENCH_LIVE_TRAFFIC", raising=False)
     st = {"kernel_launches": 2, "kernel_ms_total": 13.0, "kernel_bytes_total": 2 * 1000, "kernel_busy_ms_total": 13.0}
     monkeypatch.setattr(bench, "LIVE_TRAFFIC", (1001.0, 1000, "live: test"))
     r = bench.roofline_of(st, "resnet18-fedavg", 0, "k_fedavg")
@@ -180,8 +193,7 @@ def test_headline_printed_inside_the_budget_when_a_child_overruns():
     inside --budget-s."""
     import time
 
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    env["PGH_BENCH_STUB"] = "config1=0,config4=1000,config5=0,config3=0,group=0"
+    env = _env({"PGH_BENCH_STUB": "config1=0,config4=1000,config5=0,config3=0,group=0"})
     budget = 75
     t0 = time.time()
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
@@ -221,3 +233,26 @@ def test_spawned_ranks_line_survives_a_hung_headline():
     rec = _json_line(r.stdout)
     assert rec["value"] is None and "did not finish within" in rec["error"]
     assert rec["config4"] == {"dry_run": True, "stub": "config4"}
+
+
+def test_cpu_baseline_on_the_n8_line():
+    """the driver's N = 8 launch (torch.distributed.run, 8 ranks) carries a
+    measured cpu_baseline -- timed by rank 0 before the world forms, at the node's 1 thread and on
+    every usable core, with the core count and CPU model, its sample size and whether the close
+    figures are extrapolated from it.  (A 20 K-param shard and 1 s of CPU work keep the test short;
+    the driver's run times the 11.7 M-param shard for --cpu-seconds, default 12.)"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.pop("PGH_BENCH_STUB", None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", "29533", str(ROOT / "bench.py"),
+                        "--gpus", "8", "--dry-run", "--no-config-lines", "--no-group-line", "--params", "20000",
+                        "--cpu-seconds", "1"], cwd=str(ROOT), env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 8 and rec["dist_backend"] == "gloo"
+    cb = rec["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] == "port" and cb["cpu_model"], cb
+    assert cb["all_cores"]["cores"] >= 1 and cb["all_cores"]["value"] > 0, cb
+    assert cb["sample_clients"] == 32 and cb["workload_clients"] == 1000 and cb["extrapolated"] is True
+    assert "8-GPU world" in cb["measured"] and "cycle_manager.py:276-296" in cb["sample"]
+    assert rec["budget"]["stages_s"]["cpu_baseline"] > 0

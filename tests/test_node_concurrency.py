@@ -359,6 +359,68 @@ def test_two_inline_closers_do_not_deadlock_the_gate():
     assert not g._upgrading and not g._exclusive
 
 
+class BarrierWarehouse(SlowUpdateWarehouse):
+    """``update`` (the report's DB write, under its shared gate hold) of the named threads waits
+    until all of them are there, so every report holds the gate shared before any close starts."""
+
+    def __init__(self, wh, parties):
+        super().__init__(wh)
+        self.barrier = threading.Barrier(parties)
+        self.threads = set()
+
+    def update(self):
+        if threading.current_thread().name in self.threads:
+            self.threads.discard(threading.current_thread().name)
+            self.barrier.wait(10)
+        return self.wh.update()
+
+
+def test_two_inline_closes_on_the_node_do_not_deadlock():
+    """two reports of two FL processes each complete their cycle and run
+    complete_cycle inline, both while holding the report gate shared.  The first close takes the
+    engine lock and waits for the exclusive gate -- for the other report's hold; the other close
+    must not block on the engine lock behind it.  It gives up (GateUpgradeConflict, logged by
+    complete_cycle as the reference logs a failed close), its handler ends, the first close
+    finishes; a re-report then closes the second cycle, and the saved checkpoints equal the
+    reference node's."""
+    cfg1 = {"min_diffs": 1, "max_diffs": 1, "num_cycles": 0}
+    mod = make_node()
+    node = pnode.install(mod, engine=NumpyEngine(), framing="template", fold_batch=1)
+    mod.run_task_once = lambda name, func, *args: func(*args)  # complete_cycle inline, in the handler
+    cm = mod.cycle_manager
+    bw = BarrierWarehouse(cm._worker_cycles, 2)
+    cm._worker_cycles = bw
+    pa, _, _ = host_process(mod, cfg1, ckpt_bytes())
+    pb, _, _ = host_process(mod, cfg1, ckpt_bytes(1))
+    ka, kb = assign(mod, "a", pa), assign(mod, "b", pb)
+    ts = [threading.Thread(target=cm.submit_worker_diff, args=("a", ka, diff_bytes("a")), name="report-a"),
+          threading.Thread(target=cm.submit_worker_diff, args=("b", kb, diff_bytes("b")), name="report-b")]
+    bw.threads = {t.name for t in ts}
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(15)
+    assert not any(t.is_alive() for t in ts), "deadlock: an inline close waited on the engine lock"
+    assert len(cm.task_errors) == 1 and isinstance(cm.task_errors[0], pnode.GateUpgradeConflict), cm.task_errors
+    assert node.stats["gate_conflicts"] == 1
+    assert len(checkpoints(mod)) == 3  # 2 initial + exactly one closed cycle
+    # the gate and the engine lock are free again: the cycle left open closes on the next report
+    done = {r[2] for r in checkpoints(mod)}
+    for w, k, p in (("a", ka, pa), ("b", kb, pb)):
+        cm.submit_worker_diff(w, k, diff_bytes(w))
+    assert len(checkpoints(mod)) == 4 and len(cm.task_errors) == 1
+    assert done <= {r[2] for r in checkpoints(mod)}
+    node.uninstall()
+
+    ref = make_node()
+    ra, _, _ = host_process(ref, cfg1, ckpt_bytes())
+    rb, _, _ = host_process(ref, cfg1, ckpt_bytes(1))
+    rka, rkb = assign(ref, "a", ra), assign(ref, "b", rb)
+    ref.cycle_manager.submit_worker_diff("a", rka, diff_bytes("a"))
+    ref.cycle_manager.submit_worker_diff("b", rkb, diff_bytes("b"))
+    assert sorted(r[2] for r in checkpoints(mod)) == sorted(r[2] for r in checkpoints(ref))
+
+
 def test_assignment_while_the_cycle_state_is_built_is_recorded(monkeypatch):
     """a cycle the node just created is prepared under the engine lock without a rows
     query; an assign handler that runs meanwhile finds the lock taken.  Its assignment is recorded
