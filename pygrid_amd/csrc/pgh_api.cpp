@@ -466,12 +466,54 @@ int take_pin_slot(pgh_ctx* c, int* slot) {
     return PGH_OK;
 }
 
+// The stream and page-locked cells of piped rings (own_d2h): at least `bytes` of cells.  Made on
+// first use; grown only after every piece already on the stream has landed.
+static int ensure_d2h_cells(pgh_ctx* c, size_t bytes) {
+    if (!c->d2h) {
+        CK(c, hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking));
+        // prime the stream with a small H2D: the runtime then runs its D2H copies on an SDMA engine
+        // (an unprimed stream's D2H went to blit kernels that share the CUs with the fold, r05k/-r05x/)
+        void* d = nullptr;
+        CK(c, hipMalloc(&d, 64));
+        const hipError_t e1 = hipMemcpyAsync(d, c->h_pin[0], 64, hipMemcpyHostToDevice, c->d2h);
+        const hipError_t e2 = e1 == hipSuccess ? hipStreamSynchronize(c->d2h) : e1;
+        (void)hipFree(d);
+        CK(c, e2);
+    }
+    if (c->d2h_cap >= bytes) return PGH_OK;
+    CK(c, hipStreamSynchronize(c->d2h));
+    if (c->h_d2h) (void)hipHostFree(c->h_d2h);
+    c->h_d2h = nullptr;
+    c->d2h_cap = 0;
+    if (hipHostMalloc((void**)&c->h_d2h, bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(c, PGH_E_OOM, "page-locked D2H cells of %zu bytes failed", bytes);
+    }
+    c->d2h_cap = bytes;
+    return PGH_OK;
+}
+
 int d2h_ring_begin(pgh_ctx* c, pgh_ctx::D2HRing* r, const uint8_t* src, size_t total, hipStream_t s, bool piped,
                    bool may_wait) {
     *r = pgh_ctx::D2HRing{};
     r->src = src;
     r->total = total;
     r->piped = piped;
+    if (piped && c->own_d2h) {  // up to D2H_OWN_CELLS pieces in flight, none of the staging slots held
+        r->piece = D2H_PIECE;
+        r->n_pieces = (total + r->piece - 1) / r->piece;
+        RC(ensure_d2h_cells(c, std::min(r->n_pieces, D2H_OWN_CELLS) * r->piece));
+        r->base = c->h_d2h;
+        r->cells = c->d2h_cap / r->piece;
+        r->per_slot = r->cells;
+        r->s = c->d2h;
+        while (c->d2h_ev.size() < std::min(r->cells, r->n_pieces)) {
+            hipEvent_t e = nullptr;
+            CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->d2h_ev.push_back(e);
+        }
+        return PGH_OK;
+    }
     r->s = piped ? c->copy : s;
     r->piece = std::min(c->pin_slot, D2H_PIECE);
     r->per_slot = c->pin_slot / r->piece;  // >= 1 (pin_slot >= 4096)
@@ -505,6 +547,7 @@ int d2h_ring_begin(pgh_ctx* c, pgh_ctx::D2HRing* r, const uint8_t* src, size_t t
 }
 
 static uint8_t* d2h_cell(const pgh_ctx* c, const pgh_ctx::D2HRing& r, size_t j) {
+    if (r.base) return r.base + (j % r.cells) * r.piece;
     return c->h_pin[r.free_slot[(j % r.cells) / r.per_slot]] + (j % r.per_slot) * r.piece;
 }
 
@@ -1144,6 +1187,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_PINNED_GATHER")) c->pinned_gather = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_BLOCK_BYTES")) c->block_bytes = (size_t)std::max(0LL, std::atoll(e));
     if (const char* e = std::getenv("PGH_FINAL_RANGES")) c->final_split = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("PGH_D2H_STREAM")) c->own_d2h = std::atoi(e) != 0;
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming) == hipSuccess &&
@@ -1240,6 +1284,9 @@ void pgh_destroy(pgh_ctx* c) {
         if (c->h_pin[k]) (void)hipHostFree(c->h_pin[k]);
         if (c->pin_ev[k]) (void)hipEventDestroy(c->pin_ev[k]);
     }
+    if (c->d2h) (void)hipStreamSynchronize(c->d2h);
+    if (c->h_d2h) (void)hipHostFree(c->h_d2h);
+    if (c->d2h) (void)hipStreamDestroy(c->d2h);
     for (hipEvent_t e : {c->copy_done, c->xsync, c->aux_ev})
         if (e) (void)hipEventDestroy(e);
     for (auto e : c->fold_ev_pool) (void)hipEventDestroy(e);

@@ -245,6 +245,7 @@ struct pgh_ctx {
         int n_free = 0;
         hipStream_t s = nullptr;
         bool piped = false;
+        uint8_t* base = nullptr;  // the cells of a piped ring: h_d2h (own_d2h), else the free pinned slots
     };
     // The new checkpoint's D2H as the FINAL pass of a report-time close starts it: the pieces whose
     // ranges finished while the later ranges were still being issued (pgh_slots.cpp); the patch /
@@ -252,6 +253,15 @@ struct pgh_ctx {
     // staging copy takes a pinned slot (take_pin_slot).
     D2HRing pre_d2h;
     bool pre_d2h_valid = false;
+    // A piped ring's pieces on a stream and in page-locked cells of their own (PGH_D2H_STREAM,
+    // default 1): on the copy stream they queued behind the last reports' H2D, and they waited for
+    // a staging slot those reports still held -- with reports back to back, until every report had
+    // landed.  PCIe is full duplex: the new checkpoint's pieces run beside that H2D.  The stream is
+    // primed with a small H2D when made, so the runtime sends its D2H to an SDMA engine (r05ae).
+    bool own_d2h = true;
+    hipStream_t d2h = nullptr;
+    uint8_t* h_d2h = nullptr;
+    size_t d2h_cap = 0;
     int copy_threads = 8;
     std::vector<int> local_cpus;  // PGH_NUMA (default on): the GPU's socket, for the copy pool + pinned ring
     std::unique_ptr<CopyPool> pool_copy;
@@ -430,6 +440,7 @@ struct OutPiece {
 // copy-out of the earlier ones (r01ac: 4, 8, 16 MiB within the noise of the 47 MB report-time close;
 // with the parallel pre-fault, r01ak, 8 MiB pieces closed in 2.3-2.4 ms vs 2.6-2.7 for one piece).
 constexpr size_t D2H_PIECE = 8u << 20;
+constexpr size_t D2H_OWN_CELLS = 8;  // a piped ring's own cells: 64 MiB at most (ResNet-18: 6 pieces)
 // Ranged report ingest (pgh_set_ingest_ranges): one chunk = the params of one D2H piece = two
 // 4 MiB FINAL ranges of a report-time close (pgh_slots.cpp).
 constexpr int64_t INGEST_CHUNK = (int64_t)(D2H_PIECE / 4);

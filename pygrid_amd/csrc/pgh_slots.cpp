@@ -39,8 +39,8 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
     // a close right behind a ranged ingest (pgh_set_ingest_ranges) orders each FINAL range after the
     // chunk of the last report it reads instead of after the whole copy stream
     const bool ranged = final && n > 0 && n <= pgh::ROWTAB_MAX && c->pg >= (1 << 20) && ranged_ingest_valid(c);
-    if (ranged && c->dec_last) CK(c, hipStreamWaitEvent(s, c->dec_last, 0));
-    else RC(order_after_ingest(c, s));
+    if (!ranged) RC(order_after_ingest(c, s));
+    else if (c->dec_last) CK(c, hipStreamWaitEvent(s, c->dec_last, 0));  // the copy stream: per range below
     if (mode == PGH_WEIGHTED_MEAN && n > 0) {
         if ((int64_t)c->weights.size() < total)
             return fail(c, PGH_E_STATE, "weighted mean: %zu weights for %lld clients", c->weights.size(),

@@ -47,16 +47,20 @@ def test_close_time_knobs(monkeypatch, env):
             _check(CycleAggregator(eng).average_plan_diffs({}, ck_pb, d_pbs), O.fedavg_mean(ckpt, diffs))
 
 
+@pytest.mark.parametrize("own", ["1", "0"], ids=["d2h-stream", "PGH_D2H_STREAM=0"])
 @pytest.mark.parametrize("pinned", [0, 2 << 20, 2 * 81_920], ids=["ring-default", "ring-2MiB", "ring-160KiB"])
-def test_d2h_pieces_wrap_a_small_pinned_ring(pinned):
+def test_d2h_pieces_wrap_a_small_pinned_ring(monkeypatch, pinned, own):
     """stage_d2h_pieces queues every D2H piece that fits the pinned ring at once and refills a cell
     as soon as its piece is copied out: a 4.4 MB checkpoint through a ring of 2 x 1 MiB (5 pieces
-    over 2 cells) or 2 x 80 KiB (55 pieces), after a report-time close (its pieces wait on the
-    FINAL ranges' marks) and after a close-time fold, bit-exact."""
+    over 2 cells) or 2 x 80 KiB (55 pieces), after a close-time fold and -- with PGH_D2H_STREAM=0,
+    where the report-time close's pieces also use the staging slots -- after a report-time close
+    (its pieces wait on the FINAL ranges' marks), bit-exact.  By default the report-time close's
+    pieces run on the D2H stream's own cells whatever the staging ring's size."""
     from pygrid_amd import Engine
     from pygrid_amd.cycle import CycleAggregator
     from pygrid_amd.incremental import IncrementalCycle
 
+    monkeypatch.setenv("PGH_D2H_STREAM", own)
     ckpt, diffs, ck_pb, d_pbs = _case(915, n=4)
     want = O.fedavg_mean(ckpt, diffs)
     with Engine(0, pinned_bytes=pinned) as eng:
@@ -69,13 +73,16 @@ def test_d2h_pieces_wrap_a_small_pinned_ring(pinned):
         _check(CycleAggregator(eng).average_plan_diffs({}, ck_pb, d_pbs), want)
 
 
-def test_report_time_close_in_output_ranges():
+@pytest.mark.parametrize("own", ["1", "0"], ids=["d2h-stream", "PGH_D2H_STREAM=0"])
+def test_report_time_close_in_output_ranges(monkeypatch, own):
     """The report-time close's FINAL pass runs as ranges of 4 MiB of output on one stream, the D2H
     pieces behind them (no knob since r04): a 1.1 M-param shard (two ranges, the second short)
-    closes bit-exact."""
+    closes bit-exact -- its pieces on the D2H stream (default) or on the copy stream through the
+    staging slots (PGH_D2H_STREAM=0)."""
     from pygrid_amd import Engine
     from pygrid_amd.incremental import IncrementalCycle
 
+    monkeypatch.setenv("PGH_D2H_STREAM", own)
     ckpt, diffs, ck_pb, d_pbs = _case(911, n=6)
     with Engine(0) as eng:
         inc = IncrementalCycle(eng, [int(np.prod(s)) for s in SHAPES], slots=8, checkpoint=ck_pb)
@@ -84,6 +91,32 @@ def test_report_time_close_in_output_ranges():
         for w in (5, 1, 3, 0, 2, 4):  # worker 6 never reports
             inc.reported(w, d_pbs[w])
         _check(inc.close(ck_pb), O.fedavg_mean(ckpt, diffs))
+
+
+def test_report_time_close_wraps_the_d2h_cells():
+    """A shard of 20 M params (80 MB: 10 D2H pieces) has more pieces than the D2H stream's 8 cells:
+    pieces 9-10 go out into cells the host has copied out, behind the FINAL ranges that wrote
+    them; three chained report-time closes (the cells reused across closes), bit-exact."""
+    from pygrid_amd import Engine
+    from pygrid_amd.incremental import IncrementalCycle
+    from pygrid_amd.state_schema import build_state_fast
+
+    shapes = [(4000, 5000), (7,)]
+    rng = np.random.default_rng(931)
+    ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
+    ck_pb = build_state_fast(ckpt)
+    numel = [int(np.prod(s)) for s in shapes]
+    with Engine(0) as eng:
+        for cyc in range(3):
+            diffs = [[(rng.standard_normal(s) * 1e-2).astype(F) for s in shapes] for _ in range(3)]
+            inc = IncrementalCycle(eng, numel, slots=4, checkpoint=ck_pb)
+            for w in range(4):
+                inc.assigned(w)
+            for w in (2, 1, 3):  # worker 0 never reports: all three rows fold at close
+                inc.reported(w, build_state_fast(diffs[w - 1]))
+            ck_pb = inc.close(ck_pb)
+            ckpt = O.fedavg_mean(ckpt, diffs)
+            _check(ck_pb, ckpt)
 
 
 def test_group_copy_threads_and_rccl_off(monkeypatch):
