@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PGH_ABI_VERSION 9
+#define PGH_ABI_VERSION 10
 
 typedef struct pgh_ctx pgh_ctx;
 
@@ -71,6 +71,10 @@ typedef struct {
     uint64_t h2d_staged_bytes_total; /* of h2d_bytes_total: bytes host threads first copied into
                                  * the pinned staging ring (pageable sources); page-locked sources
                                  * (pgh_host_alloc) are DMA'd as they lie and do not count */
+    uint64_t d2h_bytes_total;   /* ABI 10: bytes moved HBM -> host through the D2H ring (results) */
+    uint64_t d2h_kernel_bytes_total; /* ABI 10: of d2h_bytes_total, moved by K6 k_copy_to_host (a
+                                 * report-time close's pieces issued while the copy stream still
+                                 * ran H2D, PGH_D2H_STREAM=2) instead of an SDMA copy */
 } pgh_stats_t;
 
 /* ---- context lifecycle ------------------------------------------------------------------ */

@@ -35,6 +35,8 @@ class Stats(C.Structure):
         ("max_clients", C.c_int32),
         ("kernel_busy_ms_total", C.c_double),
         ("h2d_staged_bytes_total", C.c_uint64),
+        ("d2h_bytes_total", C.c_uint64),
+        ("d2h_kernel_bytes_total", C.c_uint64),
     ]
 
 
@@ -138,7 +140,7 @@ SIGNATURES = {
     "pgh_b64_decode_clean": (_i, [_vp, _sz, _vp, _sz, C.POINTER(_sz), _i]),
 }
 
-ABI_VERSION = 9  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
+ABI_VERSION = 10  # include/pgh_api.h PGH_ABI_VERSION (Stats layout above)
 _LIB = None
 
 

@@ -884,6 +884,8 @@ int stats(pgh_ctx* c, pgh_stats_t* out) {
         r.h2d_ms_total = std::max(r.h2d_ms_total, s.h2d_ms_total);
         r.h2d_bytes_total += s.h2d_bytes_total;
         r.h2d_staged_bytes_total += s.h2d_staged_bytes_total;
+        r.d2h_bytes_total += s.d2h_bytes_total;
+        r.d2h_kernel_bytes_total += s.d2h_kernel_bytes_total;
         r.close_ms_last = std::max(r.close_ms_last, s.close_ms_last);
         r.ld = std::max(r.ld, s.ld);
         r.n_folded = std::max(r.n_folded, s.n_folded);

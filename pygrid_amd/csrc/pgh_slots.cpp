@@ -86,7 +86,7 @@ int slot_fold(pgh_ctx* c, int mode, const int32_t* slots, int n, bool final) {
         bool prequeue = false;
         if (K > 1 && (a.flags & pgh::FL_FINAL)) {
             RC(d2h_ring_begin(c, &pre, (const uint8_t*)c->d_out, 4 * (size_t)c->pg, s, true, false));
-            prequeue = pre.n_free > 0;
+            prequeue = pre.base || pre.n_free > 0;  // own cells, or a free staging slot
         }
         for (int r = 0; r < K; ++r) {
             const hipStream_t rs = s;

@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(_lib.SIGNATURES), "ctypes signatures out of sync with the header"
-    assert lib.pgh_abi_version() == _lib.ABI_VERSION == 9
+    assert lib.pgh_abi_version() == _lib.ABI_VERSION == 10
     assert b"pgh_create_group" in (ROOT / "pygrid_amd" / "libpygrid_hip.so").read_bytes()
 
 

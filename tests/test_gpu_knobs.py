@@ -47,7 +47,11 @@ def test_close_time_knobs(monkeypatch, env):
             _check(CycleAggregator(eng).average_plan_diffs({}, ck_pb, d_pbs), O.fedavg_mean(ckpt, diffs))
 
 
-@pytest.mark.parametrize("own", ["1", "0"], ids=["d2h-stream", "PGH_D2H_STREAM=0"])
+D2H_MODES = ["2", "3", "1", "0"]
+D2H_IDS = ["d2h-default", "PGH_D2H_STREAM=3 (K6 always)", "PGH_D2H_STREAM=1 (SDMA only)", "PGH_D2H_STREAM=0"]
+
+
+@pytest.mark.parametrize("own", D2H_MODES, ids=D2H_IDS)
 @pytest.mark.parametrize("pinned", [0, 2 << 20, 2 * 81_920], ids=["ring-default", "ring-2MiB", "ring-160KiB"])
 def test_d2h_pieces_wrap_a_small_pinned_ring(monkeypatch, pinned, own):
     """stage_d2h_pieces queues every D2H piece that fits the pinned ring at once and refills a cell
@@ -73,12 +77,13 @@ def test_d2h_pieces_wrap_a_small_pinned_ring(monkeypatch, pinned, own):
         _check(CycleAggregator(eng).average_plan_diffs({}, ck_pb, d_pbs), want)
 
 
-@pytest.mark.parametrize("own", ["1", "0"], ids=["d2h-stream", "PGH_D2H_STREAM=0"])
+@pytest.mark.parametrize("own", D2H_MODES, ids=D2H_IDS)
 def test_report_time_close_in_output_ranges(monkeypatch, own):
     """The report-time close's FINAL pass runs as ranges of 4 MiB of output on one stream, the D2H
     pieces behind them (no knob since r04): a 1.1 M-param shard (two ranges, the second short)
-    closes bit-exact -- its pieces on the D2H stream (default) or on the copy stream through the
-    staging slots (PGH_D2H_STREAM=0)."""
+    closes bit-exact -- its pieces on the D2H stream (default: SDMA, or K6 k_copy_to_host while the
+    copy stream still runs H2D; 3: K6 for every piece; 1: SDMA only) or on the copy stream through
+    the staging slots (0).  The stats count the result's bytes, and at 3 every one of them by K6."""
     from pygrid_amd import Engine
     from pygrid_amd.incremental import IncrementalCycle
 
@@ -90,17 +95,29 @@ def test_report_time_close_in_output_ranges(monkeypatch, own):
             inc.assigned(w)
         for w in (5, 1, 3, 0, 2, 4):  # worker 6 never reports
             inc.reported(w, d_pbs[w])
+        eng.reset_stats()
         _check(inc.close(ck_pb), O.fedavg_mean(ckpt, diffs))
+        st = eng.stats()
+        P = sum(int(np.prod(s)) for s in SHAPES)
+        assert st["d2h_bytes_total"] == 4 * P
+        if own == "3":
+            assert st["d2h_kernel_bytes_total"] == 4 * P
+        if own in ("1", "0"):
+            assert st["d2h_kernel_bytes_total"] == 0
 
 
-def test_report_time_close_wraps_the_d2h_cells():
+@pytest.mark.parametrize("mode", ["2", "3"], ids=["d2h-default", "PGH_D2H_STREAM=3 (K6 always)"])
+def test_report_time_close_wraps_the_d2h_cells(monkeypatch, mode):
     """A shard of 20 M params (80 MB: 10 D2H pieces) has more pieces than the D2H stream's 8 cells:
     pieces 9-10 go out into cells the host has copied out, behind the FINAL ranges that wrote
-    them; three chained report-time closes (the cells reused across closes), bit-exact."""
+    them; three chained report-time closes (the cells reused across closes), each right behind its
+    last report (by default the pieces issued while that report's H2D still runs go through K6),
+    bit-exact -- also with K6 for every piece."""
     from pygrid_amd import Engine
     from pygrid_amd.incremental import IncrementalCycle
     from pygrid_amd.state_schema import build_state_fast
 
+    monkeypatch.setenv("PGH_D2H_STREAM", mode)
     shapes = [(4000, 5000), (7,)]
     rng = np.random.default_rng(931)
     ckpt = [rng.standard_normal(s).astype(F) for s in shapes]
