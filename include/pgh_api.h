@@ -157,7 +157,7 @@ int pgh_ingest_state(pgh_ctx* ctx, int client, const uint8_t* pb, size_t n);
  * order of pgh_set_layout (PySyft 0.2.9 int64 share tensors, test_basic_syft_operations.py:
  * 388-454; wire schema restated, parity unpinned like pgh_ingest_state).  The payload bytes go
  * to HBM as they are (PCIe carries the varints) and are decoded there (k_varint_decode); the
- * host only checks the framing, counts the values per 64 KiB chunk and rejects varints longer
+ * host only checks the framing, counts the values per 16 KiB chunk and rejects varints longer
  * than 10 bytes, cut-off payloads and count/layout mismatches (PGH_E_PARSE). */
 int pgh_ingest_state_shares(pgh_ctx* ctx, int client, int n_parties, const uint8_t* const* pbs, const size_t* ns);
 /* Fill slab rows [0, n_clients) with the deterministic synthetic diffs (or shares) of

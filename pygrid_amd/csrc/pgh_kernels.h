@@ -96,7 +96,7 @@ hipError_t launch_synth_shares(int64_t* out, const SlabMap& m, int64_t ncols, in
 // bytes sit in HBM as received, each tensor's payload starting 16-byte aligned; they are cut into
 // chunks of at most VARINT_CHUNK bytes.  `first` = index (in the flat layout) of the first value
 // whose LAST byte lies in the chunk: the host counts terminator bytes per chunk while staging.
-constexpr int VARINT_CHUNK = 65536;
+constexpr int VARINT_CHUNK = 16384;  // one wave of K4 per chunk
 struct VChunk {
     int64_t off;       // chunk start, bytes from the payload buffer base (16-aligned)
     int64_t span_off;  // start of the tensor payload holding the chunk (nothing before it is read)

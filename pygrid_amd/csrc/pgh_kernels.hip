@@ -535,39 +535,8 @@ __global__ __launch_bounds__(BLOCK) void k_synth_shares(int64_t* out, SlabMap m,
     }
 }
 
-// Packed varints -> int64 (TensorData.contents_int64 of secagg share States).  One workgroup per
-// 64 KiB chunk, walked in 4 KiB windows staged in LDS with the 16 bytes before them (a varint is
-// at most 10 bytes, so a value ending in the window starts at offset >= -9).  Per window:
-//   1. lane t owns bytes [16t, 16t + 16): its terminators (bit 7 clear) come from its 16-byte load
-//      in registers; a wave prefix sum (DPP) + the per-wave totals give each value's rank;
-//   2. every lane writes the window offsets of its value ends into LDS by rank (a compacted list);
-//   3. the workgroup decodes the list rank by rank, lane = rank mod 256: value r spans
-//      (end[r - 1], end[r]] (end[-1] = the last end of the previous window, or of the 16 bytes
-//      before the chunk), its <= 10 bytes are independent LDS reads, the 7-bit groups are packed
-//      and the next values' bytes masked off the result by length -- no data-dependent loop, no
-//      divergence past the last rank; value r goes to flat index first + rank, so consecutive
-//      lanes store consecutive int64s (one base address per window when the window's values lie
-//      in one slab block of the shard).
-// The next window's 16-byte load is issued before the current one is decoded.  Byte-level work on
-// a stream PCIe fills at ~55 GB/s; HBM traffic is ~2 bytes per byte in.
-constexpr int VWIN = 4096;
+// Packed varints -> int64 (TensorData.contents_int64 of secagg share States): K4 below.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint32_t pack7x4(uint32_t w) {  // the low 7 bits of 4 bytes -> 28 bits
-    w &= 0x7F7F7F7Fu;
-    w = (w & 0x007F007Fu) | ((w & 0x7F007F00u) >> 1);
-    return (w & 0x00003FFFu) | ((w & 0x3FFF0000u) >> 2);
-}
-
-__device__ __forceinline__ uint32_t term_mask16(const u32x4& v) {  // bit k: byte k has bit 7 clear
-    uint32_t tm = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const uint32_t nt = ~v[w] & 0x80808080u;
-        tm |= (((nt >> 7) & 1u) | ((nt >> 14) & 2u) | ((nt >> 21) & 4u) | ((nt >> 28) & 8u)) << (4 * w);
-    }
-    return tm;
-}
 
 // Inclusive prefix sum over a wave64 in DPP moves (row shifts inside each 16-lane row, then the
 // row totals broadcast into the rows after them): no LDS round trips, unlike __shfl_up's
@@ -582,97 +551,164 @@ __device__ __forceinline__ int wave_inclusive_sum(int x) {
     return x;
 }
 
-__global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, const VChunk* chunks, int64_t* row,
-                                                       SlabMap m, int64_t lo, int64_t hi) {
-    __shared__ u32x4 win4[1 + 256 + 1];  // [0]: the 16 bytes before the window; [257]: slack for reads past an end
-    __shared__ uint16_t ends[VWIN];      // window offsets of the value ends, by rank
-    __shared__ int wsum[4];
-    constexpr int NW = VARINT_CHUNK / VWIN;
-    const uint8_t* win = reinterpret_cast<const uint8_t*>(win4) + 16;  // win[-16 .. 4111]
-    const VChunk ch = chunks[blockIdx.x];
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int p = 16 * t;
+// The value whose bytes are win[s .. e] (s >= e - 9, win[-16 .. 1039] readable), from the 12 bytes
+// at s (three funnel shifts of the four aligned dwords around it).  The 7-bit groups are summed
+// whole bytes at a time in byte dot products: raw = sum_i b_i 128^i over bytes b_0 .. b_9, i.e.
+// sum_i (v_i + 128 c_i) 128^i with v_i the 7-bit group and c_i the continuation bit.  c_i = 1 for
+// every byte before the last (e), so raw = value + K(len) + (multiples of 2^(7 len) from the bytes
+// past e), with K(len) = sum_{j=1}^{len-1} 2^(7j); subtracting K(10) differs from K(len) only by
+// multiples of 2^(7 len) too, so value = (raw - K(10)) mod 2^(7 len) (all 64 bits at len 10).
+__device__ __forceinline__ uint64_t varint_at(const uint8_t* win, int s, int e) {
+    const uint32_t* wd = reinterpret_cast<const uint32_t*>(win + (s & ~3));
+    const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
+    const uint32_t sh = (uint32_t)(s & 3);
+    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);  // bytes 0-3 of the value
+    const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);  // 4-7
+    const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);  // 8-11
+    constexpr uint32_t LO = 0x00008001u, HI = 0x80010000u;       // byte weights (1, 128, 0, 0), (0, 0, 1, 128)
+    // b0 + 128 b1 + 2^14 (b2 + 128 b3) < 2^30: no wrap
+    const uint32_t a = __builtin_amdgcn_udot4(w0, LO, 0u, false) + (__builtin_amdgcn_udot4(w0, HI, 0u, false) << 14);
+    const uint32_t b = __builtin_amdgcn_udot4(w1, LO, 0u, false) + (__builtin_amdgcn_udot4(w1, HI, 0u, false) << 14);
+    const uint32_t c = __builtin_amdgcn_udot4(w2, LO, 0u, false);  // b8 + 128 b9 (only b9's bit 0 stays, at 63)
+    const uint64_t raw = (uint64_t)a + ((uint64_t)b << 28) + ((uint64_t)c << 56);
+    constexpr uint64_t K10 = 0x8102040810204080ull;  // sum_{j=1}^{9} 2^(7j)
+    const int cut = max(57 - __mul24(e - s, 7), 0);   // 64 - 7 len: the bits above the value (24-bit mul)
+    return ((raw - K10) << cut) >> cut;
+}
+
+// Terminator bits of 16 bytes (bit k: byte k has bit 7 clear) in byte dot products: the 0x80 bytes
+// of ~v & 0x80808080 weighted 1, 2, 4, 8 (16 .. 128 for the second dword) sum to 128 x the mask.
+__device__ __forceinline__ uint32_t term_mask16(const u32x4& v) {
+    const uint32_t t0 = ~v[0] & 0x80808080u, t1 = ~v[1] & 0x80808080u;
+    const uint32_t t2 = ~v[2] & 0x80808080u, t3 = ~v[3] & 0x80808080u;
+    const uint32_t m01 = __builtin_amdgcn_udot4(t0, 0x08040201u, __builtin_amdgcn_udot4(t1, 0x80402010u, 0u, false), false);
+    const uint32_t m23 = __builtin_amdgcn_udot4(t2, 0x08040201u, __builtin_amdgcn_udot4(t3, 0x80402010u, 0u, false), false);
+    return (m01 >> 7) | (m23 << 1);
+}
+
+// K4: one WAVE per chunk of <= VARINT_CHUNK bytes (16 KiB), four independent waves per workgroup
+// and no workgroup barrier.  Per 1 KiB window: lane t owns bytes [16t, 16t + 16) and decodes the
+// values that END there itself -- a value is at most 10 bytes, so it starts in lane t's bytes or
+// lane t - 1's, both staged in the wave's LDS window; its rank is a DPP wave prefix sum of the
+// terminator counts, its start the last terminator of lane t - 1 (DPP wave shift) or, for lane 0,
+// the carry from the previous window.  The chunk table's `first` (the host counts terminators per
+// chunk while staging) gives each wave its starting rank, so the waves never wait for each other.
+// Rounds 2-5 ran a block form (a workgroup per 64 KiB chunk compacting the value ends of 4 KiB
+// windows into an LDS list by rank, three barriers per window): 55-58 us per 111 MB message of
+// shares against this form's 40.5-41 us (tools/exp_varint.cpp, profiles/r06m/).
+// Byte-level work on a stream PCIe fills at ~55 GB/s; HBM traffic is ~1.84 bytes per byte in.
+constexpr int VWIN = 1024;
+constexpr int VSTAGE = 256;  // values of a window staged per wave (int64 shares: <= 115 values of 9-10 bytes)
+__global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, const VChunk* chunks, int n_chunks,
+                                                         int64_t* row, SlabMap m, int64_t lo, int64_t hi) {
+    __shared__ u32x4 lds[4][1 + 64 + 1];      // per wave: [0] the 16 bytes before the window, [65] slack
+    __shared__ uint64_t stage[4][2][VSTAGE];   // per wave: two windows' values by rank
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int k = (int)blockIdx.x * 4 + wave;
+    if (k >= n_chunks) return;  // wave-uniform; nothing below synchronises across waves
+    u32x4* const win4 = lds[wave];
+    const uint8_t* const win = reinterpret_cast<const uint8_t*>(win4) + 16;  // win[-16 .. 1039]
+    const VChunk ch = chunks[k];
+    const int p = 16 * lane;
     const u32x4 zero = {0, 0, 0, 0};
-    // Loads are unconditional (a branch around a load makes hipcc wait for it at once, which would
-    // serialise the prefetch): an offset past the chunk is clamped to its last 16 bytes and what it
-    // reads is masked out by the chunk length.  The value end before the window, in window offsets,
-    // comes from the 16 bytes before the chunk (zero bytes at a payload's start read as
-    // terminators: the first value starts at offset 0).
+    // Loads are unconditional (a branch around a load makes hipcc wait for it at once): offsets past
+    // the chunk clamp to its last 16 bytes, masked out by the chunk length; zero bytes before a
+    // payload's start read as terminators (the first value starts at offset 0).
     const bool has_before = ch.off > ch.span_off;
     const u32x4 b16 = *reinterpret_cast<const u32x4*>(bytes + (has_before ? ch.off - 16 : ch.off));
     const int last16 = (ch.n - 1) & ~15;
-    // the next window's 16 bytes are loaded one window ahead (loading the whole chunk up front
-    // costs occupancy: 79 vs 63 us per 111 MB message, profiles/r02x/)
-    u32x4 nxt = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + ch.off + min(p, last16)));
+    auto load = [&](int w0) {
+        return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + ch.off + min(w0 + p, last16)));
+    };
     const u32x4 before = has_before ? b16 : zero;
     const uint32_t tb = term_mask16(before);
-    int carry = tb ? (31 - __clz(tb)) - 16 : -16;
-    if (t == 0) win4[257] = zero;
-    u32x4 last = before;  // lane 255: the previous window's last 16 bytes
+    int carry = tb ? (31 - __clz(tb)) - 16 : -16;  // window offset of the last value end before the window
+    if (lane == 0) win4[65] = zero;
+    u32x4 last = before;  // lane 63: the previous window's last 16 bytes
     int64_t base = ch.first;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-        const int w0 = VWIN * i;
-        if (w0 >= ch.n) break;  // uniform over the workgroup
-        const u32x4 v = nxt;
-        nxt = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + ch.off + min(w0 + VWIN + p, last16)));
-        win4[1 + t] = v;
-        if (t == 255) win4[0] = last;
+    // A window's values leave through LDS (by rank, then out in rows of 64 consecutive values) and
+    // their stores are issued one window LATER, right after the wait for the next window's bytes:
+    // the compiler's wait for a window's load also covers the stores issued before it (it cannot
+    // count a loop of them), so stores issued just before it would hold the wait up; issued a
+    // window earlier, they are done by then.
+    int pend_n = 0;
+    int64_t* pend_dst = row;
+    const uint64_t* pend_stg = stage[wave][0];
+    auto flush = [&]() {
+        for (int q = lane; q < pend_n; q += 64) pend_dst[q] = (int64_t)pend_stg[q];
+        pend_n = 0;
+    };
+    auto window = [&](const u32x4& v, int w0, uint64_t* stg) {
+        win4[1 + lane] = v;  // (the wait for this window's bytes)
+        if (lane == 63) win4[0] = last;
+        flush();             // the previous window's stores
         uint32_t tm = term_mask16(v);
         const int lim = ch.n - w0 - p;  // bytes of mine inside the chunk
         if (lim < 16) tm &= lim > 0 ? (1u << lim) - 1u : 0u;
         const int cnt = __popc(tm);
         const int x = wave_inclusive_sum(cnt);
-        if (lane == 63) wsum[wave] = x;
-        __syncthreads();
-        int rank = x - cnt, total = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const int sw = wsum[w];
-            rank += w < wave ? sw : 0;
-            total += sw;
-        }
-        while (tm) {
-            ends[rank++] = (uint16_t)(p + __ffs(tm) - 1);
-            tm &= tm - 1;
-        }
-        __syncthreads();
+        const int total = __builtin_amdgcn_readlane(x, 63);
+        // my last value end; lane t - 1's is where my first value starts (every full 16 bytes of
+        // valid input hold a value end); lane 0 takes the carry
+        const int mylast = tm ? p + 31 - __clz(tm) : -64;
+        const int prev = __builtin_amdgcn_update_dpp(carry, mylast, 0x138, 0xf, 0xf, false);  // wave_shr:1
+        const uint64_t with = __ballot(tm != 0);
         // the window's values inside the shard and in one slab block (the usual case): consecutive
-        // addresses from one base, a wave-uniform test instead of a slab-map lookup per value
+        // addresses from one base
         const int64_t l0 = base - lo, l1 = base + total - 1 - lo;
         const bool flat = base >= lo && base + total <= hi && ((m.off + l0) >> m.bshift) == ((m.off + l1) >> m.bshift);
         int64_t* const dst0 = row + (flat ? m.at(l0) : 0);
-        for (int r = t; r < total; r += 256) {
-            const int e = ends[r];
-            // validated input: s >= e - 9 (the clamp only keeps malformed bytes inside the window)
-            const int s = max(r ? (int)ends[r - 1] + 1 : carry + 1, e - 9);
-            const int len = e - s + 1;
-            // bytes [s, s + 12) from the four aligned dwords around them (win[-16 .. 4111] are in
-            // bounds: s >= -15 and s <= 4095), the 7-bit groups of each dword packed in 32-bit
-            // arithmetic; the bytes past the value's end (the next values') land at bits >= 7 * len
-            // and are masked off the result
-            const uint32_t* wd = reinterpret_cast<const uint32_t*>(win + (s & ~3));
-            const uint32_t d0 = wd[0], d1 = wd[1], d2 = wd[2], d3 = wd[3];
-            const uint32_t sh = (uint32_t)(s & 3);
-            const uint32_t p0 = pack7x4(__builtin_amdgcn_alignbyte(d1, d0, sh));
-            const uint32_t p1 = pack7x4(__builtin_amdgcn_alignbyte(d2, d1, sh));
-            const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-            const uint32_t lo32 = p0 | (p1 << 28);
-            const uint32_t hi32 = (p1 >> 4) | ((w2 & 0x7Fu) << 24) | ((w2 << 23) & 0x80000000u);
-            uint64_t val = ((uint64_t)hi32 << 32) | lo32;
-            val &= len >= 10 ? ~0ull : (1ull << (7 * len)) - 1ull;
-            if (flat) {
-                dst0[r] = (int64_t)val;
-            } else {
-                const int64_t idx = base + r;
+        // LDS writes above, reads below: one wave, in order; keep the compiler from moving them
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int r = x - cnt, pe = prev;  // r: my first value's rank in the window
+        uint32_t left = tm;
+        auto next = [&]() -> uint64_t {  // my next value, in order (validated input: s >= e - 9)
+            const int e = p + __ffs(left) - 1;
+            const uint64_t val = varint_at(win, max(pe + 1, e - 9), e);
+            pe = e;
+            left &= left - 1;
+            return val;
+        };
+        // wave-uniform branches: one loop per case rather than a branch per value (decoding a
+        // lane's two values as two independent chains measured no faster, r06m)
+        if (flat && total <= VSTAGE) {
+            while (left) stg[r++] = next();
+            pend_n = total;
+            pend_dst = dst0;
+            pend_stg = stg;
+        } else if (flat) {  // a dense window (> VSTAGE values, short varints)
+            while (left) dst0[r++] = (int64_t)next();
+        } else {            // a shard or slab-block edge inside the window
+            while (left) {
+                const int64_t idx = base + r++;
+                const uint64_t val = next();
                 if (idx >= lo && idx < hi) row[m.at(idx - lo)] = (int64_t)val;
             }
         }
-        carry = (total ? (int)ends[total - 1] : carry) - VWIN;
+        if (with) carry = __builtin_amdgcn_readlane(mylast, 63 - __clzll(with));
+        carry -= VWIN;
         base += total;
         last = v;
-        __syncthreads();  // win4 / ends / wsum are rewritten by the next window
+        // the next window's LDS writes come after this window's reads (in order within the wave)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // the next window's bytes are loaded before this one is decoded (loading two ahead measured the
+    // same: 40.9-41.2 vs 40.6-41.1 us per 111 MB, r06m); two registers used in turn over a fully
+    // unrolled chunk (no copy of a register a load is still writing)
+    u32x4 buf[2];
+    buf[0] = load(0);
+#pragma unroll
+    for (int i = 0; i < VARINT_CHUNK / VWIN; ++i) {  // the host cuts chunks of <= VARINT_CHUNK bytes
+        if (i * VWIN >= ch.n) break;
+        buf[(i + 1) & 1] = load((i + 1) * VWIN);
+        window(buf[i & 1], i * VWIN, stage[wave][i & 1]);
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    flush();
 }
 
 int cu_count() {
@@ -965,7 +1001,7 @@ hipError_t launch_varint_decode(const uint8_t* bytes, const VChunk* chunks, int 
         m.off != 0 || !valid_map(m, 0) || lo > hi)
         return hipErrorInvalidValue;
     if (n_chunks == 0) return hipSuccess;
-    k_varint_decode<<<(unsigned)n_chunks, 256, 0, s>>>(bytes, chunks, row, m, lo, hi);
+    k_varint_decode<<<(unsigned)((n_chunks + 3) / 4), 256, 0, s>>>(bytes, chunks, n_chunks, row, m, lo, hi);
     return hipGetLastError();
 }
 

@@ -82,19 +82,51 @@ def test_share_state_rows_decode_exactly(engine):
 
 
 def test_share_state_varints_across_chunk_edges(engine):
-    """A 10-byte varint straddling every 64 KiB chunk edge and 4 KiB window edge of the payload."""
+    """A 10-byte varint straddling every 16 KiB chunk edge and 1 KiB window edge of the payload."""
     P = 40_000  # 10-byte varints: 400,000 payload bytes, 7 chunks
     vals = np.full(P, -5, dtype=np.int64)  # negative: 10 bytes each
     vals[::7] = 3                           # 1-byte varints shift the alignment
     pb = build_state_i64_fast([vals])
     payload = varint_encode(vals)
     ends = np.flatnonzero(np.frombuffer(payload, np.uint8) < 0x80)
-    assert any(e % 65536 < 9 for e in ends)  # some varint ends just past a chunk edge
+    assert any(e % 16_384 < 9 for e in ends)  # some varint ends just past a chunk edge
     engine.set_layout([P])
     engine.reserve(1, 1, 1)
     engine.ingest_state_shares(0, [pb])
     s, _ = engine.secagg(10, 3)
     assert np.array_equal(s, vals)
+
+
+def test_share_state_wave_edges(engine):
+    """K4 (a wave per 16 KiB chunk, 1 KiB windows, lane t decoding the values that end in its 16
+    bytes) on a payload built around its edges: 10-byte varints straddling chunk and window edges,
+    16-byte lane regions holding 16 one-byte values beside regions holding one 10-byte value's
+    tail, windows denser than its LDS stage (> 256 values), the int64 extremes, and a shard range
+    cutting a window."""
+    P = 120_000
+    vals = np.full(P, -5, dtype=np.int64)                 # 10 bytes each
+    vals[::7] = 3                                          # 1-byte values shift the alignment
+    vals[50_000:53_000] = np.arange(3_000) % 128           # a run of 1-byte values (16 ends per lane)
+    vals[60_000:60_050] = [0, -1, 2**63 - 1, -2**63, 127, 128, 2**56, 2**56 - 1, 2**63 - 2**56, -128] * 5
+    payload = varint_encode(vals)
+    ends = np.flatnonzero(np.frombuffer(payload, np.uint8) < 0x80)
+    assert any(e % 16_384 < 9 for e in ends) and any(e % 1_024 < 9 for e in ends)
+    numel = [70_001, P - 70_001]
+    pb = build_state_i64_fast(split(vals, numel))
+    engine.set_layout(numel)
+    engine.reserve(1, 1, 1)
+    engine.ingest_state_shares(0, [pb])
+    s, _ = engine.secagg(10, 3)
+    assert np.array_equal(s, vals)
+    lo, hi = 50_688, 90_112  # a shard boundary inside a window
+    engine.set_shard(lo, hi)
+    try:
+        engine.reserve(1, 1, 1)
+        engine.ingest_state_shares(0, [pb])
+        s, _ = engine.secagg(10, 3)
+    finally:
+        engine.set_layout(numel)
+    assert np.array_equal(s, vals[lo:hi])
 
 
 def test_share_state_sharded_context(engine):
@@ -141,7 +173,7 @@ def test_share_state_rejects_malformed_and_leaves_slab(engine, case):
     good = np.arange(P, dtype=np.int64) * 3 - 7
     payload = bytearray(varint_encode(good))
     n_values = P
-    if case == "overlong_at_chunk_edge":   # 12 continuation bytes around byte 65,536
+    if case == "overlong_at_chunk_edge":   # 12 continuation bytes around byte 65,536 (a chunk edge)
         payload[65_530:65_542] = b"\xff" * 12
     elif case == "overlong_inside":
         payload[1_000:1_011] = b"\x81" * 11
@@ -197,8 +229,8 @@ def test_cycle_aggregator_secure_aggregate_states(engine):
 
 @pytest.mark.parametrize("seed", range(12))
 def test_share_state_random_value_mixes(engine, seed):
-    """k_varint_decode under random mixes: windows of only 1-byte varints (4,096 values per 4 KiB
-    window, the longest rank list), only 10-byte ones, runs of each, random tensor splits and party
+    """k_varint_decode under random mixes: windows of only 1-byte varints (1,024 values per 1 KiB
+    window: 16 per lane, past the LDS stage), only 10-byte ones, runs of each, random tensor splits and party
     counts -- the decoded sum bit-exact against the oracle over google.protobuf-parsed shares."""
     rng = np.random.default_rng(900 + seed)
     P = int(rng.choice([1, 17, 4_096, 4_097, 65_536, 70_001, 150_000]))
