@@ -134,9 +134,9 @@ def group_line(args, limit_s: int = 240) -> dict:
 CONFIG_LINES = {"config1": ("mnist-state", 1, None, True, 120), "config4": ("c4-stream", None, 5, False, 180),
                 "config5": ("c5-ingest", None, 5, False, 180), "config3": ("resnet18-secagg", None, 10, True, 240)}
 FOLD_BYTES_NOTE = {
-    "c5-ingest": "fold batch 2: each fold launch also reads and writes the running state (4 B + 4 B per param "
-                 "per 2 clients), so the fold kernel moves 2x its diff bytes; fold_frac counts those bytes, "
-                 "e2e_frac only the diff bytes (the step is PCIe-bound)",
+    "c5-ingest": "fold batch 4 (half the 8-slot ring): each fold launch also reads and writes the running state "
+                 "(4 B + 4 B per param per 4 clients), so the fold kernel moves 1.5x its diff bytes; fold_frac counts "
+                 "those bytes, e2e_frac only the diff bytes (the step is PCIe-bound)",
     "c4-stream": "value and e2e_frac include the on-device generation of every chunk (4 B written per param per "
                  "client, alternating with the fold); fold_frac is the fold kernel alone",
     "resnet18-secagg": "fold_frac: 8*S*N*P + 12*P bytes (shares in; int64 sum and float32 decode out) over the "

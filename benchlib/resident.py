@@ -143,7 +143,7 @@ def run_c4(ctx, args, eng, N, pg, P):
     kern_gbs = ctx.sum_over_ranks(4 * N * pg * args.steps / (st["kernel_ms_total"] / 1e3) / 1e9)
     cfg = {"workload": f"c4-stream: P_shard={pg} params/GPU x {N} clients fp32 (SURVEY 8(d) config 4 shard), "
                        f"{R}-slot HBM ring, {chunk}-client chunks generated on-device ({args.synth} generator)",
-           "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R, "generator": args.synth,
+           "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R, "fold_batch": chunk, "generator": args.synth,
            "parallelism": f"param-shard{ctx.world}" + (f" + {ctx.coll} all-gather" if ctx.world > 1 else ""),
            "kernel_variant": eng.effective_variant()}
     extra = {"fold_kernel_client_diff_GBps_aggregated": round(kern_gbs, 1),
@@ -166,6 +166,7 @@ def run_c5(ctx, args, eng, N, pg, P):
     from pygrid_amd.sharding import gather_flat
 
     R = args.ring or 8
+    batch = max(1, R // 2)  # fold half the ring at a time: the other half takes the next H2D copies
     n_host = 4  # distinct host buffers, re-sent as different clients
     bufs = [PinnedBuffer((pg,)) for _ in range(n_host)]  # shard-sized host diffs
     rng = np.random.default_rng(args.seed + ctx.rank)
@@ -181,7 +182,7 @@ def run_c5(ctx, args, eng, N, pg, P):
     full = [out]
 
     def step():
-        eng.stream_begin(1, 2)
+        eng.stream_begin(1, batch)
         for k in range(N):
             eng.ingest(k, bufs[k % n_host].array)
         eng.stream_finish_device(ckpt.data_ptr(), out.data_ptr(), sp)
@@ -204,8 +205,8 @@ def run_c5(ctx, args, eng, N, pg, P):
     kern_gbs = 4 * N * pg * args.steps / (st["kernel_ms_total"] / 1e3) / 1e9
     ingest_gbs = st["h2d_bytes_total"] / (st["h2d_ms_total"] / 1e3) / 1e9 if st["h2d_ms_total"] else None
     cfg = {"workload": f"c5-ingest: P_shard={pg} params/GPU x {N} clients fp32 iterative plan (SURVEY 8(d) "
-                       f"config 5 shard), pinned host -> HBM over PCIe, {R}-slot ring, fold batch 2",
-           "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R,
+                       f"config 5 shard), pinned host -> HBM over PCIe, {R}-slot ring, fold batch {batch}",
+           "clients": N, "params_per_gpu": pg, "params_total": P, "ring_slots": R, "fold_batch": batch,
            "parallelism": f"param-shard{ctx.world}" + (f" + {ctx.coll} all-gather" if ctx.world > 1 else ""),
            "kernel_variant": eng.effective_variant(1)}
     extra = {"bound_by": "PCIe host->device (Gen5 x16, 63 GB/s spec per GPU)",
