@@ -586,65 +586,77 @@ __device__ __forceinline__ uint32_t term_mask16(const u32x4& v) {
     return (m01 >> 7) | (m23 << 1);
 }
 
-// K4: one WAVE per chunk of <= VARINT_CHUNK bytes (16 KiB), four independent waves per workgroup
-// and no workgroup barrier.  Per 1 KiB window: lane t owns bytes [16t, 16t + 16) and decodes the
-// values that END there itself -- a value is at most 10 bytes, so it starts in lane t's bytes or
-// lane t - 1's, both staged in the wave's LDS window; its rank is a DPP wave prefix sum of the
-// terminator counts, its start the last terminator of lane t - 1 (DPP wave shift) or, for lane 0,
-// the carry from the previous window.  The chunk table's `first` (the host counts terminators per
-// chunk while staging) gives each wave its starting rank, so the waves never wait for each other.
+// K4: one workgroup per chunk of <= VARINT_CHUNK bytes (16 KiB), one wave per 4 KiB of it.  Each
+// wave loads its 4 KiB (four 1 KiB windows, 16 bytes per lane each) at once, counts the value ends
+// (terminator bytes) in them, and the four counts -- one barrier -- give each wave its starting
+// rank from the chunk's `first` (the host counts terminators per chunk while staging).  Then per
+// window lane t decodes the values that END in its 16 bytes itself: a value is at most 10 bytes,
+// so it starts in lane t's bytes or lane t - 1's, both staged in the wave's LDS window; its rank
+// is a DPP wave prefix sum of the terminator counts, its start the last terminator of lane t - 1
+// (DPP wave shift) or, for lane 0, the carry from the previous window (or the 16 bytes before the
+// wave's 4 KiB).  The values leave through LDS by rank, in rows of 64 consecutive int64s.
 // Rounds 2-5 ran a block form (a workgroup per 64 KiB chunk compacting the value ends of 4 KiB
-// windows into an LDS list by rank, three barriers per window): 55-58 us per 111 MB message of
-// shares against this form's 40.5-41 us (tools/exp_varint.cpp, profiles/r06m/).
+// windows into an LDS list by rank, three barriers per window): 55.6-57.9 us per 111 MB message of
+// shares against this form's 37.4-38.1 us (tools/exp_varint.cpp, profiles/r06m/, r06q/).
 // Byte-level work on a stream PCIe fills at ~55 GB/s; HBM traffic is ~1.84 bytes per byte in.
-constexpr int VWIN = 1024;
+constexpr int VWIN = 1024;                  // a window: 64 lanes x 16 bytes
+constexpr int VSUB = 4096;                  // a wave's part of a chunk
+constexpr int VNW = VSUB / VWIN;            // windows per wave
+static_assert(VARINT_CHUNK == 4 * VSUB, "K4: four waves of VSUB bytes per chunk");
 constexpr int VSTAGE = 256;  // values of a window staged per wave (int64 shares: <= 115 values of 9-10 bytes)
-__global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, const VChunk* chunks, int n_chunks,
-                                                         int64_t* row, SlabMap m, int64_t lo, int64_t hi) {
-    __shared__ u32x4 lds[4][1 + 64 + 1];      // per wave: [0] the 16 bytes before the window, [65] slack
-    __shared__ uint64_t stage[4][2][VSTAGE];   // per wave: two windows' values by rank
+__global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, const VChunk* chunks, int64_t* row,
+                                                       SlabMap m, int64_t lo, int64_t hi) {
+    __shared__ u32x4 lds[4][1 + 64 + 1];    // per wave: [0] the 16 bytes before the window, [65] slack
+    __shared__ uint64_t stage[4][VSTAGE];    // per wave: the window's values by rank
+    __shared__ int wcount[4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int k = (int)blockIdx.x * 4 + wave;
-    if (k >= n_chunks) return;  // wave-uniform; nothing below synchronises across waves
     u32x4* const win4 = lds[wave];
+    uint64_t* const stg = stage[wave];
     const uint8_t* const win = reinterpret_cast<const uint8_t*>(win4) + 16;  // win[-16 .. 1039]
-    const VChunk ch = chunks[k];
+    const VChunk ch = chunks[blockIdx.x];
+    const int sub0 = wave * VSUB;                    // this wave's bytes: [sub0, sub0 + subn) of the chunk
+    const int subn = max(0, min(VSUB, ch.n - sub0));  // (0 for the waves past a short chunk's end)
     const int p = 16 * lane;
     const u32x4 zero = {0, 0, 0, 0};
     // Loads are unconditional (a branch around a load makes hipcc wait for it at once): offsets past
-    // the chunk clamp to its last 16 bytes, masked out by the chunk length; zero bytes before a
+    // the chunk clamp to its last 16 bytes, masked out by the byte counts; zero bytes before a
     // payload's start read as terminators (the first value starts at offset 0).
-    const bool has_before = ch.off > ch.span_off;
-    const u32x4 b16 = *reinterpret_cast<const u32x4*>(bytes + (has_before ? ch.off - 16 : ch.off));
     const int last16 = (ch.n - 1) & ~15;
-    auto load = [&](int w0) {
-        return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + ch.off + min(w0 + p, last16)));
-    };
+    const bool has_before = sub0 > 0 || ch.off > ch.span_off;
+    const u32x4 b16 = *reinterpret_cast<const u32x4*>(bytes + ch.off + (has_before ? min(sub0, last16 + 16) - 16 : 0));
+    u32x4 buf[VNW];
+#pragma unroll
+    for (int i = 0; i < VNW; ++i)
+        buf[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + ch.off + min(sub0 + i * VWIN + p, last16)));
+    // value ends per window (bit k: byte p + k ends a value), this wave's total, the waves before it
+    uint32_t tms[VNW];
+    int mine = 0;
+#pragma unroll
+    for (int i = 0; i < VNW; ++i) {
+        uint32_t tm = term_mask16(buf[i]);
+        const int lim = subn - i * VWIN - p;  // bytes of mine inside the wave's part
+        if (lim < 16) tm &= lim > 0 ? (1u << lim) - 1u : 0u;
+        tms[i] = tm;
+        mine += __popc(tm);
+    }
+    const int wtot = __builtin_amdgcn_readlane(wave_inclusive_sum(mine), 63);
+    if (lane == 0) wcount[wave] = wtot;
+    __syncthreads();
+    int64_t base = ch.first;
+    for (int w = 0; w < wave; ++w) base += wcount[w];
+    if (subn == 0) return;  // (after the barrier: every wave reaches it)
     const u32x4 before = has_before ? b16 : zero;
     const uint32_t tb = term_mask16(before);
     int carry = tb ? (31 - __clz(tb)) - 16 : -16;  // window offset of the last value end before the window
     if (lane == 0) win4[65] = zero;
     u32x4 last = before;  // lane 63: the previous window's last 16 bytes
-    int64_t base = ch.first;
-    // A window's values leave through LDS (by rank, then out in rows of 64 consecutive values) and
-    // their stores are issued one window LATER, right after the wait for the next window's bytes:
-    // the compiler's wait for a window's load also covers the stores issued before it (it cannot
-    // count a loop of them), so stores issued just before it would hold the wait up; issued a
-    // window earlier, they are done by then.
-    int pend_n = 0;
-    int64_t* pend_dst = row;
-    const uint64_t* pend_stg = stage[wave][0];
-    auto flush = [&]() {
-        for (int q = lane; q < pend_n; q += 64) pend_dst[q] = (int64_t)pend_stg[q];
-        pend_n = 0;
-    };
-    auto window = [&](const u32x4& v, int w0, uint64_t* stg) {
-        win4[1 + lane] = v;  // (the wait for this window's bytes)
+#pragma unroll
+    for (int i = 0; i < VNW; ++i) {
+        if (i * VWIN >= subn) break;
+        const u32x4 v = buf[i];
+        const uint32_t tm = tms[i];
+        win4[1 + lane] = v;
         if (lane == 63) win4[0] = last;
-        flush();             // the previous window's stores
-        uint32_t tm = term_mask16(v);
-        const int lim = ch.n - w0 - p;  // bytes of mine inside the chunk
-        if (lim < 16) tm &= lim > 0 ? (1u << lim) - 1u : 0u;
         const int cnt = __popc(tm);
         const int x = wave_inclusive_sum(cnt);
         const int total = __builtin_amdgcn_readlane(x, 63);
@@ -673,11 +685,12 @@ __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, con
         };
         // wave-uniform branches: one loop per case rather than a branch per value (decoding a
         // lane's two values as two independent chains measured no faster, r06m)
-        if (flat && total <= VSTAGE) {
+        if (flat && total <= VSTAGE) {  // by rank into LDS, then out in rows of 64 consecutive values
             while (left) stg[r++] = next();
-            pend_n = total;
-            pend_dst = dst0;
-            pend_stg = stg;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int q = lane; q < total; q += 64) dst0[q] = (int64_t)stg[q];
         } else if (flat) {  // a dense window (> VSTAGE values, short varints)
             while (left) dst0[r++] = (int64_t)next();
         } else {            // a shard or slab-block edge inside the window
@@ -695,20 +708,7 @@ __global__ __launch_bounds__(256) void k_varint_decode(const uint8_t* bytes, con
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    // the next window's bytes are loaded before this one is decoded (loading two ahead measured the
-    // same: 40.9-41.2 vs 40.6-41.1 us per 111 MB, r06m); two registers used in turn over a fully
-    // unrolled chunk (no copy of a register a load is still writing)
-    u32x4 buf[2];
-    buf[0] = load(0);
-#pragma unroll
-    for (int i = 0; i < VARINT_CHUNK / VWIN; ++i) {  // the host cuts chunks of <= VARINT_CHUNK bytes
-        if (i * VWIN >= ch.n) break;
-        buf[(i + 1) & 1] = load((i + 1) * VWIN);
-        window(buf[i & 1], i * VWIN, stage[wave][i & 1]);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    flush();
 }
 
 int cu_count() {
@@ -1001,7 +1001,7 @@ hipError_t launch_varint_decode(const uint8_t* bytes, const VChunk* chunks, int 
         m.off != 0 || !valid_map(m, 0) || lo > hi)
         return hipErrorInvalidValue;
     if (n_chunks == 0) return hipSuccess;
-    k_varint_decode<<<(unsigned)((n_chunks + 3) / 4), 256, 0, s>>>(bytes, chunks, n_chunks, row, m, lo, hi);
+    k_varint_decode<<<(unsigned)n_chunks, 256, 0, s>>>(bytes, chunks, row, m, lo, hi);
     return hipGetLastError();
 }
 
