@@ -72,9 +72,9 @@ typedef struct {
                                  * the pinned staging ring (pageable sources); page-locked sources
                                  * (pgh_host_alloc) are DMA'd as they lie and do not count */
     uint64_t d2h_bytes_total;   /* ABI 10: bytes moved HBM -> host through the D2H ring (results) */
-    uint64_t d2h_kernel_bytes_total; /* ABI 10: of d2h_bytes_total, moved by K6 k_copy_to_host (a
-                                 * report-time close's pieces issued while the copy stream still
-                                 * ran H2D, PGH_D2H_STREAM=2) instead of an SDMA copy */
+    uint64_t d2h_kernel_bytes_total; /* ABI 10: of d2h_bytes_total, moved by a kernel instead of an
+                                 * SDMA copy -- 0 since K6 k_copy_to_host was removed (r06s: it
+                                 * read FINAL ranges before they had run); kept for the layout */
 } pgh_stats_t;
 
 /* ---- context lifecycle ------------------------------------------------------------------ */

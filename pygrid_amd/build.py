@@ -16,9 +16,9 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libpygrid_hip.so"
-SOURCES = [CSRC / "pgh_kernels.hip", CSRC / "pgh_copy.hip", CSRC / "pgh_api.cpp", CSRC / "pgh_ingest.cpp", CSRC / "pgh_reduce.cpp",
+SOURCES = [CSRC / "pgh_kernels.hip", CSRC / "pgh_api.cpp", CSRC / "pgh_ingest.cpp", CSRC / "pgh_reduce.cpp",
            CSRC / "pgh_slots.cpp", CSRC / "pgh_group.cpp", CSRC / "pgh_state.cpp", CSRC / "pgh_b64.cpp"]
-HEADERS = [CSRC / "pgh_kernels.h", CSRC / "pgh_copy.h", CSRC / "pgh_state.h", CSRC / "pgh_internal.h", CSRC / "pgh_ctx.h",
+HEADERS = [CSRC / "pgh_kernels.h", CSRC / "pgh_state.h", CSRC / "pgh_internal.h", CSRC / "pgh_ctx.h",
            ROOT / "include" / "pgh_api.h"]
 ARCH = os.environ.get("PGH_OFFLOAD_ARCH", "gfx950")
 

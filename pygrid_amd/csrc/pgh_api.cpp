@@ -507,10 +507,6 @@ int d2h_ring_begin(pgh_ctx* c, pgh_ctx::D2HRing* r, const uint8_t* src, size_t t
         r->cells = c->d2h_cap / r->piece;
         r->per_slot = r->cells;
         r->s = c->d2h;
-        if (c->d2h_mode >= 2 && c->d2h_probe) {  // what the copy stream holds now: H2D a piece must not queue behind
-            CK(c, hipEventRecord(c->d2h_probe, c->copy));
-            r->probe = true;
-        }
         while (c->d2h_ev.size() < std::min(r->cells, r->n_pieces)) {
             hipEvent_t e = nullptr;
             CK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -582,18 +578,7 @@ static int d2h_piece_ready(pgh_ctx* c, const pgh_ctx::D2HRing& r, size_t j, bool
 
 static int d2h_issue(pgh_ctx* c, pgh_ctx::D2HRing* r) {
     const size_t j = r->queued, off = j * r->piece, len = std::min(r->piece, r->total - off);
-    if (r->probe && c->d2h_mode == 2) {  // H2D issued before the ring still running: K6 beside it, not SDMA after it
-        const hipError_t q = hipEventQuery(c->d2h_probe);
-        if (q == hipSuccess) r->probe = false;
-        else if (q != hipErrorNotReady) CK(c, q);
-    }
-    if (r->probe) {
-        const hipError_t e = pgh::launch_copy_to_host(d2h_cell(c, *r, j), r->src + off, len, D2H_KERNEL_WGS, r->s);
-        if (e != hipSuccess) return fail(c, PGH_E_HIP, "D2H copy kernel launch failed: %s", hipGetErrorString(e));
-        c->st.d2h_kernel_bytes_total += len;
-    } else {
-        CK(c, hipMemcpyAsync(d2h_cell(c, *r, j), r->src + off, len, hipMemcpyDeviceToHost, r->s));
-    }
+    CK(c, hipMemcpyAsync(d2h_cell(c, *r, j), r->src + off, len, hipMemcpyDeviceToHost, r->s));
     c->st.d2h_bytes_total += len;
     CK(c, hipEventRecord(c->d2h_ev[j % r->cells], r->s));
     ++r->queued;
@@ -1203,7 +1188,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
     if (const char* e = std::getenv("PGH_PINNED_GATHER")) c->pinned_gather = std::atoi(e) != 0;
     if (const char* e = std::getenv("PGH_BLOCK_BYTES")) c->block_bytes = (size_t)std::max(0LL, std::atoll(e));
     if (const char* e = std::getenv("PGH_FINAL_RANGES")) c->final_split = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("PGH_D2H_STREAM")) c->d2h_mode = std::max(0, std::min(3, std::atoi(e)));
+    if (const char* e = std::getenv("PGH_D2H_STREAM")) c->d2h_mode = std::max(0, std::min(1, std::atoi(e)));
     c->own_d2h = c->d2h_mode > 0;
     bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess &&
@@ -1213,8 +1198,7 @@ int pgh_create(int device, size_t pinned_bytes, pgh_ctx** out) {
               hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->pin_ev[0], hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&c->pin_ev[1], hipEventDisableTiming) == hipSuccess &&
-              (!c->own_d2h || (hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) == hipSuccess &&
-                               hipEventCreateWithFlags(&c->d2h_probe, hipEventDisableTiming) == hipSuccess));
+              (!c->own_d2h || hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) == hipSuccess);
     if (!ok) { pgh_destroy(c); return fail(nullptr, PGH_E_HIP, "stream/event creation failed"); }
     {
         // the pinned ring on the GPU's socket: allocated by a thread bound there, pages placed by
@@ -1308,7 +1292,6 @@ void pgh_destroy(pgh_ctx* c) {
     if (c->d2h) (void)hipStreamSynchronize(c->d2h);
     if (c->h_d2h) (void)hipHostFree(c->h_d2h);
     if (c->d2h) (void)hipStreamDestroy(c->d2h);
-    if (c->d2h_probe) (void)hipEventDestroy(c->d2h_probe);
     for (hipEvent_t e : {c->copy_done, c->xsync, c->aux_ev})
         if (e) (void)hipEventDestroy(e);
     for (auto e : c->fold_ev_pool) (void)hipEventDestroy(e);

@@ -31,7 +31,6 @@
 #include "../../include/pgh_api.h"
 #include "pgh_internal.h"
 #include "pgh_kernels.h"
-#include "pgh_copy.h"
 #include "pgh_state.h"
 
 namespace pgh_detail {
@@ -247,7 +246,6 @@ struct pgh_ctx {
         hipStream_t s = nullptr;
         bool piped = false;
         uint8_t* base = nullptr;  // the cells of a piped ring: h_d2h (own_d2h), else the free pinned slots
-        bool probe = false;       // d2h_probe marks the copy stream's work at ring start (d2h_mode 2)
     };
     // The new checkpoint's D2H as the FINAL pass of a report-time close starts it: the pieces whose
     // ranges finished while the later ranges were still being issued (pgh_slots.cpp); the patch /
@@ -258,15 +256,12 @@ struct pgh_ctx {
     // A piped ring's pieces on a stream and in page-locked cells of their own (PGH_D2H_STREAM,
     // default 1): on the copy stream they queued behind the last reports' H2D, and they waited for
     // a staging slot those reports still held -- with reports back to back, until every report had
-    // landed.  PCIe is full duplex: the new checkpoint's pieces run beside that H2D.  The stream is
-    // primed with a small H2D when made, so the runtime sends its D2H to an SDMA engine (r05ae).
-    // PGH_D2H_STREAM=2 (the default) also sends a piece that is issued while the copy stream still
-    // holds H2D issued before the ring started (reports back to back) through K6 k_copy_to_host:
-    // SDMA runs host <-> HBM copies of both directions one after another on one engine, the CUs'
-    // stores reach the host beside it (r06e/, r06g/).  3: every piece of a piped ring by K6 (tests).
+    // landed.  The stream is primed with a small H2D when made, so the runtime sends its D2H to an
+    // SDMA engine (r05ae).  (Rounds 6's K6 k_copy_to_host, pieces copied out by a kernel beside an H2D
+    // backlog, was removed: copying a piece right behind the FINAL ranges that wrote it on another
+    // stream, it read ranges that had not run yet -- profiles/r06s/.)
     bool own_d2h = true;
-    int d2h_mode = 2;
-    hipEvent_t d2h_probe = nullptr;
+    int d2h_mode = 1;
     hipStream_t d2h = nullptr;
     uint8_t* h_d2h = nullptr;
     size_t d2h_cap = 0;
@@ -449,7 +444,6 @@ struct OutPiece {
 // with the parallel pre-fault, r01ak, 8 MiB pieces closed in 2.3-2.4 ms vs 2.6-2.7 for one piece).
 constexpr size_t D2H_PIECE = 8u << 20;
 constexpr size_t D2H_OWN_CELLS = 8;  // a piped ring's own cells: 64 MiB at most (ResNet-18: 6 pieces)
-constexpr int D2H_KERNEL_WGS = 64;    // K6's grid: PCIe bounds it, the fold keeps the other CUs
 // Ranged report ingest (pgh_set_ingest_ranges): one chunk = the params of one D2H piece = two
 // 4 MiB FINAL ranges of a report-time close (pgh_slots.cpp).
 constexpr int64_t INGEST_CHUNK = (int64_t)(D2H_PIECE / 4);
